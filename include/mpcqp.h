@@ -1,0 +1,145 @@
+/*
+ * mpcqp.h -- C ABI of the MI355X batched linear-MPC QP solver (libmpcqp.so).
+ *
+ * Drop-in boundary for the reference's `osqp.OSQP()` call sites.  Each entry
+ * point below replaces one step of the reference's OSQP usage:
+ *
+ *   mpcqp_setup_batch     <- prob = osqp.OSQP(); prob.setup(P, q, A, l, u, **settings)
+ *                            vehicle_lateral_mpc_slack_increment.py:118,121
+ *                            Control/MPC/mpc_kinematics.py:194-195
+ *                            Control/MPC/mpc_dynamics.py:240-241,392-393
+ *                            Control/MPC/mpc_kinematics_pred_matrix.py:195-196,260-261,346-347
+ *                            Control/MPC/mpc_increment_kinematics_pred_matrix.py:241-242
+ *                            Control/MPC/mpc_bottleneck_check.py:197-198
+ *                            Control/MPC/mpc_incre_kine_func.py:179-180
+ *   mpcqp_update_batch    <- prob.update(q=q_new, l=l_new, u=u_new)
+ *                            vehicle_lateral_mpc_slack_increment.py:237,269
+ *   mpcqp_warm_start_batch<- prob.warm_start(x=..., y=...)   (osqp API; used for
+ *                            the receding-horizon shift)
+ *   mpcqp_solve_batch     <- res = prob.solve(); res.x, res.y, res.info.status, res.info.iter
+ *                            vehicle_lateral_mpc_slack_increment.py:248,252,256
+ *                            Control/MPC/mpc_dynamics.py:396,406-407
+ *   mpcqp_free            <- end of the OSQP object's lifetime
+ *
+ * One handle holds B independent QP instances that SHARE one sparsity pattern
+ * (P upper-triangular CSC n x n, A CSC m x n, int32, 0-based) and carry their
+ * own values.  Per-instance arrays are instance-major:  Px[B*nnzP], Ax[B*nnzA],
+ * q[B*n], l[B*m], u[B*m], x[B*n], y[B*m].  Values follow the order of the
+ * pattern's data arrays (osqp-python keeps triu(P) in CSC order).
+ *
+ * Ownership: every input is copied into device memory during the call; the
+ * caller may free or reuse its buffers afterwards.  Outputs go to
+ * caller-allocated buffers.  Host-pointer entry points block until results
+ * are on the host; *_device entry points take device pointers on the
+ * handle's (single) device and enqueue on `stream` (hipStream_t, NULL = the
+ * handle's own stream) without synchronising.
+ *
+ * Errors: entry points return 0 on success or an MPCQP_E* code; the message
+ * is in mpcqp_last_error() (thread-local).  Numerical outcomes never fail a
+ * call: they are reported per instance in status[] with OSQP's values.
+ * A handle must be used from one host thread at a time.
+ */
+#ifndef MPCQP_H
+#define MPCQP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* per-instance status (same values as OSQP's constants.h) */
+#define MPCQP_DUAL_INFEASIBLE_INACCURATE 4
+#define MPCQP_PRIMAL_INFEASIBLE_INACCURATE 3
+#define MPCQP_SOLVED_INACCURATE 2
+#define MPCQP_SOLVED 1
+#define MPCQP_MAX_ITER_REACHED (-2)
+#define MPCQP_PRIMAL_INFEASIBLE (-3)
+#define MPCQP_DUAL_INFEASIBLE (-4)
+#define MPCQP_NON_CVX (-7)
+#define MPCQP_UNSOLVED (-10)
+
+/* call error codes */
+#define MPCQP_OK 0
+#define MPCQP_EINVAL 1        /* bad argument / data validation (e.g. l > u) */
+#define MPCQP_EUNSUPPORTED 2  /* sparsity structure or setting not supported */
+#define MPCQP_EDEVICE 3       /* HIP runtime error / no device */
+#define MPCQP_ENOMEM 4
+
+typedef struct {
+    double rho, sigma, alpha;
+    double eps_abs, eps_rel, eps_prim_inf, eps_dual_inf;
+    double adaptive_rho_tolerance;
+    int32_t max_iter, scaling, check_termination, warm_start;
+    int32_t adaptive_rho, adaptive_rho_interval, scaled_termination, polish, verbose;
+} mpcqp_settings;
+
+typedef struct {
+    int32_t n, m, nb, block, npad, max_level;
+    int64_t batch;
+    int32_t n_devices;
+    int64_t lds_bytes_solve;    /* dynamic LDS per workgroup of the ADMM kernel */
+    int64_t bytes_per_instance; /* device workspace per instance */
+} mpcqp_plan_info;
+
+typedef struct mpcqp_handle mpcqp_handle;
+
+/* OSQP 0.6 defaults; adaptive_rho_interval = 0 resolves to 4*check_termination
+ * (OSQP's non-profiling rule, pinned). */
+void mpcqp_default_settings(mpcqp_settings *s);
+
+/* Symbolic analysis + allocation + per-instance setup (scaling, rho classes).
+ * device_mask: bit d selects HIP device d; 0 = device 0.  The batch is split
+ * into contiguous shards across the selected devices (no collectives). */
+int mpcqp_setup_batch(int32_t n, int32_t m,
+                      const int32_t *Pp, const int32_t *Pi,
+                      const int32_t *Ap, const int32_t *Ai,
+                      int64_t B, const double *Px, const double *Ax,
+                      const double *q, const double *l, const double *u,
+                      const mpcqp_settings *settings, uint32_t device_mask,
+                      mpcqp_handle **out);
+
+/* q, l, u may each be NULL (not updated). */
+int mpcqp_update_batch(mpcqp_handle *h, const double *q, const double *l, const double *u);
+/* x, y may each be NULL (keeps the current iterate of that part). */
+int mpcqp_warm_start_batch(mpcqp_handle *h, const double *x, const double *y);
+/* any output may be NULL */
+int mpcqp_solve_batch(mpcqp_handle *h, double *x, double *y, int32_t *status, int32_t *iters);
+/* info of the last solve; any output may be NULL */
+int mpcqp_get_info_batch(mpcqp_handle *h, double *obj_val, double *pri_res, double *dua_res,
+                         double *rho_estimate, int32_t *rho_updates);
+/* infeasibility certificates of the last solve (OSQP res.prim_inf_cert / dua_inf_cert) */
+int mpcqp_get_certificates(mpcqp_handle *h, double *prim_inf_cert, double *dual_inf_cert);
+
+/* ---- device-resident entry points (single-device handles) ---- */
+/* Allocate a handle with its workspace but no data (pattern only). */
+int mpcqp_create(int32_t n, int32_t m, const int32_t *Pp, const int32_t *Pi,
+                 const int32_t *Ap, const int32_t *Ai, int64_t B,
+                 const mpcqp_settings *settings, int32_t device, mpcqp_handle **out);
+int mpcqp_setup_device(mpcqp_handle *h, const double *dPx, const double *dAx, const double *dq,
+                       const double *dl, const double *du, void *stream);
+int mpcqp_update_device(mpcqp_handle *h, const double *dq, const double *dl, const double *du,
+                        void *stream);
+int mpcqp_warm_start_device(mpcqp_handle *h, const double *dx, const double *dy, void *stream);
+int mpcqp_solve_device(mpcqp_handle *h, double *dx, double *dy, int32_t *dstatus, int32_t *diters,
+                       void *stream);
+int mpcqp_synchronize(mpcqp_handle *h);
+/* hipEvent-bracketed timing of the ADMM kernel launches of the last *_device
+ * solve on the handle's stream: milliseconds, or -1 when unavailable. */
+double mpcqp_last_kernel_ms(mpcqp_handle *h);
+
+int mpcqp_get_plan_info(const mpcqp_handle *h, mpcqp_plan_info *info);
+void mpcqp_free(mpcqp_handle *h);
+const char *mpcqp_last_error(void);
+
+/* Host-only symbolic analysis (no device needed): block-tridiagonal plan of
+ * K = P + sigma I + A' diag(rho) A.  var_pad[n] receives each variable's padded
+ * index, bsize[*nb] the block sizes (capacity n).  Used by the CPU test-suite. */
+int mpcqp_analyze(int32_t n, int32_t m, const int32_t *Pp, const int32_t *Pi,
+                  const int32_t *Ap, const int32_t *Ai, int32_t *nb, int32_t *block,
+                  int32_t *var_pad, int32_t *bsize);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPCQP_H */

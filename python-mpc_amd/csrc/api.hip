@@ -1,0 +1,496 @@
+// api.hip -- C ABI of libmpcqp.so (declared in include/mpcqp.h).
+//
+// Host side of the drop-in boundary for `osqp.OSQP().setup()/update()/solve()`
+// (vehicle_lateral_mpc_slack_increment.py:118-121,237,248,269;
+// Control/MPC/mpc_dynamics.py:392-396).  The host only performs the symbolic
+// analysis of the shared sparsity pattern (plan.cpp), memory management and
+// kernel launches; every per-instance number is computed by the HIP kernels in
+// kernels.hip.  There is no CPU fallback: without a HIP device every entry
+// point that needs one returns MPCQP_EDEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/mpcqp.h"
+#include "kernels.h"
+#include "plan.h"
+
+using namespace mpcqp;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                        \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return fail(MPCQP_EDEVICE, "%s failed: %s", #expr, hipGetErrorString(e_));      \
+    } while (0)
+
+struct Shard {
+    int dev = 0;
+    long b0 = 0, B = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int* dplan = nullptr;
+    void* dws = nullptr;    // one allocation for the whole workspace
+    void* dio = nullptr;    // staging for the host-pointer API
+    double *in_Px = nullptr, *in_Ax = nullptr, *in_q = nullptr, *in_l = nullptr, *in_u = nullptr;
+    double *out_x = nullptr, *out_y = nullptr;
+    KParams kp{};
+};
+
+}  // namespace
+
+struct mpcqp_handle {
+    Plan plan;
+    mpcqp_settings set{};
+    int n = 0, m = 0;
+    long B = 0;
+    std::vector<Shard> shards;
+    bool timed = false;
+    double last_ms = -1.0;
+};
+
+namespace {
+
+template <class T>
+size_t carve(size_t& off, size_t count) {
+    off = (off + 255) & ~(size_t)255;
+    size_t o = off;
+    off += count * sizeof(T);
+    return o;
+}
+
+int upload_plan(const Plan& pl, Shard& s) {
+    std::vector<const std::vector<int>*> parts = {
+        &pl.pad_var, &pl.acsc_ptr, &pl.acsc_row, &pl.acsc_v, &pl.acsr_ptr, &pl.acsr_col, &pl.acsr_v,
+        &pl.psym_ptr, &pl.psym_col, &pl.psym_v, &pl.p_r, &pl.p_c, &pl.a_r, &pl.a_c,
+        &pl.asm_blk_ptr, &pl.asm_tgt, &pl.asm_term_ptr, &pl.term_a, &pl.term_b, &pl.term_r};
+    std::vector<size_t> offs;
+    std::vector<int> flat;
+    for (auto* v : parts) {
+        offs.push_back(flat.size());
+        flat.insert(flat.end(), v->begin(), v->end());
+        flat.push_back(0);  // never allocate zero-length parts
+    }
+    HIPCHK(hipMalloc(&s.dplan, flat.size() * sizeof(int)));
+    HIPCHK(hipMemcpy(s.dplan, flat.data(), flat.size() * sizeof(int), hipMemcpyHostToDevice));
+    const int** dst[] = {&s.kp.pad_var, &s.kp.acsc_ptr, &s.kp.acsc_row, &s.kp.acsc_v, &s.kp.acsr_ptr,
+                         &s.kp.acsr_col, &s.kp.acsr_v, &s.kp.psym_ptr, &s.kp.psym_col, &s.kp.psym_v,
+                         &s.kp.p_r, &s.kp.p_c, &s.kp.a_r, &s.kp.a_c, &s.kp.asm_blk_ptr, &s.kp.asm_tgt,
+                         &s.kp.asm_term_ptr, &s.kp.term_a, &s.kp.term_b, &s.kp.term_r};
+    for (size_t i = 0; i < parts.size(); ++i) *dst[i] = s.dplan + offs[i];
+    return 0;
+}
+
+size_t workspace_bytes(const Plan& pl, long B, bool with_io) {
+    size_t off = 0;
+    const long n = pl.n, m = pl.m, np = pl.npad, nb = pl.nb;
+    const long SS = (long)kS * kS;
+    carve<double>(off, B * pl.nnzP); carve<double>(off, B * pl.nnzA);
+    carve<double>(off, B * np); carve<double>(off, B * np);            // q, D
+    carve<double>(off, B * m); carve<double>(off, B * m); carve<double>(off, B * m);  // l u E
+    carve<double>(off, B * np); carve<double>(off, B * m); carve<double>(off, B * m); // x z y
+    carve<double>(off, B * 4);
+    carve<double>(off, B * nb * SS); carve<double>(off, B * nb * SS); carve<double>(off, B * nb * SS);
+    carve<double>(off, B * m); carve<double>(off, B * n);              // certificates
+    for (int i = 0; i < 4; ++i) carve<double>(off, B);
+    carve<signed char>(off, B * m);
+    for (int i = 0; i < 4; ++i) carve<int>(off, B);
+    if (with_io) {
+        carve<double>(off, B * pl.nnzP); carve<double>(off, B * pl.nnzA);
+        carve<double>(off, B * n); carve<double>(off, B * m); carve<double>(off, B * m);
+        carve<double>(off, B * n); carve<double>(off, B * m);
+    }
+    return off + 256;
+}
+
+int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
+    const Plan& pl = h->plan;
+    HIPCHK(hipSetDevice(s.dev));
+    HIPCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreate(&s.ev0));
+    HIPCHK(hipEventCreate(&s.ev1));
+    if (int e = upload_plan(pl, s)) return e;
+    const long B = s.B, n = pl.n, m = pl.m, np = pl.npad, nb = pl.nb;
+    const long SS = (long)kS * kS;
+    size_t total = workspace_bytes(pl, B, with_io);
+    hipError_t e = hipMalloc(&s.dws, total);
+    if (e != hipSuccess)
+        return fail(MPCQP_ENOMEM, "hipMalloc(%zu bytes) failed: %s", total, hipGetErrorString(e));
+    HIPCHK(hipMemset(s.dws, 0, total));
+    char* base = (char*)s.dws;
+    size_t off = 0;
+    KParams& k = s.kp;
+    k.Px = (double*)(base + carve<double>(off, B * pl.nnzP));
+    k.Ax = (double*)(base + carve<double>(off, B * pl.nnzA));
+    k.q = (double*)(base + carve<double>(off, B * np));
+    k.D = (double*)(base + carve<double>(off, B * np));
+    k.l = (double*)(base + carve<double>(off, B * m));
+    k.u = (double*)(base + carve<double>(off, B * m));
+    k.E = (double*)(base + carve<double>(off, B * m));
+    k.x = (double*)(base + carve<double>(off, B * np));
+    k.z = (double*)(base + carve<double>(off, B * m));
+    k.y = (double*)(base + carve<double>(off, B * m));
+    k.scal = (double*)(base + carve<double>(off, B * 4));
+    k.F = (double*)(base + carve<double>(off, B * nb * SS));
+    k.H = (double*)(base + carve<double>(off, B * nb * SS));
+    k.Si = (double*)(base + carve<double>(off, B * nb * SS));
+    k.dyc = (double*)(base + carve<double>(off, B * m));
+    k.dxc = (double*)(base + carve<double>(off, B * n));
+    k.obj = (double*)(base + carve<double>(off, B));
+    k.pri = (double*)(base + carve<double>(off, B));
+    k.dua = (double*)(base + carve<double>(off, B));
+    k.rho_est = (double*)(base + carve<double>(off, B));
+    k.ct = (signed char*)(base + carve<signed char>(off, B * m));
+    k.status = (int*)(base + carve<int>(off, B));
+    k.iter = (int*)(base + carve<int>(off, B));
+    k.rho_upd = (int*)(base + carve<int>(off, B));
+    k.err = (int*)(base + carve<int>(off, B));
+    if (with_io) {
+        s.in_Px = (double*)(base + carve<double>(off, B * pl.nnzP));
+        s.in_Ax = (double*)(base + carve<double>(off, B * pl.nnzA));
+        s.in_q = (double*)(base + carve<double>(off, B * n));
+        s.in_l = (double*)(base + carve<double>(off, B * m));
+        s.in_u = (double*)(base + carve<double>(off, B * m));
+        s.out_x = (double*)(base + carve<double>(off, B * n));
+        s.out_y = (double*)(base + carve<double>(off, B * m));
+    }
+    k.n = pl.n; k.m = pl.m; k.nb = pl.nb; k.npad = pl.npad; k.nnzP = pl.nnzP; k.nnzA = pl.nnzA;
+    const mpcqp_settings& st = h->set;
+    k.sigma = st.sigma; k.alpha = st.alpha; k.eps_abs = st.eps_abs; k.eps_rel = st.eps_rel;
+    k.eps_pinf = st.eps_prim_inf; k.eps_dinf = st.eps_dual_inf; k.rho0 = st.rho;
+    k.rho_tol = st.adaptive_rho_tolerance;
+    k.max_iter = st.max_iter; k.scaling = st.scaling; k.check_term = st.check_termination;
+    k.warm_start = st.warm_start; k.adaptive_rho = st.adaptive_rho; k.scaled_term = st.scaled_termination;
+    int interval = st.adaptive_rho_interval;
+    if (st.adaptive_rho && interval == 0) interval = st.check_termination ? 4 * st.check_termination : 100;
+    k.rho_interval = interval;
+    if (size_t lds = lds_solve_bytes(k); lds > 160 * 1024)
+        return fail(MPCQP_EUNSUPPORTED, "problem needs %zu bytes of LDS per instance (> 160 KiB)", lds);
+    return 0;
+}
+
+int validate_settings(const mpcqp_settings& s) {
+    if (!(s.rho > 0) || !(s.sigma > 0) || s.max_iter <= 0 || s.eps_abs < 0 || s.eps_rel < 0 ||
+        (s.eps_abs == 0 && s.eps_rel == 0) || !(s.eps_prim_inf > 0) || !(s.eps_dual_inf > 0) ||
+        !(s.alpha > 0 && s.alpha < 2) || s.scaling < 0 || s.check_termination < 0 ||
+        s.adaptive_rho_interval < 0 || !(s.adaptive_rho_tolerance >= 1))
+        return fail(MPCQP_EINVAL, "invalid settings");
+    if (s.polish) return fail(MPCQP_EUNSUPPORTED, "polish is not supported (the reference never enables it)");
+    return 0;
+}
+
+int make_handle(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
+                const int32_t* Ai, int64_t B, const mpcqp_settings* settings, std::vector<int> devs,
+                bool with_io, mpcqp_handle** out) {
+    if (!out) return fail(MPCQP_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (B <= 0) return fail(MPCQP_EINVAL, "batch must be positive");
+    if (!Pp || !Pi || !Ap || !Ai) return fail(MPCQP_EINVAL, "NULL pattern array");
+    auto h = std::make_unique<mpcqp_handle>();
+    if (settings) h->set = *settings;
+    else mpcqp_default_settings(&h->set);
+    if (int e = validate_settings(h->set)) return e;
+    std::string err = build_plan(n, m, Pp, Pi, Ap, Ai, h->plan);
+    if (!err.empty()) {
+        bool unsup = err.rfind("unsupported", 0) == 0;
+        return fail(unsup ? MPCQP_EUNSUPPORTED : MPCQP_EINVAL, "%s", err.c_str());
+    }
+    h->n = n; h->m = m; h->B = B;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(MPCQP_EDEVICE, "no HIP device available (the solver has no CPU fallback)");
+    for (int d : devs)
+        if (d < 0 || d >= ndev) return fail(MPCQP_EDEVICE, "device %d not present (%d devices)", d, ndev);
+    const long nd = (long)devs.size();
+    for (long i = 0; i < nd; ++i) {
+        Shard s;
+        s.dev = devs[i];
+        s.b0 = B * i / nd;
+        s.B = B * (i + 1) / nd - s.b0;
+        if (s.B <= 0) continue;
+        h->shards.push_back(s);
+    }
+    for (auto& s : h->shards)
+        if (int e = alloc_shard(h.get(), s, with_io)) { mpcqp_free(h.release()); return e; }
+    *out = h.release();
+    return 0;
+}
+
+int check_bounds_host(const mpcqp_handle* h, const double* l, const double* u, long B) {
+    if (!l || !u) return 0;
+    const long m = h->m;
+    for (long i = 0; i < B * m; ++i) {
+        double li = std::max(l[i], -1e30), ui = std::min(u[i], 1e30);
+        if (!(li <= ui))
+            return fail(MPCQP_EINVAL, "instance %ld row %ld: lower bound must be lower than or equal to upper bound",
+                        i / m, i % m);
+    }
+    return 0;
+}
+
+int sync_all(mpcqp_handle* h) {
+    for (auto& s : h->shards) {
+        HIPCHK(hipSetDevice(s.dev));
+        HIPCHK(hipStreamSynchronize(s.stream));
+    }
+    return 0;
+}
+
+int check_err_flags(mpcqp_handle* h) {
+    for (auto& s : h->shards) {
+        std::vector<int> err(s.B);
+        HIPCHK(hipSetDevice(s.dev));
+        HIPCHK(hipMemcpy(err.data(), s.kp.err, sizeof(int) * s.B, hipMemcpyDeviceToHost));
+        for (long i = 0; i < s.B; ++i)
+            if (err[i]) return fail(MPCQP_EINVAL, "instance %ld: invalid data (l > u or NaN bounds)", s.b0 + i);
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+void mpcqp_default_settings(mpcqp_settings* s) {
+    s->rho = 0.1; s->sigma = 1e-6; s->alpha = 1.6;
+    s->eps_abs = 1e-3; s->eps_rel = 1e-3; s->eps_prim_inf = 1e-4; s->eps_dual_inf = 1e-4;
+    s->adaptive_rho_tolerance = 5.0;
+    s->max_iter = 4000; s->scaling = 10; s->check_termination = 25; s->warm_start = 1;
+    s->adaptive_rho = 1; s->adaptive_rho_interval = 0; s->scaled_termination = 0; s->polish = 0;
+    s->verbose = 0;
+}
+
+const char* mpcqp_last_error(void) { return g_err.c_str(); }
+
+int mpcqp_analyze(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
+                  const int32_t* Ai, int32_t* nb, int32_t* block, int32_t* var_pad, int32_t* bsize) {
+    Plan pl;
+    std::string err = build_plan(n, m, Pp, Pi, Ap, Ai, pl);
+    if (!err.empty()) return fail(err.rfind("unsupported", 0) == 0 ? MPCQP_EUNSUPPORTED : MPCQP_EINVAL, "%s", err.c_str());
+    if (nb) *nb = pl.nb;
+    if (block) *block = kS;
+    if (var_pad) std::copy(pl.var_pad.begin(), pl.var_pad.end(), var_pad);
+    if (bsize) std::copy(pl.bsize.begin(), pl.bsize.end(), bsize);
+    return 0;
+}
+
+int mpcqp_setup_batch(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
+                      const int32_t* Ai, int64_t B, const double* Px, const double* Ax, const double* q,
+                      const double* l, const double* u, const mpcqp_settings* settings,
+                      uint32_t device_mask, mpcqp_handle** out) {
+    if (!Px || !Ax || !q || !l || !u) return fail(MPCQP_EINVAL, "NULL data array");
+    std::vector<int> devs;
+    for (int d = 0; d < 32; ++d)
+        if (device_mask & (1u << d)) devs.push_back(d);
+    if (devs.empty()) devs.push_back(0);
+    mpcqp_handle* h = nullptr;
+    if (int e = make_handle(n, m, Pp, Pi, Ap, Ai, B, settings, devs, true, &h)) return e;
+    if (int e = check_bounds_host(h, l, u, B)) { mpcqp_free(h); return e; }
+    const Plan& pl = h->plan;
+    auto upload = [&](Shard& s) -> int {
+        const long b0 = s.b0, Bs = s.B;
+        HIPCHK(hipSetDevice(s.dev));
+        HIPCHK(hipMemcpyAsync(s.in_Px, Px + b0 * pl.nnzP, sizeof(double) * Bs * pl.nnzP, hipMemcpyHostToDevice, s.stream));
+        HIPCHK(hipMemcpyAsync(s.in_Ax, Ax + b0 * pl.nnzA, sizeof(double) * Bs * pl.nnzA, hipMemcpyHostToDevice, s.stream));
+        HIPCHK(hipMemcpyAsync(s.in_q, q + b0 * n, sizeof(double) * Bs * n, hipMemcpyHostToDevice, s.stream));
+        HIPCHK(hipMemcpyAsync(s.in_l, l + b0 * m, sizeof(double) * Bs * m, hipMemcpyHostToDevice, s.stream));
+        HIPCHK(hipMemcpyAsync(s.in_u, u + b0 * m, sizeof(double) * Bs * m, hipMemcpyHostToDevice, s.stream));
+        HIPCHK(launch_setup(s.kp, Bs, s.in_Px, s.in_Ax, s.in_q, s.in_l, s.in_u, s.stream));
+        return 0;
+    };
+    for (auto& s : h->shards)
+        if (int e = upload(s)) { mpcqp_free(h); return e; }
+    if (int e = sync_all(h)) { mpcqp_free(h); return e; }
+    if (int e = check_err_flags(h)) { mpcqp_free(h); return e; }
+    *out = h;
+    return 0;
+}
+
+int mpcqp_update_batch(mpcqp_handle* h, const double* q, const double* l, const double* u) {
+    if (!h) return fail(MPCQP_EINVAL, "NULL handle");
+    if (l && u)
+        if (int e = check_bounds_host(h, l, u, h->B)) return e;
+    const long n = h->n, m = h->m;
+    for (auto& s : h->shards) {
+        HIPCHK(hipSetDevice(s.dev));
+        if (q) HIPCHK(hipMemcpyAsync(s.in_q, q + s.b0 * n, sizeof(double) * s.B * n, hipMemcpyHostToDevice, s.stream));
+        if (l) HIPCHK(hipMemcpyAsync(s.in_l, l + s.b0 * m, sizeof(double) * s.B * m, hipMemcpyHostToDevice, s.stream));
+        if (u) HIPCHK(hipMemcpyAsync(s.in_u, u + s.b0 * m, sizeof(double) * s.B * m, hipMemcpyHostToDevice, s.stream));
+        HIPCHK(launch_update(s.kp, s.B, q ? s.in_q : nullptr, l ? s.in_l : nullptr, u ? s.in_u : nullptr, s.stream));
+    }
+    if (int e = sync_all(h)) return e;
+    if (l || u) return check_err_flags(h);
+    return 0;
+}
+
+int mpcqp_warm_start_batch(mpcqp_handle* h, const double* x, const double* y) {
+    if (!h) return fail(MPCQP_EINVAL, "NULL handle");
+    const long n = h->n, m = h->m;
+    for (auto& s : h->shards) {
+        HIPCHK(hipSetDevice(s.dev));
+        if (x) HIPCHK(hipMemcpyAsync(s.out_x, x + s.b0 * n, sizeof(double) * s.B * n, hipMemcpyHostToDevice, s.stream));
+        if (y) HIPCHK(hipMemcpyAsync(s.out_y, y + s.b0 * m, sizeof(double) * s.B * m, hipMemcpyHostToDevice, s.stream));
+        HIPCHK(launch_warm(s.kp, s.B, x ? s.out_x : nullptr, y ? s.out_y : nullptr, s.stream));
+        s.kp.warm_start = 1;
+    }
+    h->set.warm_start = 1;
+    return sync_all(h);
+}
+
+int mpcqp_solve_batch(mpcqp_handle* h, double* x, double* y, int32_t* status, int32_t* iters) {
+    if (!h) return fail(MPCQP_EINVAL, "NULL handle");
+    const long n = h->n, m = h->m;
+    for (auto& s : h->shards) {
+        HIPCHK(hipSetDevice(s.dev));
+        HIPCHK(hipEventRecord(s.ev0, s.stream));
+        HIPCHK(launch_solve(s.kp, s.B, s.out_x, s.out_y, 0, s.stream));
+        HIPCHK(hipEventRecord(s.ev1, s.stream));
+        if (x) HIPCHK(hipMemcpyAsync(x + s.b0 * n, s.out_x, sizeof(double) * s.B * n, hipMemcpyDeviceToHost, s.stream));
+        if (y) HIPCHK(hipMemcpyAsync(y + s.b0 * m, s.out_y, sizeof(double) * s.B * m, hipMemcpyDeviceToHost, s.stream));
+        if (status) HIPCHK(hipMemcpyAsync(status + s.b0, s.kp.status, sizeof(int) * s.B, hipMemcpyDeviceToHost, s.stream));
+        if (iters) HIPCHK(hipMemcpyAsync(iters + s.b0, s.kp.iter, sizeof(int) * s.B, hipMemcpyDeviceToHost, s.stream));
+    }
+    if (int e = sync_all(h)) return e;
+    float ms = 0.f;
+    h->last_ms = -1.0;
+    if (h->shards.size() == 1 && hipEventElapsedTime(&ms, h->shards[0].ev0, h->shards[0].ev1) == hipSuccess)
+        h->last_ms = ms;
+    return 0;
+}
+
+int mpcqp_get_info_batch(mpcqp_handle* h, double* obj_val, double* pri_res, double* dua_res,
+                         double* rho_estimate, int32_t* rho_updates) {
+    if (!h) return fail(MPCQP_EINVAL, "NULL handle");
+    for (auto& s : h->shards) {
+        HIPCHK(hipSetDevice(s.dev));
+        if (obj_val) HIPCHK(hipMemcpy(obj_val + s.b0, s.kp.obj, sizeof(double) * s.B, hipMemcpyDeviceToHost));
+        if (pri_res) HIPCHK(hipMemcpy(pri_res + s.b0, s.kp.pri, sizeof(double) * s.B, hipMemcpyDeviceToHost));
+        if (dua_res) HIPCHK(hipMemcpy(dua_res + s.b0, s.kp.dua, sizeof(double) * s.B, hipMemcpyDeviceToHost));
+        if (rho_estimate) HIPCHK(hipMemcpy(rho_estimate + s.b0, s.kp.rho_est, sizeof(double) * s.B, hipMemcpyDeviceToHost));
+        if (rho_updates) HIPCHK(hipMemcpy(rho_updates + s.b0, s.kp.rho_upd, sizeof(int) * s.B, hipMemcpyDeviceToHost));
+    }
+    return 0;
+}
+
+int mpcqp_get_certificates(mpcqp_handle* h, double* prim_inf_cert, double* dual_inf_cert) {
+    if (!h) return fail(MPCQP_EINVAL, "NULL handle");
+    for (auto& s : h->shards) {
+        HIPCHK(hipSetDevice(s.dev));
+        if (prim_inf_cert)
+            HIPCHK(hipMemcpy(prim_inf_cert + s.b0 * h->m, s.kp.dyc, sizeof(double) * s.B * h->m, hipMemcpyDeviceToHost));
+        if (dual_inf_cert)
+            HIPCHK(hipMemcpy(dual_inf_cert + s.b0 * h->n, s.kp.dxc, sizeof(double) * s.B * h->n, hipMemcpyDeviceToHost));
+    }
+    return 0;
+}
+
+int mpcqp_create(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
+                 const int32_t* Ai, int64_t B, const mpcqp_settings* settings, int32_t device,
+                 mpcqp_handle** out) {
+    return make_handle(n, m, Pp, Pi, Ap, Ai, B, settings, std::vector<int>{device}, false, out);
+}
+
+static hipStream_t pick(Shard& s, void* stream) { return stream ? (hipStream_t)stream : s.stream; }
+
+int mpcqp_setup_device(mpcqp_handle* h, const double* dPx, const double* dAx, const double* dq,
+                       const double* dl, const double* du, void* stream) {
+    if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "device entry points need a single-device handle");
+    Shard& s = h->shards[0];
+    HIPCHK(hipSetDevice(s.dev));
+    HIPCHK(launch_setup(s.kp, s.B, dPx, dAx, dq, dl, du, pick(s, stream)));
+    return 0;
+}
+
+int mpcqp_update_device(mpcqp_handle* h, const double* dq, const double* dl, const double* du, void* stream) {
+    if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "device entry points need a single-device handle");
+    Shard& s = h->shards[0];
+    HIPCHK(hipSetDevice(s.dev));
+    HIPCHK(launch_update(s.kp, s.B, dq, dl, du, pick(s, stream)));
+    return 0;
+}
+
+int mpcqp_warm_start_device(mpcqp_handle* h, const double* dx, const double* dy, void* stream) {
+    if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "device entry points need a single-device handle");
+    Shard& s = h->shards[0];
+    HIPCHK(hipSetDevice(s.dev));
+    HIPCHK(launch_warm(s.kp, s.B, dx, dy, pick(s, stream)));
+    s.kp.warm_start = 1;
+    h->set.warm_start = 1;
+    return 0;
+}
+
+int mpcqp_solve_device(mpcqp_handle* h, double* dx, double* dy, int32_t* dstatus, int32_t* diters, void* stream) {
+    if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "device entry points need a single-device handle");
+    Shard& s = h->shards[0];
+    hipStream_t st = pick(s, stream);
+    HIPCHK(hipSetDevice(s.dev));
+    HIPCHK(hipEventRecord(s.ev0, st));
+    HIPCHK(launch_solve(s.kp, s.B, dx, dy, 0, st));
+    HIPCHK(hipEventRecord(s.ev1, st));
+    if (dstatus) HIPCHK(hipMemcpyAsync(dstatus, s.kp.status, sizeof(int) * s.B, hipMemcpyDeviceToDevice, st));
+    if (diters) HIPCHK(hipMemcpyAsync(diters, s.kp.iter, sizeof(int) * s.B, hipMemcpyDeviceToDevice, st));
+    h->timed = true;
+    return 0;
+}
+
+int mpcqp_synchronize(mpcqp_handle* h) {
+    if (!h) return fail(MPCQP_EINVAL, "NULL handle");
+    return sync_all(h);
+}
+
+double mpcqp_last_kernel_ms(mpcqp_handle* h) {
+    if (!h || h->shards.size() != 1) return -1.0;
+    Shard& s = h->shards[0];
+    float ms = 0.f;
+    if (hipSetDevice(s.dev) != hipSuccess) return -1.0;
+    if (hipEventSynchronize(s.ev1) != hipSuccess) return -1.0;
+    if (hipEventElapsedTime(&ms, s.ev0, s.ev1) != hipSuccess) return -1.0;
+    return ms;
+}
+
+int mpcqp_get_plan_info(const mpcqp_handle* h, mpcqp_plan_info* info) {
+    if (!h || !info) return fail(MPCQP_EINVAL, "NULL argument");
+    info->n = h->n; info->m = h->m; info->nb = h->plan.nb; info->block = kS;
+    info->npad = h->plan.npad; info->max_level = h->plan.max_level;
+    info->batch = h->B; info->n_devices = (int)h->shards.size();
+    info->lds_bytes_solve = h->shards.empty() ? 0 : (int64_t)lds_solve_bytes(h->shards[0].kp);
+    info->bytes_per_instance = (int64_t)(workspace_bytes(h->plan, 1, false));
+    return 0;
+}
+
+void mpcqp_free(mpcqp_handle* h) {
+    if (!h) return;
+    for (auto& s : h->shards) {
+        (void)hipSetDevice(s.dev);
+        if (s.stream) (void)hipStreamSynchronize(s.stream);
+        if (s.dws) (void)hipFree(s.dws);
+        if (s.dplan) (void)hipFree(s.dplan);
+        if (s.ev0) (void)hipEventDestroy(s.ev0);
+        if (s.ev1) (void)hipEventDestroy(s.ev1);
+        if (s.stream) (void)hipStreamDestroy(s.stream);
+    }
+    delete h;
+}
+
+}  // extern "C"

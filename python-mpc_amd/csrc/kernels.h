@@ -1,0 +1,51 @@
+// kernels.h -- device-side interface shared by kernels.hip and api.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "plan.h"
+
+namespace mpcqp {
+
+constexpr int kThreads = 256;  // one workgroup (4 wavefronts) per QP instance
+
+// status values (OSQP constants.h)
+enum : int {
+    MPCQP_DUAL_INFEASIBLE_INACCURATE_ = 4,
+    MPCQP_PRIMAL_INFEASIBLE_INACCURATE_ = 3,
+    MPCQP_SOLVED_INACCURATE_ = 2,
+    MPCQP_SOLVED_ = 1,
+    MPCQP_MAX_ITER_REACHED_ = -2,
+    MPCQP_PRIMAL_INFEASIBLE_ = -3,
+    MPCQP_DUAL_INFEASIBLE_ = -4,
+    MPCQP_NON_CVX_ = -7,
+    MPCQP_UNSOLVED_ = -10,
+};
+
+// Everything a kernel needs: plan (shared pattern, read-only) + per-instance
+// workspace (instance-major arrays) + settings.  Passed by value.
+struct KParams {
+    int n, m, nb, npad, nnzP, nnzA;
+    // plan
+    const int *pad_var, *acsc_ptr, *acsc_row, *acsc_v, *acsr_ptr, *acsr_col, *acsr_v;
+    const int *psym_ptr, *psym_col, *psym_v, *p_r, *p_c, *a_r, *a_c;
+    const int *asm_blk_ptr, *asm_tgt, *asm_term_ptr, *term_a, *term_b, *term_r;
+    // workspace
+    double *Px, *Ax, *q, *D, *l, *u, *E, *x, *z, *y, *scal, *F, *H, *Si, *dyc, *dxc;
+    double *obj, *pri, *dua, *rho_est;
+    signed char* ct;
+    int *status, *iter, *rho_upd, *err;
+    // settings
+    double sigma, alpha, eps_abs, eps_rel, eps_pinf, eps_dinf, rho0, rho_tol;
+    int max_iter, scaling, check_term, warm_start, adaptive_rho, rho_interval, scaled_term;
+};
+
+size_t lds_setup_bytes(const KParams& p);
+size_t lds_solve_bytes(const KParams& p);
+hipError_t launch_setup(const KParams& p, long B, const double* Px, const double* Ax, const double* q,
+                        const double* l, const double* u, hipStream_t st);
+hipError_t launch_update(const KParams& p, long B, const double* q, const double* l, const double* u,
+                         hipStream_t st);
+hipError_t launch_warm(const KParams& p, long B, const double* x, const double* y, hipStream_t st);
+hipError_t launch_solve(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st);
+
+}  // namespace mpcqp

@@ -1,0 +1,226 @@
+// plan.cpp -- symbolic analysis of the shared sparsity pattern (see plan.h).
+#include "plan.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <queue>
+
+namespace mpcqp {
+
+namespace {
+
+struct Graph {
+    std::vector<std::vector<int>> adj;
+};
+
+// BFS from `s` restricted to unvisited-in-component vertices; returns levels.
+std::vector<std::vector<int>> bfs_levels(const Graph& g, int s, std::vector<int>& mark, int stamp) {
+    std::vector<std::vector<int>> levels;
+    std::vector<int> cur{s};
+    mark[s] = stamp;
+    while (!cur.empty()) {
+        levels.push_back(cur);
+        std::vector<int> nxt;
+        for (int v : cur) {
+            // Cuthill-McKee flavour: visit neighbours by increasing degree
+            std::vector<int> nb;
+            for (int w : g.adj[v])
+                if (mark[w] != stamp) { mark[w] = stamp; nb.push_back(w); }
+            std::stable_sort(nb.begin(), nb.end(), [&](int a, int b) {
+                return g.adj[a].size() < g.adj[b].size();
+            });
+            nxt.insert(nxt.end(), nb.begin(), nb.end());
+        }
+        cur.swap(nxt);
+    }
+    return levels;
+}
+
+}  // namespace
+
+std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
+                       const int32_t* Ai, Plan& pl) {
+    char buf[256];
+    if (n <= 0 || m < 0) return "invalid dimensions";
+    if (Pp[0] != 0 || Ap[0] != 0) return "CSC column pointers must start at 0";
+    for (int j = 0; j < n; ++j) {
+        if (Pp[j + 1] < Pp[j] || Ap[j + 1] < Ap[j]) return "CSC column pointers must be nondecreasing";
+        for (int p = Pp[j]; p < Pp[j + 1]; ++p)
+            if (Pi[p] < 0 || Pi[p] > j) return "P must be upper triangular";
+        for (int p = Ap[j]; p < Ap[j + 1]; ++p)
+            if (Ai[p] < 0 || Ai[p] >= m) return "A row index out of range";
+    }
+    pl = Plan();
+    pl.n = n; pl.m = m; pl.nnzP = Pp[n]; pl.nnzA = Ap[n];
+
+    // rows of A
+    std::vector<std::vector<std::pair<int, int>>> rows(m);  // (col, value idx)
+    for (int j = 0; j < n; ++j)
+        for (int p = Ap[j]; p < Ap[j + 1]; ++p) rows[Ai[p]].push_back({j, p});
+
+    // graph of K = P + A'A (off-diagonal pattern)
+    Graph g;
+    g.adj.assign(n, {});
+    for (int j = 0; j < n; ++j)
+        for (int p = Pp[j]; p < Pp[j + 1]; ++p) {
+            int i = Pi[p];
+            if (i != j) { g.adj[i].push_back(j); g.adj[j].push_back(i); }
+        }
+    for (int r = 0; r < m; ++r)
+        for (auto& a : rows[r])
+            for (auto& b : rows[r])
+                if (a.first != b.first) g.adj[a.first].push_back(b.first);
+    for (auto& v : g.adj) {
+        std::sort(v.begin(), v.end());
+        v.erase(std::unique(v.begin(), v.end()), v.end());
+    }
+
+    // components, pseudo-peripheral BFS level structures
+    std::vector<int> comp(n, -1), mark(n, -1);
+    std::vector<std::vector<int>> all_levels, iso_levels;
+    int stamp = 0;
+    for (int v0 = 0; v0 < n; ++v0) {
+        if (comp[v0] >= 0) continue;
+        // collect component
+        std::vector<int> cv{v0};
+        comp[v0] = v0;
+        for (size_t t = 0; t < cv.size(); ++t)
+            for (int w : g.adj[cv[t]])
+                if (comp[w] < 0) { comp[w] = v0; cv.push_back(w); }
+        if (cv.size() == 1) { iso_levels.push_back({v0}); continue; }
+        int s = cv[0];
+        for (int v : cv)
+            if (g.adj[v].size() < g.adj[s].size()) s = v;
+        auto lv = bfs_levels(g, s, mark, stamp++);
+        for (int it = 0; it < 16; ++it) {  // George-Liu pseudo-peripheral search
+            int cand = lv.back()[0];
+            for (int v : lv.back())
+                if (g.adj[v].size() < g.adj[cand].size()) cand = v;
+            auto lv2 = bfs_levels(g, cand, mark, stamp++);
+            if (lv2.size() > lv.size()) { lv.swap(lv2); s = cand; }
+            else {
+                // prefer the narrower structure among equal-depth ones
+                size_t w1 = 0, w2 = 0;
+                for (auto& L : lv) w1 = std::max(w1, L.size());
+                for (auto& L : lv2) w2 = std::max(w2, L.size());
+                if (lv2.size() == lv.size() && w2 < w1) lv.swap(lv2);
+                break;
+            }
+        }
+        for (auto& L : lv) all_levels.push_back(L);
+    }
+    for (auto& L : iso_levels) all_levels.push_back(L);
+
+    // merge consecutive levels into blocks of <= kS
+    std::vector<std::vector<int>> blocks;
+    for (auto& L : all_levels) {
+        pl.max_level = std::max<int>(pl.max_level, (int)L.size());
+        if ((int)L.size() > kS) {
+            snprintf(buf, sizeof buf,
+                     "unsupported sparsity: a level set of K has %zu > %d variables", L.size(), kS);
+            return buf;
+        }
+        if (!blocks.empty() && blocks.back().size() + L.size() <= (size_t)kS)
+            blocks.back().insert(blocks.back().end(), L.begin(), L.end());
+        else
+            blocks.push_back(L);
+    }
+    pl.nb = (int)blocks.size();
+    pl.npad = pl.nb * kS;
+    pl.bsize.resize(pl.nb);
+    pl.var_pad.assign(n, -1);
+    pl.pad_var.assign(pl.npad, -1);
+    for (int k = 0; k < pl.nb; ++k) {
+        pl.bsize[k] = (int)blocks[k].size();
+        for (int t = 0; t < pl.bsize[k]; ++t) {
+            pl.var_pad[blocks[k][t]] = k * kS + t;
+            pl.pad_var[k * kS + t] = blocks[k][t];
+        }
+    }
+    for (int j = 0; j < n; ++j)
+        if (pl.var_pad[j] < 0) return "internal: unplaced variable";
+
+    // A by padded column
+    pl.acsc_ptr.assign(pl.npad + 1, 0);
+    for (int pc = 0; pc < pl.npad; ++pc) {
+        int j = pl.pad_var[pc];
+        pl.acsc_ptr[pc + 1] = pl.acsc_ptr[pc] + (j >= 0 ? Ap[j + 1] - Ap[j] : 0);
+    }
+    pl.acsc_row.resize(pl.nnzA);
+    pl.acsc_v.resize(pl.nnzA);
+    for (int pc = 0; pc < pl.npad; ++pc) {
+        int j = pl.pad_var[pc];
+        if (j < 0) continue;
+        int q = pl.acsc_ptr[pc];
+        for (int p = Ap[j]; p < Ap[j + 1]; ++p, ++q) { pl.acsc_row[q] = Ai[p]; pl.acsc_v[q] = p; }
+    }
+    // A by row
+    pl.acsr_ptr.assign(m + 1, 0);
+    for (int r = 0; r < m; ++r) pl.acsr_ptr[r + 1] = pl.acsr_ptr[r] + (int)rows[r].size();
+    pl.acsr_col.resize(pl.nnzA);
+    pl.acsr_v.resize(pl.nnzA);
+    for (int r = 0; r < m; ++r) {
+        int q = pl.acsr_ptr[r];
+        for (auto& e : rows[r]) { pl.acsr_col[q] = pl.var_pad[e.first]; pl.acsr_v[q] = e.second; ++q; }
+    }
+    // full symmetric P by padded row
+    std::vector<std::vector<std::pair<int, int>>> prow(pl.npad);
+    pl.p_r.resize(pl.nnzP);
+    pl.p_c.resize(pl.nnzP);
+    for (int j = 0; j < n; ++j)
+        for (int p = Pp[j]; p < Pp[j + 1]; ++p) {
+            int i = Pi[p];
+            int pi = pl.var_pad[i], pj = pl.var_pad[j];
+            pl.p_r[p] = pi; pl.p_c[p] = pj;
+            prow[pi].push_back({pj, p});
+            if (i != j) prow[pj].push_back({pi, p});
+        }
+    pl.psym_ptr.assign(pl.npad + 1, 0);
+    for (int r = 0; r < pl.npad; ++r) pl.psym_ptr[r + 1] = pl.psym_ptr[r] + (int)prow[r].size();
+    for (int r = 0; r < pl.npad; ++r)
+        for (auto& e : prow[r]) { pl.psym_col.push_back(e.first); pl.psym_v.push_back(e.second); }
+    pl.a_r.resize(pl.nnzA);
+    pl.a_c.resize(pl.nnzA);
+    for (int j = 0; j < n; ++j)
+        for (int p = Ap[j]; p < Ap[j + 1]; ++p) { pl.a_r[p] = Ai[p]; pl.a_c[p] = pl.var_pad[j]; }
+
+    // assembly terms: key = block*2*S*S + tile index
+    struct Term { long key; int a, b, r; };
+    std::vector<Term> terms;
+    const long SS = (long)kS * kS;
+    std::string err;
+    auto add = [&](int pi, int pj, int a, int b, int r) {
+        int bi = pi / kS, bj = pj / kS, li = pi % kS, lj = pj % kS;
+        if (bi == bj) terms.push_back({bi * 2 * SS + li * kS + lj, a, b, r});
+        else if (bi == bj + 1) terms.push_back({bi * 2 * SS + SS + li * kS + lj, a, b, r});
+        else if (bj == bi + 1) { /* upper block: covered by the transposed entry */ }
+        else err = "internal: coupling beyond neighbouring blocks";
+    };
+    for (int r = 0; r < pl.npad; ++r)
+        for (auto& e : prow[r]) add(r, e.first, e.second, 0, -1);
+    for (int r = 0; r < m; ++r)
+        for (auto& a : rows[r])
+            for (auto& b : rows[r]) add(pl.var_pad[a.first], pl.var_pad[b.first], a.second, b.second, r);
+    if (!err.empty()) return err;
+    std::stable_sort(terms.begin(), terms.end(), [](const Term& x, const Term& y) { return x.key < y.key; });
+    pl.asm_blk_ptr.assign(pl.nb + 1, 0);
+    pl.asm_term_ptr.push_back(0);
+    for (size_t t = 0; t < terms.size();) {
+        size_t u = t;
+        while (u < terms.size() && terms[u].key == terms[t].key) {
+            pl.term_a.push_back(terms[u].a);
+            pl.term_b.push_back(terms[u].b);
+            pl.term_r.push_back(terms[u].r);
+            ++u;
+        }
+        int blk = (int)(terms[t].key / (2 * SS));
+        pl.asm_tgt.push_back((int)(terms[t].key % (2 * SS)));
+        pl.asm_term_ptr.push_back((int)pl.term_a.size());
+        pl.asm_blk_ptr[blk + 1]++;
+        t = u;
+    }
+    for (int k = 0; k < pl.nb; ++k) pl.asm_blk_ptr[k + 1] += pl.asm_blk_ptr[k];
+    return "";
+}
+
+}  // namespace mpcqp

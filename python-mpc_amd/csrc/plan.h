@@ -1,0 +1,51 @@
+// plan.h -- host-side symbolic analysis for the MI355X batched QP solver.
+//
+// Everything here depends only on the SHARED sparsity pattern of the batch
+// (P upper-triangular CSC, A CSC -- the arrays osqp.OSQP().setup() receives at
+// vehicle_lateral_mpc_slack_increment.py:121 / Control/MPC/mpc_dynamics.py:393).
+// It is computed once per handle; no per-instance numbers are touched on the
+// host.
+//
+// The reduced KKT matrix  K = P + sigma I + A' diag(rho) A  (SPD, n x n) is
+// put in block-tridiagonal form: breadth-first level sets of K's graph (per
+// connected component, from a pseudo-peripheral vertex) only couple to the
+// neighbouring level, so consecutive levels merged into blocks of <= S
+// variables give  K = tridiag(E_k, D_k, E_{k+1}').  Every variable gets a
+// "padded" index  k*S + local  so the device works on uniform S x S tiles.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace mpcqp {
+
+constexpr int kS = 32;  // block (tile) size
+
+struct Plan {
+    int n = 0, m = 0, nb = 0, npad = 0, nnzP = 0, nnzA = 0;
+    std::vector<int> bsize;       // [nb]
+    std::vector<int> var_pad;     // [n]    user variable -> padded index
+    std::vector<int> pad_var;     // [npad] padded index -> user variable or -1
+    // A by padded column (CSC): entries (row, value index into user Ax)
+    std::vector<int> acsc_ptr, acsc_row, acsc_v;
+    // A by row (CSR): entries (padded column, value index)
+    std::vector<int> acsr_ptr, acsr_col, acsr_v;
+    // full symmetric P by padded row: (padded column, value index into user Px)
+    std::vector<int> psym_ptr, psym_col, psym_v;
+    // per stored value: padded row / column
+    std::vector<int> p_r, p_c;    // [nnzP] (upper triangle of the user's P)
+    std::vector<int> a_r, a_c;    // [nnzA] (row, padded column)
+    // K assembly.  Per block k the device fills two S*S tiles:
+    //   D_k (local index i*S+j)  and  E_k = K(block k, block k-1) (index S*S + i*S + j).
+    // Targets of block k: asm_tgt[asm_blk_ptr[k] .. asm_blk_ptr[k+1]),
+    // terms of target t: [asm_term_ptr[t], asm_term_ptr[t+1]).
+    // term: r >= 0  -> rho[r] * Ax[a] * Ax[b];  r == -1 -> Px[a].
+    std::vector<int> asm_blk_ptr, asm_tgt, asm_term_ptr, term_a, term_b, term_r;
+    int max_level = 0;            // largest BFS level (diagnostic)
+};
+
+// Returns "" on success, otherwise an error message.
+std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi,
+                       const int32_t* Ap, const int32_t* Ai, Plan& out);
+
+}  // namespace mpcqp

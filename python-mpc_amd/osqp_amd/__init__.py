@@ -1,0 +1,373 @@
+"""osqp_amd -- drop-in for the reference's `osqp.OSQP` on AMD MI355X.
+
+The reference builds sparse MPC QPs in Python and calls OSQP through
+``prob = osqp.OSQP(); prob.setup(P, q, A, l, u, **settings)``, ``prob.update(q=, l=, u=)``,
+``res = prob.solve()`` and reads ``res.x`` / ``res.info.status``
+(vehicle_lateral_mpc_slack_increment.py:118,121,237,248,252,256,269;
+Control/MPC/mpc_kinematics.py:194-198; Control/MPC/mpc_dynamics.py:240-244,392-396).
+This package mirrors that surface (same names, argument meaning, status strings
+and ValueError behaviour) and forwards to the C ABI in include/mpcqp.h
+(libmpcqp.so), whose HIP kernels do all numerical work.  There is no CPU
+fallback: if the extension or a HIP device is missing, calls raise.
+
+Additions beyond osqp's API (same semantics, batched):
+  * ``OSQPBatch`` -- B instances sharing one sparsity pattern, values per instance.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import time
+from types import SimpleNamespace
+
+import numpy as np
+import scipy.sparse as sparse
+
+__all__ = ["OSQP", "OSQPBatch", "constant", "STATUS", "lib", "LIB_PATH"]
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmpcqp.so")
+OSQP_INFTY = 1e30
+
+STATUS = {
+    4: "dual infeasible inaccurate",
+    3: "primal infeasible inaccurate",
+    2: "solved inaccurate",
+    1: "solved",
+    -2: "maximum iterations reached",
+    -3: "primal infeasible",
+    -4: "dual infeasible",
+    -5: "interrupted",
+    -6: "run time limit reached",
+    -7: "problem non convex",
+    -10: "unsolved",
+}
+
+_CONSTANTS = {
+    "OSQP_INFTY": OSQP_INFTY, "OSQP_NAN": float("nan"),
+    "OSQP_SOLVED": 1, "OSQP_SOLVED_INACCURATE": 2, "OSQP_MAX_ITER_REACHED": -2,
+    "OSQP_PRIMAL_INFEASIBLE": -3, "OSQP_PRIMAL_INFEASIBLE_INACCURATE": 3,
+    "OSQP_DUAL_INFEASIBLE": -4, "OSQP_DUAL_INFEASIBLE_INACCURATE": 4,
+    "OSQP_NON_CVX": -7, "OSQP_UNSOLVED": -10,
+}
+
+
+def constant(name):
+    """osqp.constant(name)"""
+    if name not in _CONSTANTS:
+        raise ValueError("Constant not recognized")
+    return _CONSTANTS[name]
+
+
+class _Settings(C.Structure):
+    _fields_ = [
+        ("rho", C.c_double), ("sigma", C.c_double), ("alpha", C.c_double),
+        ("eps_abs", C.c_double), ("eps_rel", C.c_double),
+        ("eps_prim_inf", C.c_double), ("eps_dual_inf", C.c_double),
+        ("adaptive_rho_tolerance", C.c_double),
+        ("max_iter", C.c_int32), ("scaling", C.c_int32), ("check_termination", C.c_int32),
+        ("warm_start", C.c_int32), ("adaptive_rho", C.c_int32),
+        ("adaptive_rho_interval", C.c_int32), ("scaled_termination", C.c_int32),
+        ("polish", C.c_int32), ("verbose", C.c_int32),
+    ]
+
+
+class _PlanInfo(C.Structure):
+    _fields_ = [
+        ("n", C.c_int32), ("m", C.c_int32), ("nb", C.c_int32), ("block", C.c_int32),
+        ("npad", C.c_int32), ("max_level", C.c_int32), ("batch", C.c_int64),
+        ("n_devices", C.c_int32), ("lds_bytes_solve", C.c_int64), ("bytes_per_instance", C.c_int64),
+    ]
+
+
+_lib = None
+_P = C.POINTER
+
+
+def lib():
+    """Load libmpcqp.so (fails loudly if the HIP extension was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not found: build the HIP extension first "
+            "(python -c 'import __graft_entry__ as g; g.build()')")
+    L = C.CDLL(LIB_PATH)
+    i32p, dp, vp = _P(C.c_int32), _P(C.c_double), C.c_void_p
+    hp = _P(C.c_void_p)
+    L.mpcqp_default_settings.argtypes = [_P(_Settings)]
+    L.mpcqp_default_settings.restype = None
+    L.mpcqp_last_error.restype = C.c_char_p
+    L.mpcqp_setup_batch.argtypes = [C.c_int32, C.c_int32, i32p, i32p, i32p, i32p, C.c_int64,
+                                    dp, dp, dp, dp, dp, _P(_Settings), C.c_uint32, hp]
+    L.mpcqp_update_batch.argtypes = [vp, dp, dp, dp]
+    L.mpcqp_warm_start_batch.argtypes = [vp, dp, dp]
+    L.mpcqp_solve_batch.argtypes = [vp, dp, dp, i32p, i32p]
+    L.mpcqp_get_info_batch.argtypes = [vp, dp, dp, dp, dp, i32p]
+    L.mpcqp_get_certificates.argtypes = [vp, dp, dp]
+    L.mpcqp_create.argtypes = [C.c_int32, C.c_int32, i32p, i32p, i32p, i32p, C.c_int64,
+                               _P(_Settings), C.c_int32, hp]
+    L.mpcqp_setup_device.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+    L.mpcqp_update_device.argtypes = [vp, vp, vp, vp, vp]
+    L.mpcqp_warm_start_device.argtypes = [vp, vp, vp, vp]
+    L.mpcqp_solve_device.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.mpcqp_synchronize.argtypes = [vp]
+    L.mpcqp_last_kernel_ms.argtypes = [vp]
+    L.mpcqp_last_kernel_ms.restype = C.c_double
+    L.mpcqp_get_plan_info.argtypes = [vp, _P(_PlanInfo)]
+    L.mpcqp_free.argtypes = [vp]
+    L.mpcqp_free.restype = None
+    L.mpcqp_analyze.argtypes = [C.c_int32, C.c_int32, i32p, i32p, i32p, i32p,
+                                i32p, i32p, i32p, i32p]
+    _lib = L
+    return L
+
+
+def _dp(a):
+    return None if a is None else a.ctypes.data_as(_P(C.c_double))
+
+
+def _ip(a):
+    return None if a is None else a.ctypes.data_as(_P(C.c_int32))
+
+
+def _check(code, what):
+    if code:
+        msg = lib().mpcqp_last_error().decode()
+        if code == 1:
+            raise ValueError(f"{what}: {msg}")
+        if code == 2:
+            raise NotImplementedError(f"{what}: {msg}")
+        raise RuntimeError(f"{what}: {msg} (code {code})")
+
+
+_SETTING_NAMES = {f[0] for f in _Settings._fields_}
+_IGNORED = {"linsys_solver", "delta", "polish_refine_iter", "time_limit", "adaptive_rho_fraction"}
+
+
+def _make_settings(**kw) -> _Settings:
+    s = _Settings()
+    lib().mpcqp_default_settings(C.byref(s))
+    for k, v in kw.items():
+        if k in _IGNORED:
+            continue
+        if k not in _SETTING_NAMES:
+            raise ValueError(f"Unrecognized setting {k}")
+        if isinstance(v, bool):
+            v = int(v)
+        setattr(s, k, type(getattr(s, k))(v))
+    return s
+
+
+def canonical_data(P, A):
+    """osqp-python's prepare_data: P -> triu CSC, A -> CSC, sorted int32 indices."""
+    if P is None:
+        raise ValueError("P must be provided")
+    P = sparse.triu(sparse.csc_matrix(P), format="csc")
+    A = sparse.csc_matrix(A)
+    P.sort_indices()
+    A.sort_indices()
+    return P, A
+
+
+def analyze(P, A):
+    """Host-only symbolic analysis (no GPU): returns (nb, block, var_pad, bsize)."""
+    P, A = canonical_data(P, A)
+    n, m = P.shape[0], A.shape[0]
+    nb = C.c_int32(); blk = C.c_int32()
+    vp = np.empty(n, np.int32); bs = np.empty(max(n, 1), np.int32)
+    Pp = np.ascontiguousarray(P.indptr, np.int32); Pi = np.ascontiguousarray(P.indices, np.int32)
+    Ap = np.ascontiguousarray(A.indptr, np.int32); Ai = np.ascontiguousarray(A.indices, np.int32)
+    _check(lib().mpcqp_analyze(n, m, _ip(Pp), _ip(Pi), _ip(Ap), _ip(Ai), C.byref(nb), C.byref(blk),
+                               _ip(vp), _ip(bs)), "analyze")
+    return nb.value, blk.value, vp, bs[: nb.value].copy()
+
+
+def _drop_common_zeros(M, V):
+    keep = np.any(V != 0, axis=0)
+    if keep.all():
+        return M, V
+    M = M.copy()
+    M.data = keep.astype(np.float64)
+    M.eliminate_zeros()
+    M.sort_indices()
+    return M, V[:, keep]
+
+
+class _Handle:
+    def __init__(self, ptr):
+        self.ptr = ptr
+
+    def __del__(self):
+        if self.ptr:
+            lib().mpcqp_free(self.ptr)
+            self.ptr = None
+
+
+class OSQPBatch:
+    """B QPs with one shared sparsity pattern, solved together on the GPU(s).
+
+    setup(P, q, A, l, u, Px=None, Ax=None, device_mask=1, **settings):
+      P, A  -- scipy sparse templates (pattern; values used when Px/Ax are None)
+      q     -- (B, n);  l, u -- (B, m)
+      Px    -- (B, nnz(triu(P))) per-instance values in triu(P).tocsc() order
+      Ax    -- (B, nnz(A))       per-instance values in A.tocsc() order
+    """
+
+    def __init__(self):
+        self._h = None
+        self.n = self.m = self.B = 0
+
+    def setup(self, P, q, A, l, u, Px=None, Ax=None, device_mask=1, **settings):
+        t0 = time.perf_counter()
+        P, A = canonical_data(P, A)
+        n, m = P.shape[0], A.shape[0]
+        if P.shape != (n, n) or A.shape[1] != n:
+            raise ValueError("Matrix dimensions are not consistent")
+        q = np.atleast_2d(np.asarray(q, np.float64))
+        B = q.shape[0]
+        l = np.atleast_2d(np.asarray(l, np.float64))
+        u = np.atleast_2d(np.asarray(u, np.float64))
+        if q.shape != (B, n) or l.shape != (B, m) or u.shape != (B, m):
+            raise ValueError("q, l, u must have shapes (B, n), (B, m), (B, m)")
+        Px = np.broadcast_to(P.data if Px is None else np.asarray(Px, np.float64), (B, P.nnz))
+        Ax = np.broadcast_to(A.data if Ax is None else np.asarray(Ax, np.float64), (B, A.nnz))
+        # Entries that are zero in every instance contribute exactly 0 to every OSQP
+        # operation, so dropping them is bit-for-bit neutral; it keeps structural
+        # zeros of the reference's assembly (e.g. C~'QC~ at mpc_dynamics.py:296-297)
+        # out of the sparsity plan.
+        P, Px = _drop_common_zeros(P, Px)
+        A, Ax = _drop_common_zeros(A, Ax)
+        Px = np.ascontiguousarray(Px, np.float64)
+        Ax = np.ascontiguousarray(Ax, np.float64)
+        q = np.ascontiguousarray(q); l = np.ascontiguousarray(l); u = np.ascontiguousarray(u)
+        self._pattern = (np.ascontiguousarray(P.indptr, np.int32), np.ascontiguousarray(P.indices, np.int32),
+                         np.ascontiguousarray(A.indptr, np.int32), np.ascontiguousarray(A.indices, np.int32))
+        Pp, Pi, Ap, Ai = self._pattern
+        s = _make_settings(**settings)
+        self._settings = s
+        h = C.c_void_p()
+        _check(lib().mpcqp_setup_batch(n, m, _ip(Pp), _ip(Pi), _ip(Ap), _ip(Ai), B, _dp(Px), _dp(Ax),
+                                       _dp(q), _dp(l), _dp(u), C.byref(s), int(device_mask), C.byref(h)),
+               "setup")
+        self._h = _Handle(h.value)
+        self.n, self.m, self.B = n, m, B
+        self.setup_time = time.perf_counter() - t0
+
+    def _need(self):
+        if self._h is None:
+            raise ValueError("Workspace not initialized!")
+        return self._h.ptr
+
+    def update(self, q=None, l=None, u=None, Px=None, Ax=None, **kw):
+        h = self._need()
+        if Px is not None or Ax is not None or kw:
+            raise NotImplementedError("matrix updates (Px/Ax) are not supported; run setup() again")
+        if q is None and l is None and u is None:
+            raise ValueError("No updatable data has been specified!")
+        B, n, m = self.B, self.n, self.m
+
+        def prep(v, k, clip):
+            if v is None:
+                return None
+            v = np.asarray(v, np.float64).reshape(B, k)
+            if clip is not None:
+                v = np.maximum(v, -OSQP_INFTY) if clip < 0 else np.minimum(v, OSQP_INFTY)
+            return np.ascontiguousarray(v)
+
+        q = prep(q, n, None); l = prep(l, m, -1); u = prep(u, m, 1)
+        _check(lib().mpcqp_update_batch(h, _dp(q), _dp(l), _dp(u)), "update")
+
+    def warm_start(self, x=None, y=None):
+        h = self._need()
+        x = None if x is None else np.ascontiguousarray(np.asarray(x, np.float64).reshape(self.B, self.n))
+        y = None if y is None else np.ascontiguousarray(np.asarray(y, np.float64).reshape(self.B, self.m))
+        _check(lib().mpcqp_warm_start_batch(h, _dp(x), _dp(y)), "warm_start")
+
+    def solve(self):
+        h = self._need()
+        B, n, m = self.B, self.n, self.m
+        x = np.empty((B, n)); y = np.empty((B, m))
+        st = np.empty(B, np.int32); it = np.empty(B, np.int32)
+        t0 = time.perf_counter()
+        _check(lib().mpcqp_solve_batch(h, _dp(x), _dp(y), _ip(st), _ip(it)), "solve")
+        solve_time = time.perf_counter() - t0
+        obj = np.empty(B); pri = np.empty(B); dua = np.empty(B); rho = np.empty(B)
+        ru = np.empty(B, np.int32)
+        _check(lib().mpcqp_get_info_batch(h, _dp(obj), _dp(pri), _dp(dua), _dp(rho), _ip(ru)), "info")
+        pc = np.empty((B, m)); dc = np.empty((B, n))
+        _check(lib().mpcqp_get_certificates(h, _dp(pc), _dp(dc)), "certificates")
+        return SimpleNamespace(x=x, y=y, status_val=st, iter=it, obj_val=obj, pri_res=pri, dua_res=dua,
+                               rho_estimate=rho, rho_updates=ru, prim_inf_cert=pc, dual_inf_cert=dc,
+                               solve_time=solve_time,
+                               status=[STATUS.get(int(v), "unknown") for v in st])
+
+    def plan_info(self):
+        info = _PlanInfo()
+        _check(lib().mpcqp_get_plan_info(self._need(), C.byref(info)), "plan_info")
+        return {f[0]: getattr(info, f[0]) for f in _PlanInfo._fields_}
+
+
+class OSQP:
+    """Single-instance mirror of osqp.OSQP (runs as a batch of one on the GPU)."""
+
+    def __init__(self):
+        self._b = None
+
+    def setup(self, P=None, q=None, A=None, l=None, u=None, **settings):
+        if P is None or A is None:
+            raise ValueError("P and A must be provided")
+        n = P.shape[0]
+        m = A.shape[0]
+        q = np.zeros(n) if q is None else np.asarray(q, np.float64).ravel()
+        l = np.full(m, -np.inf) if l is None else np.asarray(l, np.float64).ravel()
+        u = np.full(m, np.inf) if u is None else np.asarray(u, np.float64).ravel()
+        if len(q) != n:
+            raise ValueError("Incorrect dimension of q")
+        if len(l) != m or len(u) != m:
+            raise ValueError("Incorrect dimension of l or u")
+        l = np.maximum(l, -OSQP_INFTY)
+        u = np.minimum(u, OSQP_INFTY)
+        self._settings_kw = dict(settings)
+        self._b = OSQPBatch()
+        self._b.setup(P, q[None, :], A, l[None, :], u[None, :], **settings)
+        self._update_time = 0.0
+
+    def update(self, q=None, l=None, u=None, Px=None, Px_idx=np.array([]), Ax=None, Ax_idx=np.array([])):
+        if self._b is None:
+            raise ValueError("Workspace not initialized!")
+        n, m = self._b.n, self._b.m
+        if q is not None and len(q) != n:
+            raise ValueError("q must have length n")
+        if l is not None:
+            if not isinstance(l, np.ndarray):
+                raise TypeError("l must be numpy.ndarray, not %s" % type(l).__name__)
+            if len(l) != m:
+                raise ValueError("l must have length m")
+        if u is not None:
+            if not isinstance(u, np.ndarray):
+                raise TypeError("u must be numpy.ndarray, not %s" % type(u).__name__)
+            if len(u) != m:
+                raise ValueError("u must have length m")
+        t0 = time.perf_counter()
+        self._b.update(q=q, l=l, u=u, Px=Px, Ax=Ax)
+        self._update_time = time.perf_counter() - t0
+
+    def warm_start(self, x=None, y=None):
+        if self._b is None:
+            raise ValueError("Workspace not initialized!")
+        self._b.warm_start(x=x, y=y)
+
+    def solve(self):
+        if self._b is None:
+            raise ValueError("Workspace not initialized!")
+        r = self._b.solve()
+        sv = int(r.status_val[0])
+        info = SimpleNamespace(
+            iter=int(r.iter[0]), status=STATUS.get(sv, "unknown"), status_val=sv, status_polish=0,
+            obj_val=float(r.obj_val[0]), pri_res=float(r.pri_res[0]), dua_res=float(r.dua_res[0]),
+            setup_time=self._b.setup_time, solve_time=r.solve_time, update_time=self._update_time,
+            polish_time=0.0, run_time=r.solve_time, rho_updates=int(r.rho_updates[0]),
+            rho_estimate=float(r.rho_estimate[0]))
+        return SimpleNamespace(x=r.x[0], y=r.y[0], info=info, prim_inf_cert=r.prim_inf_cert[0],
+                               dua_inf_cert=r.dual_inf_cert[0])

@@ -1,0 +1,260 @@
+"""Generate tests/golden/*.npz from the reference's OWN assembly code.
+
+Run in the build container (where /root/reference exists):
+    MPLBACKEND=Agg python tests/golden/make_golden.py
+
+The reference calls OSQP; `osqp` is not installed (and not vendored), so a
+capture stub is injected as sys.modules['osqp'] that records every
+setup(P, q, A, l, u, **settings) / update(**kw) the reference makes and returns
+a zero "solution".  Only DATA is committed (inputs the reference assembles and
+the linearisations it computes); no reference source is copied.  The fixtures
+pin the host-side QP assembly and the vehicle-model
+linearisation (row A3); solver outputs are produced by oracle/ and checked by
+KKT certificates (tests/test_oracle.py).
+
+Fixtures:
+  slack_n20.npz      vehicle_lateral_mpc_slack_increment.py:32-121 with N=20 (cfg 1/3/4 layout)
+                     + the update(q,l,u) vectors of loop steps 0, 401, 901 (:158-172, :237, :269)
+  vanilla_n20.npz    Control/MPC/mpc_kinematics.py:148-200 with the lateral Ad/Bd (cfg 2)
+  dyn_incr_n50.npz   Control/MPC/mpc_dynamics.py:281-434 + Vehicle_Dynamics.get_dynamics_model
+                     (cfg 5 layout), 3 seeded instances, with the Ad/Bd/gd lists used
+  kin_incr_n40.npz   Control/MPC/mpc_increment_kinematics_pred_matrix.py:150-279 +
+                     Vehicle_Kinematics.get_kinematics_model
+  linearise.npz      Vehicle_Dynamics.get_dynamics_model at 48 seeded (x, u), incl. the
+                     low-speed guard branch (vehicle_models.py:143-159)
+"""
+import io
+import json
+import os
+import sys
+import types
+import contextlib
+
+import numpy as np
+
+os.environ.setdefault("MPLBACKEND", "Agg")
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+captured = []
+
+
+class _CaptureOSQP:
+    def setup(self, P, q, A, l, u, **kw):
+        captured.append(dict(kind="setup", P=P.tocsc(), q=np.array(q, float), A=A.tocsc(),
+                             l=np.array(l, float), u=np.array(u, float), kw=kw))
+        self._n = P.shape[0]
+
+    def update(self, **kw):
+        captured.append(dict(kind="update", **{k: np.array(v, float) for k, v in kw.items()}))
+
+    def solve(self):
+        x = np.zeros(self._n)
+        return types.SimpleNamespace(x=x, y=None, info=types.SimpleNamespace(status="solved", iter=0))
+
+
+def _install_stub():
+    mod = types.ModuleType("osqp")
+    mod.OSQP = _CaptureOSQP
+    sys.modules["osqp"] = mod
+    sys.path.insert(0, os.path.join(REF, "Control", "MPC"))
+    sys.path.insert(0, os.path.join(REF, "Vehicle_Dynamics"))
+
+
+def _csc(prefix, M, d):
+    M = M.tocsc()
+    M.sort_indices()
+    d[prefix + "_indptr"] = M.indptr.astype(np.int32)
+    d[prefix + "_indices"] = M.indices.astype(np.int32)
+    d[prefix + "_data"] = M.data.astype(np.float64)
+    d[prefix + "_shape"] = np.array(M.shape, np.int64)
+
+
+def _save(name, d):
+    np.savez_compressed(os.path.join(OUT, name), **d)
+    print("wrote", name, {k: v.shape for k, v in d.items()})
+
+
+def slack():
+    src = open(os.path.join(REF, "vehicle_lateral_mpc_slack_increment.py")).read()
+    src = src.replace("N = 100", "N = 20").replace("nsim = 1500", "nsim = 902")
+    src = src.split("# Plot result")[0]
+    captured.clear()
+    g = {"__name__": "slack"}
+    with contextlib.redirect_stdout(io.StringIO()):
+        exec(compile(src, "vehicle_lateral_mpc_slack_increment.py", "exec"), g)
+    setup = [c for c in captured if c["kind"] == "setup"][0]
+    ups = [c for c in captured if c["kind"] == "update"]
+    # each loop step i makes two updates: (q,l,u) at :237 then (l,u) at :269
+    d = {}
+    _csc("P", setup["P"], d)
+    _csc("A", setup["A"], d)
+    d.update(q=setup["q"], l=setup["l"], u=setup["u"])
+    steps = [0, 401, 901]
+    d["steps"] = np.array(steps)
+    d["upd_q"] = np.stack([ups[2 * i]["q"] for i in steps])
+    d["upd_l"] = np.stack([ups[2 * i]["l"] for i in steps])
+    d["upd_u"] = np.stack([ups[2 * i]["u"] for i in steps])
+    d["settings"] = np.array(json.dumps(setup["kw"]))
+    _save("slack_n20.npz", d)
+
+
+def vanilla():
+    import scipy.sparse as sparse
+    import mpc_kinematics
+    Ad = np.array([[0.960, -0.019, 0., 0.], [0.00469, 0.961, 0., 0.], [0., 0.0196, 1., 0.], [0.163, 0., 0.166, 1.]])
+    Bd = np.array([[0.020575], [0.115], [0.001157], [0.00182]])
+    N = 20
+    Q = sparse.diags([5., 5., 10., 10.])
+    R = 10 * sparse.eye(1)
+    xmin = np.array([-np.pi, -0.5 * np.pi, -15 * np.pi / 180, -10.])
+    xmax = np.array([np.pi, 0.5 * np.pi, 15 * np.pi / 180, 10.])
+    umin = np.array([-30 * np.pi / 180])
+    umax = np.array([30 * np.pi / 180])
+    rng = np.random.default_rng(2)
+    d = {}
+    qs, ls, us, x0s = [], [], [], []
+    for t in range(4):
+        x0 = np.array([0., 0., 5 * np.pi / 180, 3.]) if t == 0 else np.array(
+            [rng.uniform(-.05, .05), rng.uniform(-.1, .1), np.deg2rad(rng.uniform(-10, 10)), rng.uniform(-3, 3)])
+        captured.clear()
+        mpc_kinematics.mpc(Ad, Bd, np.zeros((4, 1)), x0.copy(), np.zeros((4, N + 1)), Q, Q, R, N, xmin, xmax, umin, umax)
+        s = captured[-1]
+        if t == 0:
+            _csc("P", s["P"], d)
+            _csc("A", s["A"], d)
+            d["settings"] = np.array(json.dumps(s["kw"]))
+        qs.append(s["q"]); ls.append(s["l"]); us.append(s["u"]); x0s.append(x0)
+    d.update(q=np.stack(qs), l=np.stack(ls), u=np.stack(us), x0=np.stack(x0s),
+             Ad=Ad, Bd=Bd, Q=np.diag([5., 5., 10., 10.]), R=np.array([[10.]]), xmin=xmin, xmax=xmax,
+             umin=umin, umax=umax)
+    _save("vanilla_n20.npz", d)
+
+
+def dyn_incr():
+    import scipy.sparse as sparse
+    import mpc_dynamics
+    import vehicle_models
+    veh = vehicle_models.Vehicle_Dynamics(m=1300, l_f=1.25, l_r=1.40, width=1.78, length=4.25, turning_circle=10.4,
+                                          C_d=0.34, A_f=2.0, C_roll=0.015, dt=0.05)
+    N = 50
+    Q = sparse.diags([100.0, 100.0, 100.0, 50.0, 50.0, 50.0])
+    QN = sparse.diags([1000.0, 1000.0, 1000.0, 500.0, 500.0, 500.0])
+    R = sparse.diags([50, 50])
+    del_umin = np.array([-np.deg2rad(2.0), -0.5])
+    del_umax = np.array([np.deg2rad(2.0), 0.5])
+    xmin_t = np.array([-np.inf, -np.inf, -2 * np.pi, -100., -30., -0.5 * np.pi, -np.deg2rad(15), -3.])
+    xmax_t = np.array([np.inf, np.inf, 2 * np.pi, 100., 30., 0.5 * np.pi, np.deg2rad(15), 1.])
+    rng = np.random.default_rng(5)
+    d = {}
+    recs = {k: [] for k in ("q", "l", "u", "Px", "Ax", "Ad", "Bd", "gd", "xt0", "Xr")}
+    for t in range(3):
+        x0 = np.array([0., 0., rng.uniform(-np.pi / 8, np.pi / 8), rng.uniform(5, 25), rng.uniform(-.5, .5),
+                       rng.uniform(-.2, .2)])
+        u0 = np.array([np.deg2rad(rng.uniform(-5, 5)), rng.uniform(-1, 1)])
+        yoff = rng.uniform(-4, 4)
+        # zero-increment rollout (mpc_dynamics.py:506-514)
+        Ads, Bds, gds = [], [], []
+        xk = x0.reshape(6, 1).copy()
+        uk = u0.reshape(2, 1).copy()
+        for k in range(N):
+            Ad, Bd, gd = veh.get_dynamics_model(xk.copy(), uk.copy())
+            Ads.append(Ad); Bds.append(Bd); gds.append(gd)
+            xk = Ad @ xk + Bd @ uk + gd
+        Xr = np.zeros((6, N + 1))
+        Xr[0] = np.arange(N + 1) * 10.0 * 0.05
+        Xr[1] = yoff
+        Xr[3] = 10.0
+        xt = np.concatenate([x0, u0])
+        captured.clear()
+        with contextlib.redirect_stdout(io.StringIO()):
+            try:
+                mpc_dynamics.mpc_increment(Ads, Bds, gds, xt.copy(), Xr, np.zeros((8, N + 1)), np.zeros((2, N + 1)),
+                                           Q, QN, R, N, xmin_t, xmax_t, del_umin, del_umax)
+            except Exception:
+                pass  # the stub's zero solution is parsed after setup; only the setup data is needed
+        s = [c for c in captured if c["kind"] == "setup"][-1]
+        if t == 0:
+            _csc("P", s["P"], d)
+            _csc("A", s["A"], d)
+            d["settings"] = np.array(json.dumps(s["kw"]))
+        P = s["P"].tocsc(); P.sort_indices()
+        A = s["A"].tocsc(); A.sort_indices()
+        recs["Px"].append(P.data); recs["Ax"].append(A.data)
+        recs["q"].append(s["q"]); recs["l"].append(s["l"]); recs["u"].append(s["u"])
+        recs["Ad"].append(np.stack(Ads)); recs["Bd"].append(np.stack(Bds)); recs["gd"].append(np.stack(gds))
+        recs["xt0"].append(xt); recs["Xr"].append(Xr)
+    for k, v in recs.items():
+        d[k] = np.stack(v)
+    d.update(Q=np.diag([100.0, 100.0, 100.0, 50.0, 50.0, 50.0]), QN=np.diag([1000.0, 1000.0, 1000.0, 500.0, 500.0, 500.0]),
+             R=np.diag([50., 50.]), del_umin=del_umin, del_umax=del_umax, xmin_t=xmin_t, xmax_t=xmax_t)
+    _save("dyn_incr_n50.npz", d)
+
+
+def kin_incr():
+    import scipy.sparse as sparse
+    import mpc_increment_kinematics_pred_matrix as mk
+    import vehicle_models
+    veh = vehicle_models.Vehicle_Kinematics(l_f=1.25, l_r=1.40, dt=0.02)
+    N = 40
+    del_umin = np.array([-np.deg2rad(0.5), -0.5])
+    del_umax = np.array([np.deg2rad(0.5), 0.5])
+    xmin_t = np.array([-np.inf, -np.inf, -100., -2 * np.pi, -np.deg2rad(15), -3.])
+    xmax_t = np.array([np.inf, np.inf, 100., 2 * np.pi, np.deg2rad(15), 1.])
+    Q = sparse.diags([50.0, 50.0, 10.0, 50.0])
+    QN = sparse.diags([1000.0, 1000.0, 100.0, 1000.0])
+    R = sparse.diags([100, 100])
+    x0 = np.array([0.0, 0.5, 20.0, np.deg2rad(3.0)])
+    u0 = np.array([np.deg2rad(1.0), 0.01])
+    Ads, Bds, gds = [], [], []
+    xk, uk = x0.copy(), u0.copy()
+    for k in range(N):
+        A_, B_, C_ = veh.get_kinematics_model(xk.copy(), uk.copy())
+        Ads.append(A_); Bds.append(B_); gds.append(C_)
+        xk = A_ @ xk + B_ @ uk + C_[:, 0]
+    Xr = np.zeros((4, N + 1))
+    Xr[0] = np.arange(N + 1) * 20.0 * 0.02
+    Xr[2] = 20.0
+    captured.clear()
+    with contextlib.redirect_stdout(io.StringIO()):
+        try:
+            mk.mpc_increment(Ads, Bds, gds, np.concatenate([x0, u0]), Xr, np.zeros((6, N + 1)), np.zeros((2, N + 1)),
+                             Q, QN, R, N, xmin_t, xmax_t, del_umin, del_umax)
+        except Exception:
+            pass
+    s = [c for c in captured if c["kind"] == "setup"][-1]
+    d = {}
+    _csc("P", s["P"], d)
+    _csc("A", s["A"], d)
+    d.update(q=s["q"], l=s["l"], u=s["u"], settings=np.array(json.dumps(s["kw"])),
+             Ad=np.stack(Ads), Bd=np.stack(Bds), gd=np.stack(gds), xt0=np.concatenate([x0, u0]), Xr=Xr)
+    _save("kin_incr_n40.npz", d)
+
+
+def linearise():
+    import vehicle_models
+    veh = vehicle_models.Vehicle_Dynamics(m=1300, l_f=1.25, l_r=1.40, width=1.78, length=4.25, turning_circle=10.4,
+                                          C_d=0.34, A_f=2.0, C_roll=0.015, dt=0.05)
+    rng = np.random.default_rng(7)
+    X, U, Ad, Bd, gd, Xg, Ug = [], [], [], [], [], [], []
+    for t in range(48):
+        vx = rng.uniform(5, 25) if t < 40 else [0.1, 0.4, -0.2, -0.45, 0.0, 0.49, -0.01, 0.3][t - 40]
+        x = np.array([[rng.uniform(-5, 5)], [rng.uniform(-5, 5)], [rng.uniform(-np.pi, np.pi)], [vx],
+                      [rng.uniform(-.5, .5)], [rng.uniform(-.2, .2)]])
+        u = np.array([[np.deg2rad(rng.uniform(-10, 10))], [rng.uniform(-2, 2)]])
+        xc, uc = x.copy(), u.copy()
+        with contextlib.redirect_stdout(io.StringIO()):
+            A_, B_, g_ = veh.get_dynamics_model(xc, uc)
+        X.append(x[:, 0]); U.append(u[:, 0]); Ad.append(A_); Bd.append(B_); gd.append(g_[:, 0])
+        Xg.append(xc[:, 0]); Ug.append(uc[:, 0])  # state after the in-place low-speed guard
+    _save("linearise.npz", dict(x=np.stack(X), u=np.stack(U), Ad=np.stack(Ad), Bd=np.stack(Bd), gd=np.stack(gd),
+                                x_guarded=np.stack(Xg), u_guarded=np.stack(Ug), dt=np.array(0.05)))
+
+
+if __name__ == "__main__":
+    _install_stub()
+    slack()
+    vanilla()
+    dyn_incr()
+    kin_incr()
+    linearise()

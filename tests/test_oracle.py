@@ -1,0 +1,132 @@
+"""Pin the CPU oracle (oracle/osqp_oracle.c) before trusting it.  CPU only.
+
+OSQP itself is not available offline, so OSQP-iterate parity
+is unpinned; the oracle is pinned by
+  (1) the reference's own QP data (tests/golden/, captured from its builders),
+  (2) KKT optimality certificates of its tight-eps solutions -- independent of
+      how ADMM got there (stationarity, primal feasibility, complementarity),
+  (3) an independent dense numpy restatement (tests/osqp_dense_ref.py) that must
+      reproduce its iterates: same status, same iteration count, x to ~1e-9.
+"""
+import json
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import pyoracle
+from osqp_dense_ref import solve as dense_solve
+
+FIXTURES = ["vanilla_n20.npz", "slack_n20.npz", "dyn_incr_n50.npz", "kin_incr_n40.npz"]
+
+
+def instances(golden, name):
+    g = golden(name)
+    s = json.loads(str(g["settings"]))
+    if g["q"].ndim == 1:
+        yield g["P"], g["q"], g["A"], g["l"], g["u"], s
+        return
+    for t in range(g["q"].shape[0]):
+        P, A = g["P"], g["A"]
+        if "Px" in g:
+            P = P.copy(); P.data = g["Px"][t].copy()
+            A = A.copy(); A.data = g["Ax"][t].copy()
+        yield P, g["q"][t], A, g["l"][t], g["u"][t], s
+
+
+def kkt_residuals(P, q, A, l, u, x, y):
+    Pf = sp.triu(P) + sp.triu(P, 1).T
+    Ax = A @ x
+    stat = np.abs(Pf @ x + q + A.T @ y).max()
+    feas = max(0.0, (Ax - u).max(), (l - Ax).max())
+    # complementarity: y_i > 0 only at the upper bound, y_i < 0 only at the lower bound
+    comp = max(np.abs(np.minimum(y, 0) * np.minimum(np.abs(Ax - l), 1e3)).max(),
+               np.abs(np.maximum(y, 0) * np.minimum(np.abs(u - Ax), 1e3)).max())
+    return stat, feas, comp
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_oracle_tight_eps_kkt(golden, name):
+    for P, q, A, l, u, s in instances(golden, name):
+        o = pyoracle.OSQP()
+        o.setup(P, q, A, l, u, eps_abs=1e-9, eps_rel=1e-9, max_iter=200000)
+        r = o.solve()
+        assert r.info.status == "solved"
+        stat, feas, comp = kkt_residuals(P, q, A, l, u, r.x, r.y)
+        scale = max(1.0, np.abs(q).max(), np.abs(r.y).max())
+        assert stat < 1e-6 * scale, stat
+        assert feas < 1e-6, feas
+        assert comp < 1e-5 * scale, comp
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_oracle_default_eps_near_optimum(golden, name):
+    """At the reference's eps (1e-3) the solution is within a loose ball of the tight one."""
+    for P, q, A, l, u, s in instances(golden, name):
+        s = {k: v for k, v in s.items() if k != "verbose"}
+        o = pyoracle.OSQP(); o.setup(P, q, A, l, u, **s); r = o.solve()
+        t = pyoracle.OSQP(); t.setup(P, q, A, l, u, eps_abs=1e-9, eps_rel=1e-9, max_iter=200000); rt = t.solve()
+        assert r.info.status == "solved"
+        assert r.info.iter % 25 == 0
+        assert np.abs(r.x - rt.x).max() < 0.1 * max(1.0, np.abs(rt.x).max())
+
+
+@pytest.mark.parametrize("name", ["vanilla_n20.npz", "slack_n20.npz", "kin_incr_n40.npz"])
+def test_oracle_matches_dense_restatement(golden, name):
+    for P, q, A, l, u, s in instances(golden, name):
+        o = pyoracle.OSQP(); o.setup(P, q, A, l, u, warm_start=False, adaptive_rho_interval=100); r = o.solve()
+        Pd = P.toarray(); Ad = A.toarray()
+        x, y, st, k, nr = dense_solve(Pd, q, Ad, l, u)
+        assert st == "solved" and r.info.status == "solved"
+        assert k == r.info.iter and nr == r.info.rho_updates
+        assert np.abs(r.x - x).max() < 1e-8 * max(1, np.abs(x).max())
+        assert np.abs(r.y - y).max() < 1e-6 * max(1, np.abs(y).max())
+
+
+def test_oracle_update_and_warm_start(golden):
+    """update(q,l,u) rescales with the setup-time scaling; warm start keeps iterates
+    (slack script :237,248,269)."""
+    g = golden("slack_n20.npz")
+    o = pyoracle.OSQP(); o.setup(g["P"], g["q"], g["A"], g["l"], g["u"], warm_start=True)
+    r0 = o.solve()
+    o.update(q=g["upd_q"][1], l=g["upd_l"][1], u=g["upd_u"][1])
+    r1 = o.solve()
+    f = pyoracle.OSQP(); f.setup(g["P"], g["upd_q"][1], g["A"], g["upd_l"][1], g["upd_u"][1], warm_start=False)
+    rf = f.solve()
+    assert r1.info.status == rf.info.status == "solved"
+    stat, feas, comp = kkt_residuals(g["P"], g["upd_q"][1], g["A"], g["upd_l"][1], g["upd_u"][1], r1.x, r1.y)
+    assert feas < 1e-2
+    # a solve right after a solve from the same (converged) point terminates at the first check
+    r2 = o.solve()
+    assert r2.info.iter == 25
+
+
+def test_oracle_infeasibility_detection():
+    P = sp.csc_matrix(np.eye(2)); q = np.zeros(2)
+    A = sp.csc_matrix(np.array([[1.0, 0.0], [1.0, 0.0], [0.0, 1.0]]))
+    o = pyoracle.OSQP(); o.setup(P, q, A, np.array([-np.inf, 1.0, -1.0]), np.array([-1.0, np.inf, 1.0]))
+    r = o.solve()
+    assert r.info.status == "primal infeasible"
+    assert np.isnan(r.x).all()
+    c = r.prim_inf_cert
+    assert np.abs(c).max() == pytest.approx(1.0)
+    Pz = sp.csc_matrix((2, 2))
+    o = pyoracle.OSQP(); o.setup(Pz, np.array([-1.0, 0.0]), sp.csc_matrix(np.eye(2)), np.array([0.0, -1.0]),
+                                 np.array([np.inf, 1.0]))
+    assert o.solve().info.status == "dual infeasible"
+
+
+def test_oracle_nonconvex_rejected():
+    P = sp.csc_matrix(np.array([[1.0, 0.0], [0.0, -1.0]]))
+    o = pyoracle.OSQP()
+    with pytest.raises(ValueError):
+        o.setup(P, np.zeros(2), sp.csc_matrix(np.eye(2)), -np.ones(2), np.ones(2))
+
+
+def test_oracle_batch_helper_threads(golden):
+    from osqp_amd import mpc
+    b = mpc.make_batch(2, B=64)
+    r1 = pyoracle.solve_batch(b["P"], b["A"], b["Px"], b["q"], b["Ax"], b["l"], b["u"], nthreads=1)
+    r4 = pyoracle.solve_batch(b["P"], b["A"], b["Px"], b["q"], b["Ax"], b["l"], b["u"], nthreads=4)
+    assert (r1.status_val == 1).all()
+    assert np.array_equal(r1.x, r4.x) and np.array_equal(r1.iter, r4.iter)
