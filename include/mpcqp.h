@@ -128,6 +128,14 @@ int mpcqp_synchronize(mpcqp_handle *h);
  * solve on the handle's stream: milliseconds, or -1 when unavailable. */
 double mpcqp_last_kernel_ms(mpcqp_handle *h);
 
+/* Kernel timing for bench.py's roofline: while enabled, every *_device setup /
+ * solve launch is bracketed by a hipEvent pair on its stream (no host sync).
+ * mpcqp_timing_read() waits for the recorded events, returns the summed
+ * kernel milliseconds and launch counts, and clears the record. */
+int mpcqp_timing(mpcqp_handle *h, int32_t enable);
+int mpcqp_timing_read(mpcqp_handle *h, double *setup_ms, int32_t *n_setup, double *solve_ms,
+                      int32_t *n_solve);
+
 int mpcqp_get_plan_info(const mpcqp_handle *h, mpcqp_plan_info *info);
 void mpcqp_free(mpcqp_handle *h);
 const char *mpcqp_last_error(void);

@@ -68,6 +68,8 @@ struct mpcqp_handle {
     std::vector<Shard> shards;
     bool timed = false;
     double last_ms = -1.0;
+    bool collect = false;   // record hipEvent pairs around device launches
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_setup, ev_solve;
 };
 
 namespace {
@@ -413,13 +415,30 @@ int mpcqp_create(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi, con
 
 static hipStream_t pick(Shard& s, void* stream) { return stream ? (hipStream_t)stream : s.stream; }
 
+static int ev_begin(mpcqp_handle* h, std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, hipStream_t st) {
+    if (!h->collect) return 0;
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    HIPCHK(hipEventRecord(a, st));
+    v.push_back({a, b});
+    return 0;
+}
+static int ev_end(mpcqp_handle* h, std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, hipStream_t st) {
+    if (!h->collect || v.empty()) return 0;
+    HIPCHK(hipEventRecord(v.back().second, st));
+    return 0;
+}
+
 int mpcqp_setup_device(mpcqp_handle* h, const double* dPx, const double* dAx, const double* dq,
                        const double* dl, const double* du, void* stream) {
     if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "device entry points need a single-device handle");
     Shard& s = h->shards[0];
+    hipStream_t st = pick(s, stream);
     HIPCHK(hipSetDevice(s.dev));
-    HIPCHK(launch_setup(s.kp, s.B, dPx, dAx, dq, dl, du, pick(s, stream)));
-    return 0;
+    if (int e = ev_begin(h, h->ev_setup, st)) return e;
+    HIPCHK(launch_setup(s.kp, s.B, dPx, dAx, dq, dl, du, st));
+    return ev_end(h, h->ev_setup, st);
 }
 
 int mpcqp_update_device(mpcqp_handle* h, const double* dq, const double* dl, const double* du, void* stream) {
@@ -446,7 +465,9 @@ int mpcqp_solve_device(mpcqp_handle* h, double* dx, double* dy, int32_t* dstatus
     hipStream_t st = pick(s, stream);
     HIPCHK(hipSetDevice(s.dev));
     HIPCHK(hipEventRecord(s.ev0, st));
+    if (int e = ev_begin(h, h->ev_solve, st)) return e;
     HIPCHK(launch_solve(s.kp, s.B, dx, dy, 0, st));
+    if (int e = ev_end(h, h->ev_solve, st)) return e;
     HIPCHK(hipEventRecord(s.ev1, st));
     if (dstatus) HIPCHK(hipMemcpyAsync(dstatus, s.kp.status, sizeof(int) * s.B, hipMemcpyDeviceToDevice, st));
     if (diters) HIPCHK(hipMemcpyAsync(diters, s.kp.iter, sizeof(int) * s.B, hipMemcpyDeviceToDevice, st));
@@ -469,6 +490,41 @@ double mpcqp_last_kernel_ms(mpcqp_handle* h) {
     return ms;
 }
 
+static int drain(std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, double* total) {
+    double t = 0.0;
+    for (auto& e : v) {
+        float ms = 0.f;
+        HIPCHK(hipEventSynchronize(e.second));
+        HIPCHK(hipEventElapsedTime(&ms, e.first, e.second));
+        t += ms;
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
+    if (total) *total = t;
+    v.clear();
+    return 0;
+}
+
+int mpcqp_timing(mpcqp_handle* h, int32_t enable) {
+    if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "timing needs a single-device handle");
+    if (int e = hipSetDevice(h->shards[0].dev) == hipSuccess ? 0 : fail(MPCQP_EDEVICE, "hipSetDevice")) return e;
+    double t;
+    if (int e = drain(h->ev_setup, &t)) return e;
+    if (int e = drain(h->ev_solve, &t)) return e;
+    h->collect = enable != 0;
+    return 0;
+}
+
+int mpcqp_timing_read(mpcqp_handle* h, double* setup_ms, int32_t* n_setup, double* solve_ms, int32_t* n_solve) {
+    if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "timing needs a single-device handle");
+    HIPCHK(hipSetDevice(h->shards[0].dev));
+    if (n_setup) *n_setup = (int32_t)h->ev_setup.size();
+    if (n_solve) *n_solve = (int32_t)h->ev_solve.size();
+    if (int e = drain(h->ev_setup, setup_ms)) return e;
+    if (int e = drain(h->ev_solve, solve_ms)) return e;
+    return 0;
+}
+
 int mpcqp_get_plan_info(const mpcqp_handle* h, mpcqp_plan_info* info) {
     if (!h || !info) return fail(MPCQP_EINVAL, "NULL argument");
     info->n = h->n; info->m = h->m; info->nb = h->plan.nb; info->block = kS;
@@ -481,6 +537,11 @@ int mpcqp_get_plan_info(const mpcqp_handle* h, mpcqp_plan_info* info) {
 
 void mpcqp_free(mpcqp_handle* h) {
     if (!h) return;
+    if (!h->shards.empty() && hipSetDevice(h->shards[0].dev) == hipSuccess) {
+        double t;
+        drain(h->ev_setup, &t);
+        drain(h->ev_solve, &t);
+    }
     for (auto& s : h->shards) {
         (void)hipSetDevice(s.dev);
         if (s.stream) (void)hipStreamSynchronize(s.stream);

@@ -23,7 +23,7 @@ from types import SimpleNamespace
 import numpy as np
 import scipy.sparse as sparse
 
-__all__ = ["OSQP", "OSQPBatch", "constant", "STATUS", "lib", "LIB_PATH"]
+__all__ = ["OSQP", "OSQPBatch", "DeviceBatch", "constant", "STATUS", "lib", "LIB_PATH"]
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmpcqp.so")
 OSQP_INFTY = 1e30
@@ -115,6 +115,8 @@ def lib():
     L.mpcqp_last_kernel_ms.argtypes = [vp]
     L.mpcqp_last_kernel_ms.restype = C.c_double
     L.mpcqp_get_plan_info.argtypes = [vp, _P(_PlanInfo)]
+    L.mpcqp_timing.argtypes = [vp, C.c_int32]
+    L.mpcqp_timing_read.argtypes = [vp, dp, i32p, dp, i32p]
     L.mpcqp_free.argtypes = [vp]
     L.mpcqp_free.restype = None
     L.mpcqp_analyze.argtypes = [C.c_int32, C.c_int32, i32p, i32p, i32p, i32p,
@@ -371,3 +373,63 @@ class OSQP:
             rho_estimate=float(r.rho_estimate[0]))
         return SimpleNamespace(x=r.x[0], y=r.y[0], info=info, prim_inf_cert=r.prim_inf_cert[0],
                                dua_inf_cert=r.dual_inf_cert[0])
+
+
+class DeviceBatch:
+    """Device-resident batch on one GPU: inputs and outputs stay in HBM.
+
+    Thin wrapper over mpcqp_create / mpcqp_setup_device / mpcqp_solve_device for
+    callers that keep their data on the device (bench.py; a future on-device
+    QP assembly).  Arrays are any objects exposing
+    ``data_ptr()`` to contiguous float64 / int32 device memory on `device`
+    (e.g. torch tensors); this module never touches their contents.
+    P, A give the shared pattern (canonicalised like osqp-python; values ignored).
+    """
+
+    def __init__(self, P, A, B, device=0, **settings):
+        P, A = canonical_data(P, A)
+        self.n, self.m, self.B = P.shape[0], A.shape[0], int(B)
+        self.nnzP, self.nnzA = P.nnz, A.nnz
+        self._pattern = (np.ascontiguousarray(P.indptr, np.int32), np.ascontiguousarray(P.indices, np.int32),
+                         np.ascontiguousarray(A.indptr, np.int32), np.ascontiguousarray(A.indices, np.int32))
+        Pp, Pi, Ap, Ai = self._pattern
+        s = _make_settings(**settings)
+        h = C.c_void_p()
+        _check(lib().mpcqp_create(self.n, self.m, _ip(Pp), _ip(Pi), _ip(Ap), _ip(Ai), self.B, C.byref(s),
+                                  int(device), C.byref(h)), "create")
+        self._h = _Handle(h.value)
+
+    @staticmethod
+    def _ptr(t):
+        return None if t is None else C.c_void_p(t.data_ptr())
+
+    def setup(self, Px, Ax, q, l, u, stream=None):
+        _check(lib().mpcqp_setup_device(self._h.ptr, self._ptr(Px), self._ptr(Ax), self._ptr(q), self._ptr(l),
+                                        self._ptr(u), stream), "setup_device")
+
+    def update(self, q=None, l=None, u=None, stream=None):
+        _check(lib().mpcqp_update_device(self._h.ptr, self._ptr(q), self._ptr(l), self._ptr(u), stream),
+               "update_device")
+
+    def warm_start(self, x=None, y=None, stream=None):
+        _check(lib().mpcqp_warm_start_device(self._h.ptr, self._ptr(x), self._ptr(y), stream), "warm_start_device")
+
+    def solve(self, x=None, y=None, status=None, iters=None, stream=None):
+        _check(lib().mpcqp_solve_device(self._h.ptr, self._ptr(x), self._ptr(y), self._ptr(status),
+                                        self._ptr(iters), stream), "solve_device")
+
+    def synchronize(self):
+        _check(lib().mpcqp_synchronize(self._h.ptr), "synchronize")
+
+    def timing(self, enable=True):
+        _check(lib().mpcqp_timing(self._h.ptr, int(bool(enable))), "timing")
+
+    def timing_read(self):
+        sm = C.c_double(); so = C.c_double(); ns = C.c_int32(); no = C.c_int32()
+        _check(lib().mpcqp_timing_read(self._h.ptr, C.byref(sm), C.byref(ns), C.byref(so), C.byref(no)), "timing")
+        return dict(setup_ms=sm.value, n_setup=ns.value, solve_ms=so.value, n_solve=no.value)
+
+    def plan_info(self):
+        info = _PlanInfo()
+        _check(lib().mpcqp_get_plan_info(self._h.ptr, C.byref(info)), "plan_info")
+        return {f[0]: getattr(info, f[0]) for f in _PlanInfo._fields_}
