@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -86,7 +87,7 @@ int upload_plan(const Plan& pl, Shard& s) {
     std::vector<const std::vector<int>*> parts = {
         &pl.pad_var, &pl.acsc_ptr, &pl.acsc_row, &pl.acsc_v, &pl.acsr_ptr, &pl.acsr_col, &pl.acsr_v,
         &pl.psym_ptr, &pl.psym_col, &pl.psym_v, &pl.p_r, &pl.p_c, &pl.a_r, &pl.a_c,
-        &pl.asm_blk_ptr, &pl.asm_tgt, &pl.asm_term_ptr, &pl.term_a, &pl.term_b, &pl.term_r};
+        &pl.asm_blk_ptr, &pl.asm_tgt, &pl.asm_term_ptr, &pl.term_a, &pl.term_b, &pl.term_r, &pl.acsr_pos, &pl.gcol, &pl.grow};
     std::vector<size_t> offs;
     std::vector<int> flat;
     for (auto* v : parts) {
@@ -99,7 +100,8 @@ int upload_plan(const Plan& pl, Shard& s) {
     const int** dst[] = {&s.kp.pad_var, &s.kp.acsc_ptr, &s.kp.acsc_row, &s.kp.acsc_v, &s.kp.acsr_ptr,
                          &s.kp.acsr_col, &s.kp.acsr_v, &s.kp.psym_ptr, &s.kp.psym_col, &s.kp.psym_v,
                          &s.kp.p_r, &s.kp.p_c, &s.kp.a_r, &s.kp.a_c, &s.kp.asm_blk_ptr, &s.kp.asm_tgt,
-                         &s.kp.asm_term_ptr, &s.kp.term_a, &s.kp.term_b, &s.kp.term_r};
+                         &s.kp.asm_term_ptr, &s.kp.term_a, &s.kp.term_b, &s.kp.term_r, &s.kp.acsr_pos,
+                         &s.kp.gcol, &s.kp.grow};
     for (size_t i = 0; i < parts.size(); ++i) *dst[i] = s.dplan + offs[i];
     return 0;
 }
@@ -118,6 +120,8 @@ size_t workspace_bytes(const Plan& pl, long B, bool with_io) {
     for (int i = 0; i < 4; ++i) carve<double>(off, B);
     carve<signed char>(off, B * m);
     for (int i = 0; i < 4; ++i) carve<int>(off, B);
+    carve<long long>(off, B * kProfSlots);
+    carve<KParams>(off, 1);
     if (with_io) {
         carve<double>(off, B * pl.nnzP); carve<double>(off, B * pl.nnzA);
         carve<double>(off, B * n); carve<double>(off, B * m); carve<double>(off, B * m);
@@ -168,6 +172,9 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
     k.iter = (int*)(base + carve<int>(off, B));
     k.rho_upd = (int*)(base + carve<int>(off, B));
     k.err = (int*)(base + carve<int>(off, B));
+    k.prof = nullptr;
+    if (const char* ev = getenv("MPCQP_PHASE_PROF"); ev && ev[0] == '1')
+        k.prof = (long long*)(base + carve<long long>(off, B * kProfSlots));
     if (with_io) {
         s.in_Px = (double*)(base + carve<double>(off, B * pl.nnzP));
         s.in_Ax = (double*)(base + carve<double>(off, B * pl.nnzA));
@@ -177,7 +184,8 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
         s.out_x = (double*)(base + carve<double>(off, B * n));
         s.out_y = (double*)(base + carve<double>(off, B * m));
     }
-    k.n = pl.n; k.m = pl.m; k.nb = pl.nb; k.npad = pl.npad; k.nnzP = pl.nnzP; k.nnzA = pl.nnzA;
+    k.n = pl.n; k.m = pl.m; k.nb = pl.nb; k.npad = pl.npad; k.nnzP = pl.nnzP; k.nnzA = pl.nnzA; k.amax = pl.amax;
+    k.gk = pl.gather_k;
     const mpcqp_settings& st = h->set;
     k.sigma = st.sigma; k.alpha = st.alpha; k.eps_abs = st.eps_abs; k.eps_rel = st.eps_rel;
     k.eps_pinf = st.eps_prim_inf; k.eps_dinf = st.eps_dual_inf; k.rho0 = st.rho;
@@ -187,6 +195,10 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
     int interval = st.adaptive_rho_interval;
     if (st.adaptive_rho && interval == 0) interval = st.check_termination ? 4 * st.check_termination : 100;
     k.rho_interval = interval;
+    k.self = (const KParams*)(base + carve<KParams>(off, 1));
+    HIPCHK(hipMemcpy((void*)k.self, &k, sizeof(KParams), hipMemcpyHostToDevice));
+    if (solve_variant(k) < 0)
+        return fail(MPCQP_EUNSUPPORTED, "problem shape outside the solve kernel's instantiations (n=%d m=%d)", pl.n, pl.m);
     if (size_t lds = lds_solve_bytes(k); lds > 160 * 1024)
         return fail(MPCQP_EUNSUPPORTED, "problem needs %zu bytes of LDS per instance (> 160 KiB)", lds);
     return 0;
@@ -532,6 +544,17 @@ int mpcqp_get_plan_info(const mpcqp_handle* h, mpcqp_plan_info* info) {
     info->batch = h->B; info->n_devices = (int)h->shards.size();
     info->lds_bytes_solve = h->shards.empty() ? 0 : (int64_t)lds_solve_bytes(h->shards[0].kp);
     info->bytes_per_instance = (int64_t)(workspace_bytes(h->plan, 1, false));
+    return 0;
+}
+
+int mpcqp_debug_phase_times(mpcqp_handle* h, int64_t* out) {
+    if (!h || !out) return fail(MPCQP_EINVAL, "NULL argument");
+    for (auto& s : h->shards) {
+        if (!s.kp.prof) return fail(MPCQP_EINVAL, "phase timers not enabled (set MPCQP_PHASE_PROF=1 before create)");
+        HIPCHK(hipSetDevice(s.dev));
+        HIPCHK(hipStreamSynchronize(s.stream));
+        HIPCHK(hipMemcpy(out + s.b0 * kProfSlots, s.kp.prof, sizeof(int64_t) * s.B * kProfSlots, hipMemcpyDeviceToHost));
+    }
     return 0;
 }
 

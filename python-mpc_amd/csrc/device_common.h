@@ -1,0 +1,171 @@
+// device_common.h -- constants and wave/block primitives shared by the HIP kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace mpcqp {
+
+// OSQP 0.6 constants (constants.h of the published solver)
+#define OSQP_INFTY 1e30
+#define MIN_SCALING 1e-4
+#define MAX_SCALING 1e4
+#define RHO_MIN 1e-6
+#define RHO_MAX 1e6
+#define RHO_TOL 1e-4
+#define RHO_EQ_OVER_RHO_INEQ 1e3
+#define DIVISION_TOL (1.0 / OSQP_INFTY)
+
+constexpr int T = kThreads;
+
+// KParams seen through the constant address space.  Out-of-line device functions
+// get the device copy KParams::self (a kernel's by-value argument block would be
+// copied to scratch for them); re-qualifying that uniform address makes its field
+// reads scalar loads instead of per-lane flat loads into VGPRs.
+typedef __attribute__((address_space(4))) const KParams KPc;
+__device__ __forceinline__ KPc& kconst(const KParams* gp) {
+    const unsigned long long a = (unsigned long long)gp;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+    return *(KPc*)(((unsigned long long)hi << 32) | lo);
+}
+constexpr int S = kS;
+constexpr int SS = kS * kS;
+
+__device__ __forceinline__ double cmax(double a, double b) { return a > b ? a : b; }
+__device__ __forceinline__ double cmin(double a, double b) { return a < b ? a : b; }
+__device__ __forceinline__ double limit_scaling(double d) {
+    d = d < MIN_SCALING ? 1.0 : d;
+    return d > MAX_SCALING ? MAX_SCALING : d;
+}
+
+// DPP lane permutation of a double (two 32-bit moves; all lanes valid for the
+// controls used here).  CTRL: 0xB1 quad_perm[1,0,3,2], 0x4E quad_perm[2,3,0,1],
+// 0x141 row_half_mirror, 0x140 row_mirror.
+template <int CTRL>
+__device__ __forceinline__ double dpp(double v) {
+    int lo = __double2loint(v), hi = __double2hiint(v);
+    lo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, 0xF, 0xF, false);
+    hi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
+// sum over the 8 lanes of an aligned half-row (lanes 8r..8r+7), result in all 8
+__device__ __forceinline__ double reduce8(double v) {
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    v += dpp<0x141>(v);
+    return v;
+}
+
+// sum over the 16 lanes of a DPP row, result in all 16
+__device__ __forceinline__ double reduce16(double v) {
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    v += dpp<0x141>(v);
+    v += dpp<0x140>(v);
+    return v;
+}
+
+// DPP with a row mask: rows outside `RM` receive 0
+template <int CTRL, int RM>
+__device__ __forceinline__ double dpp_rows(double v) {
+    int lo = __double2loint(v), hi = __double2hiint(v);
+    lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, RM, 0xF, false);
+    hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, RM, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
+// sum over an aligned 32-lane half-wave; valid in its upper 16 lanes
+// (row_bcast:15 adds lane 15 of rows 0/2 into rows 1/3)
+__device__ __forceinline__ double reduce32_hi(double v) {
+    v = reduce16(v);
+    v += dpp_rows<0x142, 0xA>(v);
+    return v;
+}
+
+// Wave-wide reductions by DPP (rows of 16, then row_bcast:15 / row_bcast:31);
+// the result is read from lane 63 into a scalar register.
+template <int CTRL, int RM>
+__device__ __forceinline__ double dpp_keep(double v) {  // rows outside RM keep v
+    int lo = __double2loint(v), hi = __double2hiint(v);
+    lo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, RM, 0xF, false);
+    hi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, RM, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double lane63(double v) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 63),
+                            __builtin_amdgcn_readlane(__double2loint(v), 63));
+}
+__device__ __forceinline__ double wave_max(double v) {
+    v = cmax(v, dpp<0xB1>(v));
+    v = cmax(v, dpp<0x4E>(v));
+    v = cmax(v, dpp<0x141>(v));
+    v = cmax(v, dpp<0x140>(v));
+    v = cmax(v, dpp_keep<0x142, 0xA>(v));
+    v = cmax(v, dpp_keep<0x143, 0xC>(v));
+    return lane63(v);
+}
+__device__ __forceinline__ double wave_sum(double v) {
+    v = reduce16(v);
+    v += dpp_rows<0x142, 0xA>(v);
+    v += dpp_rows<0x143, 0xC>(v);
+    return lane63(v);
+}
+
+// block-wide max / sum of K values (OSQP c_max semantics per comparison)
+template <int K>
+__device__ __forceinline__ void block_max(double (&v)[K], double* red) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const double r = wave_max(v[k]);
+        if (lane == 0) red[wid * K + k] = r;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        v[k] = cmax(cmax(red[k], red[K + k]), cmax(red[2 * K + k], red[3 * K + k]));
+    __syncthreads();
+}
+
+// block-wide max of K values into out[0..K) (LDS), computed by threads k < K;
+// visible to every thread after the trailing barrier.  red needs 4*K slots.
+template <int K>
+__device__ __forceinline__ void block_max_to(const double (&v)[K], double* red, double* out) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, t = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const double r = wave_max(v[k]);
+        if (lane == 0) red[wid * K + k] = r;
+    }
+    __syncthreads();
+    if (t < K) out[t] = cmax(cmax(red[t], red[K + t]), cmax(red[2 * K + t], red[3 * K + t]));
+    __syncthreads();
+}
+
+template <int K>
+__device__ __forceinline__ void block_sum(double (&v)[K], double* red) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const double r = wave_sum(v[k]);
+        if (lane == 0) red[wid * K + k] = r;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = (red[k] + red[K + k]) + (red[2 * K + k] + red[3 * K + k]);
+    __syncthreads();
+}
+
+__device__ __forceinline__ bool block_any(bool f, int* flag) {
+    if (threadIdx.x == 0) *flag = 0;
+    __syncthreads();
+    if (f) *flag = 1;
+    __syncthreads();
+    bool r = *flag != 0;
+    __syncthreads();
+    return r;
+}
+
+}  // namespace mpcqp

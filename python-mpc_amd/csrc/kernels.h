@@ -6,7 +6,8 @@
 
 namespace mpcqp {
 
-constexpr int kThreads = 256;  // one workgroup (4 wavefronts) per QP instance
+constexpr int kThreads = 256;
+constexpr int kProfSlots = 8;  // factor, rhs, bt_solve, update, checks, tail, total cycles, total 100 MHz ticks  // one workgroup (4 wavefronts) per QP instance
 
 // status values (OSQP constants.h)
 enum : int {
@@ -24,16 +25,18 @@ enum : int {
 // Everything a kernel needs: plan (shared pattern, read-only) + per-instance
 // workspace (instance-major arrays) + settings.  Passed by value.
 struct KParams {
-    int n, m, nb, npad, nnzP, nnzA;
+    int n, m, nb, npad, nnzP, nnzA, amax, gk;
     // plan
     const int *pad_var, *acsc_ptr, *acsc_row, *acsc_v, *acsr_ptr, *acsr_col, *acsr_v;
     const int *psym_ptr, *psym_col, *psym_v, *p_r, *p_c, *a_r, *a_c;
-    const int *asm_blk_ptr, *asm_tgt, *asm_term_ptr, *term_a, *term_b, *term_r;
+    const int *asm_blk_ptr, *asm_tgt, *asm_term_ptr, *term_a, *term_b, *term_r, *acsr_pos, *gcol, *grow;
     // workspace
     double *Px, *Ax, *q, *D, *l, *u, *E, *x, *z, *y, *scal, *F, *H, *Si, *dyc, *dxc;
     double *obj, *pri, *dua, *rho_est;
     signed char* ct;
     int *status, *iter, *rho_upd, *err;
+    const struct KParams* self;  // device copy of this block (read by the out-of-line device functions)
+    long long* prof;  // optional per-instance phase timers (MPCQP_PHASE_PROF=1), kProfSlots each
     // settings
     double sigma, alpha, eps_abs, eps_rel, eps_pinf, eps_dinf, rho0, rho_tol;
     int max_iter, scaling, check_term, warm_start, adaptive_rho, rho_interval, scaled_term;
@@ -46,6 +49,7 @@ hipError_t launch_setup(const KParams& p, long B, const double* Px, const double
 hipError_t launch_update(const KParams& p, long B, const double* q, const double* l, const double* u,
                          hipStream_t st);
 hipError_t launch_warm(const KParams& p, long B, const double* x, const double* y, hipStream_t st);
+int solve_variant(const KParams& p);  // -1: no instantiation fits the plan
 hipError_t launch_solve(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st);
 
 }  // namespace mpcqp

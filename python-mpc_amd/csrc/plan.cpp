@@ -163,6 +163,8 @@ std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const
         int q = pl.acsr_ptr[r];
         for (auto& e : rows[r]) { pl.acsr_col[q] = pl.var_pad[e.first]; pl.acsr_v[q] = e.second; ++q; }
     }
+    for (int pc = 0; pc < pl.npad; ++pc) pl.max_col_nnz = std::max(pl.max_col_nnz, pl.acsc_ptr[pc + 1] - pl.acsc_ptr[pc]);
+    for (int r = 0; r < m; ++r) pl.max_row_nnz = std::max(pl.max_row_nnz, pl.acsr_ptr[r + 1] - pl.acsr_ptr[r]);
     // full symmetric P by padded row
     std::vector<std::vector<std::pair<int, int>>> prow(pl.npad);
     pl.p_r.resize(pl.nnzP);
@@ -220,6 +222,31 @@ std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const
         t = u;
     }
     for (int k = 0; k < pl.nb; ++k) pl.asm_blk_ptr[k + 1] += pl.asm_blk_ptr[k];
+    // A-pair terms address A values by their position in the padded-CSC order
+    // (the order the solve kernel keeps them in LDS)
+    std::vector<int> csc_pos(pl.nnzA);
+    for (int e = 0; e < pl.nnzA; ++e) csc_pos[pl.acsc_v[e]] = e;
+    for (size_t t = 0; t < pl.term_a.size(); ++t)
+        if (pl.term_r[t] >= 0) { pl.term_a[t] = csc_pos[pl.term_a[t]]; pl.term_b[t] = csc_pos[pl.term_b[t]]; }
+    for (size_t t = 0; t < pl.asm_tgt.size(); ++t)
+        if (pl.asm_tgt[t] >= SS) pl.amax = std::max(pl.amax, (int)((pl.asm_tgt[t] - SS) / kS) + 1);
+    pl.acsr_pos.resize(pl.nnzA);
+    for (int e = 0; e < pl.nnzA; ++e) pl.acsr_pos[e] = csc_pos[pl.acsr_v[e]];
+    pl.csc_pos = csc_pos;
+    // packed gather lists (16-bit value position | 16-bit vector index << 16), padded
+    // to kGS entries with (nnzA | 0): position nnzA holds a zero in the kernels' LDS copy
+    pl.gather_k = std::max(pl.max_col_nnz, pl.max_row_nnz);
+    if (pl.gather_k > kGS) return "unsupported sparsity: a row or column of A has more than 16 nonzeros";
+    if (pl.nnzA >= 65535 || m >= 65536 || pl.npad >= 65536) return "unsupported size: nnz(A), m and n must be < 65535";
+    const int pad = pl.nnzA;
+    pl.gcol.assign((size_t)pl.npad * kGS, pad);
+    for (int pc = 0; pc < pl.npad; ++pc)
+        for (int e = pl.acsc_ptr[pc], k = 0; e < pl.acsc_ptr[pc + 1]; ++e, ++k)
+            pl.gcol[(size_t)pc * kGS + k] = e | (pl.acsc_row[e] << 16);
+    pl.grow.assign((size_t)m * kGS, pad);
+    for (int r = 0; r < m; ++r)
+        for (int e = pl.acsr_ptr[r], k = 0; e < pl.acsr_ptr[r + 1]; ++e, ++k)
+            pl.grow[(size_t)r * kGS + k] = pl.acsr_pos[e] | (pl.acsr_col[e] << 16);
     return "";
 }
 

@@ -20,6 +20,7 @@
 namespace mpcqp {
 
 constexpr int kS = 32;  // block (tile) size
+constexpr int kGS = 16; // gather-list stride (max nonzeros per row / column of A)
 
 struct Plan {
     int n = 0, m = 0, nb = 0, npad = 0, nnzP = 0, nnzA = 0;
@@ -39,9 +40,18 @@ struct Plan {
     //   D_k (local index i*S+j)  and  E_k = K(block k, block k-1) (index S*S + i*S + j).
     // Targets of block k: asm_tgt[asm_blk_ptr[k] .. asm_blk_ptr[k+1]),
     // terms of target t: [asm_term_ptr[t], asm_term_ptr[t+1]).
-    // term: r >= 0  -> rho[r] * Ax[a] * Ax[b];  r == -1 -> Px[a].
+    // term: r >= 0  -> rho[r] * Acsc[a] * Acsc[b] (positions in the padded-CSC order);
+    //       r == -1 -> Px[a] (user order).
     std::vector<int> asm_blk_ptr, asm_tgt, asm_term_ptr, term_a, term_b, term_r;
+    std::vector<int> csc_pos;     // [nnzA] user value index -> padded-CSC position
+    std::vector<int> acsr_pos;    // [nnzA] CSR entry -> padded-CSC position of its value
     int max_level = 0;            // largest BFS level (diagnostic)
+    int max_row_nnz = 0, max_col_nnz = 0;
+    int gather_k = 0;             // max(max_row_nnz, max_col_nnz)
+    // packed gather lists: [npad*kGS] by padded column (A' w), [m*kGS] by row (A x):
+    // (position of the value in the padded-CSC order) | (vector index << 16), padding (nnzA | 0)
+    std::vector<int> gcol, grow;
+    int amax = 0;                 // max over k of (last nonzero local row of E_k) + 1: F_k rows / H_{k-1} cols
 };
 
 // Returns "" on success, otherwise an error message.

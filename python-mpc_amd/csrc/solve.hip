@@ -1,0 +1,914 @@
+// solve.hip -- the ADMM kernel (osqp_solve restated for MI355X / gfx950).
+//
+// One 256-thread workgroup (4 wavefronts) per QP instance, persistent over the
+// whole solve.  Work decomposition inside the workgroup:
+//   * thread t owns padded variables  pc = t + 256*s  (s < CS) and constraint
+//     rows  i = t + 256*s  (s < RS): x, x_prev, z, z_prev, y and delta_y live in
+//     its registers for the whole solve, with its row / column gather lists
+//     (<= KMAX entries, 16-bit indices) -- no global-memory traffic per iteration;
+//   * A is kept in LDS twice (padded-CSC order for A'w, CSR order for A x~);
+//   * the block-tridiagonal factor of K = P + sigma I + A' diag(rho) A (plan.h)
+//     is distributed over the 256 threads' registers when it has NB <= 16
+//     blocks of 32: thread (i = t/8, jg = t%8) holds elements [i][jg+8c],
+//     c < 4, of every F_k, H_k = F_{k+1}', S_k^{-1} tile; row sums of the tile
+//     mat-vecs use three DPP steps inside an 8-lane half-row.  Larger plans
+//     (NB = 0 instantiation) read the tiles from the per-instance workspace.
+// Per ADMM iteration: 2*nb + 1 workgroup barriers.
+//
+// Reference semantics: osqp_solve / update_xz_tilde / update_x / update_z /
+// update_y / update_info / check_termination / adapt_rho / store_solution of
+// OSQP 0.6 (the solver behind vehicle_lateral_mpc_slack_increment.py:248 and
+// Control/MPC/mpc_dynamics.py:396); oracle/osqp_oracle.c restates the same
+// algorithm on the CPU and tests/test_gpu_parity.py compares the two.
+#include <hip/hip_runtime.h>
+
+#include "device_common.h"
+
+namespace mpcqp {
+
+
+struct SLds {
+    double *Acsc, *Pv, *lo, *up, *qv;
+    double *w, *rb, *xt, *ys;        // per-iteration vectors (aliased by the factor scratch)
+    double *SP, *EK, *DK;            // factorisation scratch (3 tiles)
+    double* red;
+    double* res;                     // last update_info results (14 doubles)
+    long long* pacc;                 // phase timers (diagnostic)
+    signed char* ct;
+    int* flag;
+};
+
+__device__ __forceinline__ double rho_of(signed char t, double rho) {
+    return t < 0 ? RHO_MIN : (t > 0 ? RHO_EQ_OVER_RHO_INEQ * rho : rho);
+}
+
+// Assemble K's tiles for the current rho and factor them (block LDL'):
+//   S_0 = D_0,  F_k = E_k S_{k-1}^{-1},  S_k = D_k - F_k E_k',  H_{k-1} = F_k'
+// F_k, H_k, S_k^{-1} go to the per-instance workspace (Fg, Hg, Sg).
+// Returns false on a non-positive pivot (OSQP: "problem non convex").
+template <class KP>
+__device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, double* __restrict__ Fg,
+                          double* __restrict__ Hg, double* __restrict__ Sg) {
+    const int tid = threadIdx.x, i = tid >> 3, jg = tid & 7;
+    const int nb = p.nb;
+    bool ok = true;
+    double* SP = L.SP;
+    double* DK = L.DK;
+    double* EK = L.EK;
+#pragma unroll 1
+    for (int k = 0; k < nb; ++k) {
+        for (int e = tid; e < SS; e += T) { DK[e] = 0.0; EK[e] = 0.0; }
+        __syncthreads();
+        if (tid < S) DK[tid * S + tid] = p.pad_var[k * S + tid] >= 0 ? p.sigma : 1.0;
+        __syncthreads();
+        for (int t = p.asm_blk_ptr[k] + tid; t < p.asm_blk_ptr[k + 1]; t += T) {
+            double acc = 0.0;
+            for (int u = p.asm_term_ptr[t]; u < p.asm_term_ptr[t + 1]; ++u) {
+                const int r = p.term_r[u];
+                if (r < 0) acc += L.Pv[p.term_a[u]];
+                else acc += rho_of(L.ct[r], rho) * L.Acsc[p.term_a[u]] * L.Acsc[p.term_b[u]];
+            }
+            const int tg = p.asm_tgt[t];
+            if (tg < SS) DK[tg] += acc;
+            else EK[tg - SS] += acc;
+        }
+        __syncthreads();
+        if (k > 0) {
+            double f[4];
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) {
+                const int j = jg + 8 * cc;
+                double s = 0.0;
+#pragma unroll 4
+                for (int l = 0; l < S; ++l) s += EK[i * S + l] * SP[l * S + j];
+                f[cc] = s;
+            }
+            __syncthreads();  // every read of S_{k-1}^{-1} done: its tile now holds F_k
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) {
+                const int j = jg + 8 * cc;
+                SP[i * S + j] = f[cc];
+                Fg[(long)k * SS + i * S + j] = f[cc];
+                Hg[(long)(k - 1) * SS + j * S + i] = f[cc];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) {
+                const int j = jg + 8 * cc;
+                double s = 0.0;
+#pragma unroll 4
+                for (int l = 0; l < S; ++l) s += SP[i * S + l] * EK[j * S + l];
+                DK[i * S + j] -= s;
+            }
+            __syncthreads();
+        }
+        // in-place Gauss-Jordan inverse of the SPD tile
+#pragma unroll 1
+        for (int pv = 0; pv < S; ++pv) {
+            const double piv = DK[pv * S + pv];
+            const double colv = DK[i * S + pv];
+            double rowv[4];
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) rowv[cc] = DK[pv * S + jg + 8 * cc];
+            __syncthreads();
+            if (!(piv > 0.0)) ok = false;
+            const double d = 1.0 / piv;
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) {
+                const int j = jg + 8 * cc;
+                double v;
+                if (i == pv) v = (j == pv) ? d : rowv[cc] * d;
+                else if (j == pv) v = -colv * d;
+                else v = DK[i * S + j] - colv * (rowv[cc] * d);
+                DK[i * S + j] = v;
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) Sg[(long)k * SS + i * S + jg + 8 * cc] = DK[i * S + jg + 8 * cc];
+        double* t = SP; SP = DK; DK = t;  // S_k^{-1} becomes "previous"; F_k's tile is free
+        __syncthreads();
+    }
+    return ok;
+}
+
+// Register-resident factor.  F_k = E_k S_{k-1}^{-1} is nonzero only in the rows of
+// block k that couple to block k-1 (its first BFS level, local rows < A), and
+// H_{k-1} = F_k' only in those columns, so each thread keeps
+//   Si[k][4]  : S_k^{-1}[i][jg+8c],          (i, jg) = (t/8, t%8)
+//   F[k][A/8] : F_{k+1}[r][j],  A = 8 : (r, j) = (t/32, t%32);  A = 16: (t/16, t%16 + 16c)
+//   H[k][A/8] : H_k[i][jg+8c],  c < A/8
+// (A = 32 keeps the full tiles in the Si layout).
+template <int NB, int A>
+struct RegFactor {
+    static constexpr int NF = A == 32 ? 4 : A / 8;
+    double F[NB > 1 ? NB - 1 : 1][NF], H[NB > 1 ? NB - 1 : 1][NF], Si[NB > 0 ? NB : 1][4];
+    __device__ __forceinline__ void load(int nb, const double* Fg, const double* Hg, const double* Sg) {
+        const int tid = threadIdx.x, i = tid >> 3, jg = tid & 7;
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            if (k < nb) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) Si[k][c] = Sg[(long)k * SS + i * S + jg + 8 * c];
+            }
+            if (k + 1 < nb && k < NB - 1) {
+                const double* Fk = Fg + (long)(k + 1) * SS;
+                const double* Hk = Hg + (long)k * SS;
+#pragma unroll
+                for (int c = 0; c < NF; ++c) {
+                    if constexpr (A == 8) F[k][c] = Fk[(tid >> 5) * S + (tid & 31)];
+                    else if constexpr (A == 16) F[k][c] = Fk[(tid >> 4) * S + (tid & 15) + 16 * c];
+                    else F[k][c] = Fk[i * S + jg + 8 * c];
+                    H[k][c] = Hk[i * S + jg + 8 * c];
+                }
+            }
+        }
+    }
+};
+
+template <int N>
+__device__ __forceinline__ double dotn(const double (&a)[N], const double* v, int jg) {
+    double acc = a[0] * v[jg];
+#pragma unroll
+    for (int c = 1; c < N; ++c) acc += a[c] * v[jg + 8 * c];
+    return acc;
+}
+__device__ __forceinline__ double dot4(const double (&a)[4], const double* v, int jg) {
+    return (a[0] * v[jg] + a[1] * v[jg + 8]) + (a[2] * v[jg + 16] + a[3] * v[jg + 24]);
+}
+__device__ __forceinline__ double dot4g(const double* a, const double* v, int jg) {
+    return (a[jg] * v[jg] + a[jg + 8] * v[jg + 8]) + (a[jg + 16] * v[jg + 16] + a[jg + 24] * v[jg + 24]);
+}
+
+// xt = K^{-1} rb (rb is overwritten by the forward sweep).  2*nb - 1 barriers.
+template <int NB, int A>
+__device__ __forceinline__ void bt_solve(const KParams& p, const RegFactor<NB, A>& R, const double* Fg,
+                                         const double* Hg, const double* Sg, double* rb, double* xt) {
+    int opq = 0;
+    asm volatile("" : "+s"(opq));  // keep per-block LDS addresses out of the register budget
+    const int tid = threadIdx.x, i = tid >> 3, jg = (tid & 7) + opq;
+    const int nb = NB > 0 ? NB : p.nb;  // register variants are instantiated for their exact block count
+    if constexpr (NB > 0) {
+        // forward sweep w_k -= F_k w_{k-1}, fused with t_{k-1} = S_{k-1}^{-1} w_{k-1}
+#pragma unroll
+        for (int k = 1; k < NB; ++k) {
+            if (k < nb) {
+                const double* v = rb + (k - 1) * S;
+                const double s2 = reduce8(dot4(R.Si[k - 1], v, jg));
+                if constexpr (A == 8) {
+                    const int j = (tid & 31) + opq;
+                    const double s1 = reduce32_hi(R.F[k - 1][0] * v[j]);
+                    if ((tid & 31) == 31) rb[k * S + (tid >> 5)] -= s1;
+                } else if constexpr (A == 16) {
+                    const int j = (tid & 15) + opq;
+                    const double s1 = reduce16(R.F[k - 1][0] * v[j] + R.F[k - 1][1] * v[j + 16]);
+                    if ((tid & 15) == 0) rb[k * S + (tid >> 4)] -= s1;
+                } else {
+                    const double s1 = reduce8(dot4(R.F[k - 1], v, jg));
+                    if (jg == 0) rb[k * S + i] -= s1;
+                }
+                if ((tid & 7) == 0) xt[(k - 1) * S + i] = s2;
+                __syncthreads();
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            if (k == nb - 1) {
+                const double s2 = reduce8(dot4(R.Si[k], rb + k * S, jg));
+                if ((tid & 7) == 0) xt[k * S + i] = s2;
+            }
+        }
+        __syncthreads();
+        // backward sweep x_k = t_k - H_k x_{k+1}  (H_k reads only x_{k+1}[0, A))
+#pragma unroll
+        for (int k = NB - 2; k >= 0; --k) {
+            if (k <= nb - 2) {
+                const double s = reduce8(dotn(R.H[k], xt + (k + 1) * S, jg));
+                if ((tid & 7) == 0) xt[k * S + i] -= s;
+                __syncthreads();
+            }
+        }
+    } else {
+        for (int k = 1; k < nb; ++k) {
+            const double* v = rb + (k - 1) * S;
+            const double s1 = reduce8(dot4g(Fg + (long)k * SS + i * S, v, jg));
+            const double s2 = reduce8(dot4g(Sg + (long)(k - 1) * SS + i * S, v, jg));
+            if ((tid & 7) == 0) { rb[k * S + i] -= s1; xt[(k - 1) * S + i] = s2; }
+            __syncthreads();
+        }
+        {
+            const double s2 = reduce8(dot4g(Sg + (long)(nb - 1) * SS + i * S, rb + (nb - 1) * S, jg));
+            if ((tid & 7) == 0) xt[(nb - 1) * S + i] = s2;
+        }
+        __syncthreads();
+        for (int k = nb - 2; k >= 0; --k) {
+            const double s = reduce8(dot4g(Hg + (long)k * SS + i * S, xt + (k + 1) * S, jg));
+            if ((tid & 7) == 0) xt[k * S + i] -= s;
+            __syncthreads();
+        }
+    }
+}
+
+// Gather list of one column (A' w) or row (A x) of A: K packed entries
+// (value position in the padded-CSC copy of A in LDS | vector index << 16), padded
+// with the zero slot Acsc[nnzA] -- no per-entry branches, all 2K LDS reads in flight.
+template <int K>
+struct Gather {
+    unsigned e[K];
+    __device__ __forceinline__ void load(const int* list) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) e[k] = (unsigned)list[k];
+    }
+    __device__ __forceinline__ void clear(int zero_pos) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) e[k] = (unsigned)zero_pos;
+    }
+    // an opaque zero offset keeps the LDS addresses from being hoisted into
+    // registers across the ADMM loop
+    __device__ __forceinline__ double dot(const double* A, const double* vec) const {
+        int opq = 0;
+        asm volatile("" : "+s"(opq));
+        double t[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) t[k] = A[(e[k] & 0xFFFFu) + opq] * vec[(e[k] >> 16) + opq];
+#pragma unroll
+        for (int w = 1; w < K; w *= 2)
+#pragma unroll
+            for (int k = 0; k + w < K; k += 2 * w) t[k] += t[k + w];
+        return t[0];
+    }
+};
+
+struct Res {  // update_info results
+    double pri, dua, nz, nax, nq, naty, npx;    // termination (unscaled)
+    double rpri, rdua, rz, rax, rq, raty, rpx;  // rho estimate (scaled space)
+    __device__ __forceinline__ void save(double* d) const {
+        d[0] = pri; d[1] = dua; d[2] = nz; d[3] = nax; d[4] = nq; d[5] = naty; d[6] = npx;
+        d[7] = rpri; d[8] = rdua; d[9] = rz; d[10] = rax; d[11] = rq; d[12] = raty; d[13] = rpx;
+    }
+    __device__ __forceinline__ void restore(const double* d) {
+        pri = d[0]; dua = d[1]; nz = d[2]; nax = d[3]; nq = d[4]; naty = d[5]; npx = d[6];
+        rpri = d[7]; rdua = d[8]; rz = d[9]; rax = d[10]; rq = d[11]; raty = d[12]; rpx = d[13];
+    }
+};
+
+// LDS carve of the solve kernel (doubles unless noted):
+//   Acsc[nnzA] Pv[nnzP] lo[m] up[m] qv[npad] X[npad] Z[m]
+//   V = max(3 S*S, w[m] rb[npad] xt[npad] ys[m] dY[m])   (factor scratch aliases the vectors)
+//   red[128] res[16] pacc[8] ct[m bytes] flag
+// rb holds delta_x and dY delta_y of the last iteration after its update phase;
+// ys holds y whenever the out-of-line phases run.
+__host__ __device__ inline long solve_vlen(int m, int npad) {
+    const long a = 3L * m + 2L * npad, b = 3L * SS;
+    return a > b ? a : b;
+}
+
+struct SL2 {  // full carve (SLds + the solve-kernel-only arrays)
+    SLds L;
+    double *X, *Z, *dY;
+};
+
+template <class KP>
+__device__ __forceinline__ SL2 carve(const KP& p) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    SL2 c;
+    const int m = p.m, npad = p.npad;
+    c.L.Acsc = sm;
+    c.L.Pv = c.L.Acsc + p.nnzA + 1;  // Acsc[nnzA] = 0: gather padding
+    c.L.lo = c.L.Pv + p.nnzP;
+    c.L.up = c.L.lo + m;
+    c.L.qv = c.L.up + m;
+    c.X = c.L.qv + npad;
+    c.Z = c.X + npad;
+    double* V = c.Z + m;
+    c.L.w = V;
+    c.L.rb = c.L.w + m;
+    c.L.xt = c.L.rb + npad;
+    c.L.ys = c.L.xt + npad;
+    c.dY = c.L.ys + m;
+    c.L.SP = V;
+    c.L.EK = c.L.SP + SS;
+    c.L.DK = c.L.EK + SS;
+    c.L.red = V + solve_vlen(m, npad);
+    c.L.res = c.L.red + 128;
+    c.L.pacc = (long long*)(c.L.res + 16);
+    c.L.ct = (signed char*)(c.L.pacc + 8);
+    c.L.flag = (int*)(c.L.ct + ((m + 15) & ~15));
+    return c;
+}
+
+// LDS scalar slots (in res[14..15] and flag[1..]): shared outcome of the out-of-line phases
+struct Shared {
+    double* res;  // [0..13] Res, [14] obj, [15] new rho
+    int* flag;    // [0] scratch, [1] status, [2] dx_scaled, [3] dy_scaled
+};
+
+// ---- out-of-line phases: everything they need is in LDS or in the plan ----
+template <class KP>
+__device__ __forceinline__ double row_dot(const KP& p, const double* A, const double* v, int i) {
+    double acc = 0.0;
+    for (int e = p.acsr_ptr[i]; e < p.acsr_ptr[i + 1]; ++e) acc += A[p.acsr_pos[e]] * v[p.acsr_col[e]];
+    return acc;
+}
+template <class KP>
+__device__ __forceinline__ double col_dot(const KP& p, const double* A, const double* v, int pc) {
+    double acc = 0.0;
+    for (int e = p.acsc_ptr[pc]; e < p.acsc_ptr[pc + 1]; ++e) acc += A[e] * v[p.acsc_row[e]];
+    return acc;
+}
+template <class KP>
+__device__ __forceinline__ double psym_dot(const KP& p, const double* Pv, const double* v, int pc) {
+    double acc = 0.0;
+    for (int e = p.psym_ptr[pc]; e < p.psym_ptr[pc + 1]; ++e) acc += Pv[p.psym_v[e]] * v[p.psym_col[e]];
+    return acc;
+}
+
+// update_info: residuals and the norms of their tolerances (OSQP compute_pri_res /
+// compute_dua_res / compute_pri_tol / compute_dua_tol, scaled and unscaled)
+__device__ __noinline__ void update_info_nl(const KParams* gp, long b, double cinv) {
+    KPc& p = kconst(gp);
+    SL2 c = carve(p);
+    const int tid = threadIdx.x, m = p.m, npad = p.npad;
+    const double* Eg = p.E + b * m;
+    const double* Dg = p.D + b * npad;
+    double v[14];
+#pragma unroll
+    for (int k = 0; k < 14; ++k) v[k] = 0.0;
+    #pragma unroll 1
+    for (int i = tid; i < m; i += T) {
+        const double ax = row_dot(p, c.L.Acsc, c.X, i);
+        const double zi = c.Z[i];
+        const double pr = ax - zi;
+        const double ei = 1.0 / Eg[i];
+        v[0] = cmax(v[0], fabs(ei * pr));
+        v[2] = cmax(v[2], fabs(ei * zi));
+        v[3] = cmax(v[3], fabs(ei * ax));
+        v[7] = cmax(v[7], fabs(pr));
+        v[9] = cmax(v[9], fabs(zi));
+        v[10] = cmax(v[10], fabs(ax));
+    }
+    #pragma unroll 1
+    for (int pc = tid; pc < npad; pc += T) {
+        if (p.pad_var[pc] < 0) continue;
+        const double px = psym_dot(p, c.L.Pv, c.X, pc);
+        const double aty = col_dot(p, c.L.Acsc, c.L.ys, pc);
+        const double q = c.L.qv[pc];
+        const double d = (q + px) + aty;
+        const double di = 1.0 / Dg[pc];
+        v[1] = cmax(v[1], fabs(di * d));
+        v[4] = cmax(v[4], fabs(di * q));
+        v[5] = cmax(v[5], fabs(di * aty));
+        v[6] = cmax(v[6], fabs(di * px));
+        v[8] = cmax(v[8], fabs(d));
+        v[11] = cmax(v[11], fabs(q));
+        v[12] = cmax(v[12], fabs(aty));
+        v[13] = cmax(v[13], fabs(px));
+    }
+    double* r = c.L.red + 64;
+    block_max_to(v, c.L.red, r);
+    if (tid == 0) {
+        Res R;
+        if (p.scaling && !p.scaled_term) {
+            R.pri = r[0]; R.dua = cinv * r[1];
+            R.nz = r[2]; R.nax = r[3]; R.nq = r[4]; R.naty = r[5]; R.npx = r[6];
+        } else {
+            R.pri = r[7]; R.dua = r[8];
+            R.nz = r[9]; R.nax = r[10]; R.nq = r[11]; R.naty = r[12]; R.npx = r[13];
+        }
+        R.rpri = r[7]; R.rdua = r[8]; R.rz = r[9]; R.rax = r[10]; R.rq = r[11]; R.raty = r[12]; R.rpx = r[13];
+        if (m == 0) R.pri = 0.0;
+        R.save(c.L.res);
+    }
+    __syncthreads();
+}
+
+// is_primal_infeasible (delta_y in dY, projected in place as OSQP does)
+template <class KP>
+__device__ bool primal_infeasible(const KP& p, SL2& c, long b, double eps) {
+    const int tid = threadIdx.x, m = p.m, npad = p.npad;
+    const bool unscale = p.scaling && !p.scaled_term;
+    const double* Eg = p.E + b * m;
+    const double* Dg = p.D + b * npad;
+    double nd[1] = {0.0};
+    #pragma unroll 1
+    for (int i = tid; i < m; i += T) {
+        double d = c.dY[i];
+        if (c.L.up[i] > OSQP_INFTY * MIN_SCALING) d = (c.L.lo[i] < -OSQP_INFTY * MIN_SCALING) ? 0.0 : cmin(d, 0.0);
+        else if (c.L.lo[i] < -OSQP_INFTY * MIN_SCALING) d = cmax(d, 0.0);
+        c.dY[i] = d;
+        nd[0] = cmax(nd[0], fabs(unscale ? Eg[i] * d : d));
+    }
+    block_max(nd, c.L.red);
+    const double norm_dy = nd[0];
+    if (!(norm_dy > eps)) return false;
+    double sum[1] = {0.0};
+    #pragma unroll 1
+    for (int i = tid; i < m; i += T) sum[0] += c.L.up[i] * cmax(c.dY[i], 0.0) + c.L.lo[i] * cmin(c.dY[i], 0.0);
+    block_sum(sum, c.L.red);
+    if (!(sum[0] < eps * norm_dy)) return false;
+    double na[1] = {0.0};
+    #pragma unroll 1
+    for (int pc = tid; pc < npad; pc += T) {
+        if (p.pad_var[pc] < 0) continue;
+        double a = col_dot(p, c.L.Acsc, c.dY, pc);
+        if (unscale) a *= 1.0 / Dg[pc];
+        na[0] = cmax(na[0], fabs(a));
+    }
+    block_max(na, c.L.red);
+    return na[0] < eps * norm_dy;
+}
+
+// is_dual_infeasible (delta_x in rb)
+template <class KP>
+__device__ bool dual_infeasible(const KP& p, SL2& c, long b, double cs_, double eps) {
+    const int tid = threadIdx.x, m = p.m, npad = p.npad;
+    const bool unscale = p.scaling && !p.scaled_term;
+    const double* Eg = p.E + b * m;
+    const double* Dg = p.D + b * npad;
+    const double cs = unscale ? cs_ : 1.0;
+    double v[1] = {0.0}, sum[1] = {0.0};
+    #pragma unroll 1
+    for (int pc = tid; pc < npad; pc += T) {
+        if (p.pad_var[pc] < 0) continue;
+        const double dx = c.L.rb[pc];
+        v[0] = cmax(v[0], fabs(unscale ? Dg[pc] * dx : dx));
+        sum[0] += c.L.qv[pc] * dx;
+    }
+    block_max(v, c.L.red);
+    const double norm_dx = v[0];
+    if (!(norm_dx > eps)) return false;
+    block_sum(sum, c.L.red);
+    if (!(sum[0] < cs * eps * norm_dx)) return false;
+    double np[1] = {0.0};
+    #pragma unroll 1
+    for (int pc = tid; pc < npad; pc += T) {
+        if (p.pad_var[pc] < 0) continue;
+        double a = psym_dot(p, c.L.Pv, c.L.rb, pc);
+        if (unscale) a *= 1.0 / Dg[pc];
+        np[0] = cmax(np[0], fabs(a));
+    }
+    block_max(np, c.L.red);
+    if (!(np[0] < cs * eps * norm_dx)) return false;
+    bool viol = false;
+    #pragma unroll 1
+    for (int i = tid; i < m; i += T) {
+        double a = row_dot(p, c.L.Acsc, c.L.rb, i);
+        if (unscale) a *= 1.0 / Eg[i];
+        if ((c.L.up[i] < OSQP_INFTY * MIN_SCALING && a > eps * norm_dx) ||
+            (c.L.lo[i] > -OSQP_INFTY * MIN_SCALING && a < -eps * norm_dx))
+            viol = true;
+    }
+    return !block_any(viol, c.L.flag);
+}
+
+// check_termination on the Res in LDS; status / obj / certificate flags in LDS.
+__device__ __noinline__ int check_termination_nl(const KParams* gp, long b, double cval, double cinv,
+                                                 int approximate) {
+    KPc& p = kconst(gp);
+    SL2 c = carve(p);
+    Res R;
+    R.restore(c.L.res);
+    double eps_abs = p.eps_abs, eps_rel = p.eps_rel, eps_pinf = p.eps_pinf, eps_dinf = p.eps_dinf;
+    int st = MPCQP_UNSOLVED_;
+    double obj = c.L.res[14];
+    bool done = false;
+    if (R.pri > OSQP_INFTY || R.dua > OSQP_INFTY) {
+        st = MPCQP_NON_CVX_;
+        obj = __builtin_nan("");
+        done = true;
+    } else {
+        if (approximate) { eps_abs *= 10; eps_rel *= 10; eps_pinf *= 10; eps_dinf *= 10; }
+        bool prim_ok = false, dual_ok = false, prim_inf = false, dual_inf = false;
+        const bool unscale = p.scaling && !p.scaled_term;
+        if (p.m == 0) prim_ok = true;
+        else {
+            const double ep = eps_abs + eps_rel * cmax(R.nz, R.nax);
+            if (R.pri < ep) prim_ok = true;
+            else prim_inf = primal_infeasible(p, c, b, eps_pinf);
+        }
+        double mx = cmax(cmax(R.nq, R.naty), R.npx);
+        if (unscale) mx *= cinv;
+        if (R.dua < eps_abs + eps_rel * mx) dual_ok = true;
+        else dual_inf = dual_infeasible(p, c, b, cval, eps_dinf);
+        if (prim_ok && dual_ok) {
+            st = approximate ? MPCQP_SOLVED_INACCURATE_ : MPCQP_SOLVED_;
+            done = true;
+        } else if (prim_inf) {
+            st = approximate ? MPCQP_PRIMAL_INFEASIBLE_INACCURATE_ : MPCQP_PRIMAL_INFEASIBLE_;
+            obj = OSQP_INFTY;
+            if (threadIdx.x == 0) c.L.flag[3] = unscale;
+            done = true;
+        } else if (dual_inf) {
+            st = approximate ? MPCQP_DUAL_INFEASIBLE_INACCURATE_ : MPCQP_DUAL_INFEASIBLE_;
+            obj = -OSQP_INFTY;
+            if (threadIdx.x == 0) c.L.flag[2] = unscale;
+            done = true;
+        }
+    }
+    __syncthreads();
+    if (done && threadIdx.x == 0) { c.L.flag[1] = st; c.L.res[14] = obj; }
+    __syncthreads();
+    return done ? st : MPCQP_UNSOLVED_;
+}
+
+// compute_obj_val (needs X)
+__device__ __noinline__ void objective_nl(const KParams* gp, double cinv) {
+    KPc& p = kconst(gp);
+    SL2 c = carve(p);
+    const int tid = threadIdx.x;
+    double sacc[1] = {0.0};
+    #pragma unroll 1
+    for (int v = tid; v < p.nnzP; v += T) {
+        const int r = p.p_r[v], cc = p.p_c[v];
+        sacc[0] += (r == cc) ? 0.5 * c.L.Pv[v] * c.X[r] * c.X[r] : c.L.Pv[v] * c.X[r] * c.X[cc];
+    }
+    #pragma unroll 1
+    for (int pc = tid; pc < p.npad; pc += T) sacc[0] += c.L.qv[pc] * c.X[pc];
+    block_sum(sacc, c.L.red);
+    if (tid == 0) c.L.res[14] = p.scaling ? sacc[0] * cinv : sacc[0];
+    __syncthreads();
+}
+
+// store_solution + info (y is in ys)
+__device__ __noinline__ void finalize_nl(const KParams* gp, long b, double* __restrict__ xo,
+                                         double* __restrict__ yo, double cinv, double rho, int status,
+                                         int info_iter, int rho_updates) {
+    KPc& p = kconst(gp);
+    SL2 c = carve(p);
+    const int tid = threadIdx.x, n = p.n, m = p.m, npad = p.npad;
+    const double* Eg = p.E + b * m;
+    const double* Dg = p.D + b * npad;
+    Res R;
+    R.restore(c.L.res);
+    const double obj = c.L.res[14];
+    double rho_est;
+    {
+        const double pr = R.rpri / (cmax(R.rz, R.rax) + DIVISION_TOL);
+        const double du = R.rdua / (cmax(cmax(R.rq, R.raty), R.rpx) + DIVISION_TOL);
+        rho_est = cmin(cmax(rho * sqrt(pr / (du + DIVISION_TOL)), RHO_MIN), RHO_MAX);
+    }
+    const bool has_sol = !(status == MPCQP_PRIMAL_INFEASIBLE_ || status == MPCQP_PRIMAL_INFEASIBLE_INACCURATE_ ||
+                           status == MPCQP_DUAL_INFEASIBLE_ || status == MPCQP_DUAL_INFEASIBLE_INACCURATE_ ||
+                           status == MPCQP_NON_CVX_);
+    const bool pinf = status == MPCQP_PRIMAL_INFEASIBLE_ || status == MPCQP_PRIMAL_INFEASIBLE_INACCURATE_;
+    const bool dinf = status == MPCQP_DUAL_INFEASIBLE_ || status == MPCQP_DUAL_INFEASIBLE_INACCURATE_;
+    const bool dx_scaled = c.L.flag[2] != 0, dy_scaled = c.L.flag[3] != 0;
+    double nrm[2] = {0.0, 0.0};
+    #pragma unroll 1
+    for (int pc = tid; pc < npad; pc += T) {
+        double dx = c.L.rb[pc];
+        if (dx_scaled) dx *= Dg[pc];
+        c.L.rb[pc] = dx;
+        nrm[1] = cmax(nrm[1], fabs(dx));
+    }
+    #pragma unroll 1
+    for (int i = tid; i < m; i += T) {
+        double dy = c.dY[i];
+        if (dy_scaled) dy *= Eg[i];
+        c.dY[i] = dy;
+        nrm[0] = cmax(nrm[0], fabs(dy));
+    }
+    block_max(nrm, c.L.red);
+    #pragma unroll 1
+    for (int pc = tid; pc < npad; pc += T) {
+        const int j = p.pad_var[pc];
+        const double xv = c.X[pc];
+        if (j >= 0) {
+            if (xo) xo[b * n + j] = has_sol ? (p.scaling ? Dg[pc] * xv : xv) : __builtin_nan("");
+            p.dxc[b * n + j] = dinf ? c.L.rb[pc] * (1.0 / nrm[1]) : c.L.rb[pc];
+        }
+        p.x[b * npad + pc] = has_sol ? xv : 0.0;
+    }
+    #pragma unroll 1
+    for (int i = tid; i < m; i += T) {
+        const double yv = c.L.ys[i];
+        if (yo) yo[b * m + i] = has_sol ? (p.scaling ? (Eg[i] * yv) * cinv : yv) : __builtin_nan("");
+        p.dyc[b * m + i] = pinf ? c.dY[i] * (1.0 / nrm[0]) : c.dY[i];
+        p.y[b * m + i] = has_sol ? yv : 0.0;
+        p.z[b * m + i] = has_sol ? c.Z[i] : 0.0;
+    }
+    if (tid == 0) {
+        p.status[b] = status;
+        p.iter[b] = info_iter;
+        p.rho_upd[b] = rho_updates;
+        p.obj[b] = obj;
+        p.pri[b] = R.pri;
+        p.dua[b] = R.dua;
+        p.rho_est[b] = rho_est;
+        p.scal[b * 4 + 2] = rho;
+    }
+}
+
+__device__ __noinline__ bool factorize_nl(const KParams* gp, long b, double rho) {
+    KPc& p = kconst(gp);
+    SL2 c = carve(p);
+    return factorize(p, c.L, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
+                     p.Si + b * (long)p.nb * SS);
+}
+
+template <int NB, int A, int K, int CS, int RS, int W>
+__global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ xo, double* __restrict__ yo,
+                                                int factor_only) {
+    const int tid = threadIdx.x;
+    const long b = blockIdx.x;
+    const int n = p.n, m = p.m, npad = p.npad, nnzP = p.nnzP, nnzA = p.nnzA;
+    SL2 C = carve(p);
+    SLds& L = C.L;
+    double* X = C.X;
+    double* Z = C.Z;
+    double* dY = C.dY;
+    const double* Fg = p.F + b * (long)p.nb * SS;
+    const double* Hg = p.H + b * (long)p.nb * SS;
+    const double* Sg = p.Si + b * (long)p.nb * SS;
+
+    if (p.err[b]) {  // invalid data (flagged by setup/update): NaN outputs
+        for (int j = tid; j < n; j += T) if (xo) xo[b * n + j] = __builtin_nan("");
+        for (int i = tid; i < m; i += T) if (yo) yo[b * m + i] = __builtin_nan("");
+        if (tid == 0) p.status[b] = MPCQP_NON_CVX_;
+        return;
+    }
+
+    // optional phase timers (thread 0's shader clock; every phase ends at a barrier)
+#ifdef MPCQP_PHASE_PROF
+    long long tph = 0, t0c = 0, t0w = 0;
+    const bool prof = p.prof != nullptr;
+    if (prof) { t0w = wall_clock64(); t0c = tph = clock64(); if (tid < 8) L.pacc[tid] = 0; }
+#define PH(k) if (prof && tid == 0) { const long long t_ = clock64(); L.pacc[k] += t_ - tph; tph = t_; }
+#else
+#define PH(k)
+#endif
+
+    const double cval = p.scal[b * 4 + 0], cinv = p.scal[b * 4 + 1];
+    double rho = p.scal[b * 4 + 2];
+    const double sigma = p.sigma, alpha = p.alpha;
+    const bool warm = p.warm_start != 0;
+    for (int e = tid; e < nnzA; e += T) L.Acsc[e] = p.Ax[b * nnzA + p.acsc_v[e]];
+    if (tid == 0) L.Acsc[nnzA] = 0.0;  // the gather lists' padding slot
+    for (int v = tid; v < nnzP; v += T) L.Pv[v] = p.Px[b * nnzP + v];
+    for (int i = tid; i < m; i += T) {
+        L.lo[i] = p.l[b * m + i];
+        L.up[i] = p.u[b * m + i];
+        L.ct[i] = p.ct[b * m + i];
+        Z[i] = warm ? p.z[b * m + i] : 0.0;
+        dY[i] = 0.0;
+    }
+    for (int pc = tid; pc < npad; pc += T) {
+        L.qv[pc] = p.q[b * npad + pc];
+        X[pc] = warm ? p.x[b * npad + pc] : 0.0;
+    }
+    if (tid < 16) L.res[tid] = 0.0;
+    if (tid < 4) L.flag[tid] = 0;
+
+    int status = MPCQP_UNSOLVED_, rho_updates = 0, iter = 0, info_iter = 0;
+    bool can_check = false, need_factor = true;
+    // y stays in registers for the whole solve (ys is its LDS copy for the
+    // out-of-line phases; the factorisation scratch overwrites ys)
+    double y[RS];
+#pragma unroll
+    for (int s = 0; s < RS; ++s) {
+        const int i = tid + s * T;
+        y[s] = (i < m && warm) ? p.y[b * m + i] : 0.0;
+    }
+    PH(5)
+    // The solve alternates "runs" of ADMM iterations up to the next termination /
+    // rho-adaptation point (no calls, everything in registers and LDS) with the
+    // out-of-line phases.  The per-thread run state (factor tiles, gather lists)
+    // is re-derived at the start of every run, so it is not live across a call
+    // (the calling convention would otherwise spill it to scratch).
+    for (;;) {
+        __syncthreads();
+        if (need_factor) {  // start, and after a rho change
+            need_factor = false;
+            const bool ok = factorize_nl(p.self, b, rho);
+            if (!ok) {
+                if (iter == 0) {
+                    for (int j = tid; j < n; j += T) if (xo) xo[b * n + j] = __builtin_nan("");
+                    for (int i = tid; i < m; i += T) if (yo) yo[b * m + i] = __builtin_nan("");
+                    if (tid == 0) p.status[b] = MPCQP_NON_CVX_;
+                    return;
+                }
+                status = MPCQP_NON_CVX_;
+                can_check = true;  // skip the final check_termination
+                break;
+            }
+            if (factor_only) return;
+            PH(0)
+        }
+        // ---- run state ----
+        RegFactor<NB, A> RF;
+        if constexpr (NB > 0) RF.load(NB, Fg, Hg, Sg);
+        int cvar[CS];
+        Gather<K> cg[CS];
+#pragma unroll
+        for (int s = 0; s < CS; ++s) {
+            const int pc = tid + s * T;
+            cvar[s] = pc < npad ? p.pad_var[pc] : -1;
+            if (pc < npad) cg[s].load(p.gcol + (long)pc * kGS);
+            else cg[s].clear(nnzA);
+        }
+        Gather<K> rg[RS];
+#pragma unroll
+        for (int s = 0; s < RS; ++s) {
+            const int i = tid + s * T;
+            if (i < m) {
+                rg[s].load(p.grow + (long)i * kGS);
+                L.w[i] = rho_of(L.ct[i], rho) * Z[i] - y[s];  // w = rho z_prev - y (rho may be new)
+            } else {
+                rg[s].clear(nnzA);
+            }
+        }
+        // the run ends at the next termination check / rho adaptation / max_iter
+        int stop_at = p.max_iter;
+        if (p.check_term) stop_at = min(stop_at, (iter / p.check_term + 1) * p.check_term);
+        if (p.adaptive_rho && p.rho_interval) stop_at = min(stop_at, (iter / p.rho_interval + 1) * p.rho_interval);
+        __syncthreads();
+        PH(5)
+        while (iter < stop_at) {
+            ++iter;
+            // rhs = sigma x_prev - q + A' (rho z_prev - y)
+#pragma unroll
+            for (int s = 0; s < CS; ++s) {
+                const int pc = tid + s * T;
+                if (pc < npad)
+                    L.rb[pc] = cvar[s] >= 0 ? (sigma * X[pc] - L.qv[pc]) + cg[s].dot(L.Acsc, L.w) : 0.0;
+            }
+            __syncthreads();
+            PH(1)
+            bt_solve<NB, A>(p, RF, Fg, Hg, Sg, L.rb, L.xt);
+            PH(2)
+            // z~ = A x~ ; relaxed + projected z ; y ; next w.   x update; deltas for the checks.
+#pragma unroll
+            for (int s = 0; s < RS; ++s) {
+                const int i = tid + s * T;
+                if (i < m) {
+                    const double zt = rg[s].dot(L.Acsc, L.xt);
+                    const double rv = rho_of(L.ct[i], rho);
+                    const double zr = alpha * zt + (1.0 - alpha) * Z[i];
+                    const double zn = cmin(cmax(zr + (1.0 / rv) * y[s], L.lo[i]), L.up[i]);
+                    const double d = rv * (zr - zn);
+                    Z[i] = zn;
+                    dY[i] = d;
+                    y[s] += d;
+                    L.w[i] = rv * zn - y[s];
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < CS; ++s) {
+                const int pc = tid + s * T;
+                if (pc < npad) {
+                    const double xold = X[pc];
+                    const double xn = alpha * L.xt[pc] + (1.0 - alpha) * xold;
+                    X[pc] = xn;
+                    L.rb[pc] = xn - xold;
+                }
+            }
+            __syncthreads();
+            PH(3)
+        }
+#pragma unroll
+        for (int s = 0; s < RS; ++s) { const int i = tid + s * T; if (i < m) L.ys[i] = y[s]; }
+        __syncthreads();
+        // ---- out-of-line phases (only scalars live across these calls) ----
+        can_check = p.check_term && (iter % p.check_term == 0);
+        const bool do_rho = p.adaptive_rho && p.rho_interval && (iter % p.rho_interval == 0);
+        if (!can_check && !do_rho) break;  // max_iter reached
+        update_info_nl(p.self, b, cinv);
+        info_iter = iter;
+        bool stop = false;
+        if (can_check) {
+            status = check_termination_nl(p.self, b, cval, cinv, 0);
+            stop = status != MPCQP_UNSOLVED_;
+        }
+        if (!stop && do_rho) {
+            Res R;
+            R.restore(L.res);
+            const double pr = R.rpri / (cmax(R.rz, R.rax) + DIVISION_TOL);
+            const double du = R.rdua / (cmax(cmax(R.rq, R.raty), R.rpx) + DIVISION_TOL);
+            double rn = rho * sqrt(pr / (du + DIVISION_TOL));
+            rn = cmin(cmax(rn, RHO_MIN), RHO_MAX);
+            if (rn > rho * p.rho_tol || rn < rho / p.rho_tol) {
+                rho = cmin(cmax(rn, RHO_MIN), RHO_MAX);
+                rho_updates++;
+                need_factor = true;
+            }
+        }
+        __syncthreads();  // red / res reused
+        PH(4)
+        if (stop || iter >= p.max_iter) break;
+    }
+    // ys holds y here
+    if (!can_check && status == MPCQP_UNSOLVED_) {
+        update_info_nl(p.self, b, cinv);
+        info_iter = iter;
+        status = check_termination_nl(p.self, b, cval, cinv, 0);
+    }
+    const bool has_sol = !(status == MPCQP_PRIMAL_INFEASIBLE_ || status == MPCQP_PRIMAL_INFEASIBLE_INACCURATE_ ||
+                           status == MPCQP_DUAL_INFEASIBLE_ || status == MPCQP_DUAL_INFEASIBLE_INACCURATE_ ||
+                           status == MPCQP_NON_CVX_);
+    if (has_sol) objective_nl(p.self, cinv);
+    if (status == MPCQP_UNSOLVED_) {
+        status = check_termination_nl(p.self, b, cval, cinv, 1);
+        if (status == MPCQP_UNSOLVED_) status = MPCQP_MAX_ITER_REACHED_;
+    }
+    finalize_nl(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates);
+#ifdef MPCQP_PHASE_PROF
+    if (prof) {
+        __syncthreads();
+        PH(5)
+        if (tid == 0) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) p.prof[b * kProfSlots + k] = L.pacc[k];
+            p.prof[b * kProfSlots + 6] = clock64() - t0c;
+            p.prof[b * kProfSlots + 7] = wall_clock64() - t0w;
+        }
+    }
+#endif
+#undef PH
+}
+
+// ------------------------------------------------------------ launcher --
+size_t lds_solve_bytes(const KParams& p) {
+    return sizeof(double) * ((size_t)p.nnzA + 1 + p.nnzP + 3 * (size_t)p.m + 2 * (size_t)p.npad +
+                             (size_t)solve_vlen(p.m, p.npad) + 152) +
+           ((p.m + 15) & ~15) + 64;
+}
+
+template <int NB, int A, int K, int CS, int RS, int W>
+static hipError_t go(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st, size_t lds) {
+    auto k = k_solve<NB, A, K, CS, RS, W>;
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(T), lds, st, p, xo, yo, fo);
+    return hipGetLastError();
+}
+
+// Instantiations: NB = register-resident factor blocks (0: tiles read from the
+// workspace), A = coupling rows of F_k, K = gather-list length, CS / RS = columns /
+// rows per thread, W = waves per SIMD the register budget is sized for.
+int solve_variant(const KParams& p) {
+    const int cs = (p.npad + T - 1) / T, rs = (p.m + T - 1) / T;
+    if (p.nb == 4 && p.amax <= 8 && p.gk <= 6 && cs <= 1 && rs <= 1) return 0;
+    if (p.nb == 8 && p.amax <= 8 && p.gk <= 8 && cs <= 1 && rs <= 1) return 1;
+    if (p.nb == 8 && p.amax <= 16 && p.gk <= 8 && cs <= 1 && rs <= 1) return 2;
+    if (p.nb == 8 && p.amax <= 16 && p.gk <= 8 && cs <= 1 && rs <= 2) return 3;
+    if (p.gk <= 8 && cs <= 2 && rs <= 4) return 4;
+    if (p.gk <= 8 && cs <= 4 && rs <= 4) return 5;
+    if (cs <= 8 && rs <= 8) return 6;
+    return -1;
+}
+
+hipError_t launch_solve(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st) {
+    const size_t lds = lds_solve_bytes(p);
+    switch (solve_variant(p)) {
+        case 0: return go<4, 8, 6, 1, 1, 4>(p, B, xo, yo, factor_only, st, lds);
+        case 1: return go<8, 8, 8, 1, 1, 4>(p, B, xo, yo, factor_only, st, lds);
+        case 2: return go<8, 16, 8, 1, 1, 2>(p, B, xo, yo, factor_only, st, lds);
+        case 3: return go<8, 16, 8, 1, 2, 2>(p, B, xo, yo, factor_only, st, lds);
+        case 4: return go<0, 32, 8, 2, 4, 2>(p, B, xo, yo, factor_only, st, lds);
+        case 5: return go<0, 32, 8, 4, 4, 2>(p, B, xo, yo, factor_only, st, lds);
+        case 6: return go<0, 32, 16, 8, 8, 1>(p, B, xo, yo, factor_only, st, lds);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace mpcqp

@@ -25,7 +25,10 @@ import scipy.sparse as sparse
 
 __all__ = ["OSQP", "OSQPBatch", "DeviceBatch", "constant", "STATUS", "lib", "LIB_PATH"]
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmpcqp.so")
+# MPCQP_PHASE_PROF=1 selects the diagnostic build with in-kernel phase timers
+# (make -C python-mpc_amd/csrc prof -> libmpcqp_prof.so)
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                        "libmpcqp_prof.so" if os.environ.get("MPCQP_PHASE_PROF") == "1" else "libmpcqp.so")
 OSQP_INFTY = 1e30
 
 STATUS = {
@@ -117,6 +120,7 @@ def lib():
     L.mpcqp_get_plan_info.argtypes = [vp, _P(_PlanInfo)]
     L.mpcqp_timing.argtypes = [vp, C.c_int32]
     L.mpcqp_timing_read.argtypes = [vp, dp, i32p, dp, i32p]
+    L.mpcqp_debug_phase_times.argtypes = [vp, _P(C.c_int64)]
     L.mpcqp_free.argtypes = [vp]
     L.mpcqp_free.restype = None
     L.mpcqp_analyze.argtypes = [C.c_int32, C.c_int32, i32p, i32p, i32p, i32p,
@@ -433,3 +437,10 @@ class DeviceBatch:
         info = _PlanInfo()
         _check(lib().mpcqp_get_plan_info(self._h.ptr, C.byref(info)), "plan_info")
         return {f[0]: getattr(info, f[0]) for f in _PlanInfo._fields_}
+
+    def phase_times(self):
+        """Per-instance phase timers of the last solve, shape (B, 8) int64 (diagnostic;
+        needs MPCQP_PHASE_PROF=1 in the environment when the batch was created)."""
+        out = np.zeros((self.B, 8), dtype=np.int64)
+        _check(lib().mpcqp_debug_phase_times(self._h.ptr, out.ctypes.data_as(_P(C.c_int64))), "phase_times")
+        return out

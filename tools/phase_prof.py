@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""Phase breakdown of k_solve from the in-kernel timers (diagnostic, GPU only).
+
+  MPCQP_PHASE_PROF=1 python tools/phase_prof.py --config 2 [--batch B]
+
+Prints, for the slowest instance and for the mean instance, cycles per phase
+(factor, rhs, bt_solve, update, checks, tail) and cycles per ADMM iteration.
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "python-mpc_amd"))
+os.environ.setdefault("MPCQP_PHASE_PROF", "1")
+
+import numpy as np  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=None)
+    args = ap.parse_args()
+    import torch
+    from osqp_amd import DeviceBatch, mpc, _drop_common_zeros
+    spec = mpc.CONFIGS[args.config]
+    B = args.batch or spec["B"]
+    b = mpc.make_batch(args.config, B=B, seed=1000 * args.config)
+    P, Px = _drop_common_zeros(b["P"], b["Px"])
+    A, Ax = _drop_common_zeros(b["A"], b["Ax"])
+    settings = {k: v for k, v in b["settings"].items() if k != "verbose"}
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    dPx, dAx, dq, dl, du = (t(a) for a in (Px, Ax, b["q"], b["l"], b["u"]))
+    dx = torch.empty((B, b["n"]), dtype=torch.float64, device=dev)
+    dy = torch.empty((B, b["m"]), dtype=torch.float64, device=dev)
+    dst = torch.empty(B, dtype=torch.int32, device=dev)
+    dit = torch.empty(B, dtype=torch.int32, device=dev)
+    s = DeviceBatch(P, A, B, device=0, **settings)
+    for _ in range(3):
+        s.setup(dPx, dAx, dq, dl, du)
+        s.solve(dx, dy, dst, dit)
+    s.synchronize()
+    s.timing(True)
+    s.setup(dPx, dAx, dq, dl, du)
+    s.solve(dx, dy, dst, dit)
+    kt = s.timing_read()
+    pt = s.phase_times().astype(np.float64)
+    it = dit.cpu().numpy().astype(np.float64)
+    names = ["factor", "rhs", "bt_solve", "update", "checks", "tail"]
+    print(f"config {args.config} B={B} plan={s.plan_info()} kernel_ms={kt['solve_ms']:.3f}")
+    slow = int(np.argmax(pt[:, 7]))
+    for label, row, its in (("slowest", pt[slow], it[slow]), ("mean", pt.mean(0), it.mean())):
+        tot = row[6]
+        mhz = row[6] / (row[7] * 10e-3) if row[7] else 0
+        print(f"{label}: iters {its:.1f} total {tot:.0f} cyc = {row[7] * 1e-2:.1f} us  (~{mhz:.0f} MHz shader clock)"
+              f"  {tot / max(its, 1):.0f} cyc/iter")
+        for k, nm in enumerate(names):
+            print(f"   {nm:9s} {row[k]:12.0f} cyc {100 * row[k] / tot:5.1f}%  {row[k] / max(its, 1):8.0f} /iter")
+
+
+if __name__ == "__main__":
+    main()
