@@ -87,7 +87,7 @@ int upload_plan(const Plan& pl, Shard& s) {
     std::vector<const std::vector<int>*> parts = {
         &pl.pad_var, &pl.acsc_ptr, &pl.acsc_row, &pl.acsc_v, &pl.acsr_ptr, &pl.acsr_col, &pl.acsr_v,
         &pl.psym_ptr, &pl.psym_col, &pl.psym_v, &pl.p_r, &pl.p_c, &pl.a_r, &pl.a_c,
-        &pl.asm_blk_ptr, &pl.asm_tgt, &pl.asm_term_ptr, &pl.term_a, &pl.term_b, &pl.term_r, &pl.acsr_pos, &pl.gcol, &pl.grow};
+        &pl.asm_blk_ptr, &pl.asm_tgt, &pl.tterm, &pl.acsr_pos, &pl.gcol, &pl.grow};
     std::vector<size_t> offs;
     std::vector<int> flat;
     for (auto* v : parts) {
@@ -100,7 +100,7 @@ int upload_plan(const Plan& pl, Shard& s) {
     const int** dst[] = {&s.kp.pad_var, &s.kp.acsc_ptr, &s.kp.acsc_row, &s.kp.acsc_v, &s.kp.acsr_ptr,
                          &s.kp.acsr_col, &s.kp.acsr_v, &s.kp.psym_ptr, &s.kp.psym_col, &s.kp.psym_v,
                          &s.kp.p_r, &s.kp.p_c, &s.kp.a_r, &s.kp.a_c, &s.kp.asm_blk_ptr, &s.kp.asm_tgt,
-                         &s.kp.asm_term_ptr, &s.kp.term_a, &s.kp.term_b, &s.kp.term_r, &s.kp.acsr_pos,
+                         &s.kp.tterm, &s.kp.acsr_pos,
                          &s.kp.gcol, &s.kp.grow};
     for (size_t i = 0; i < parts.size(); ++i) *dst[i] = s.dplan + offs[i];
     return 0;
@@ -185,7 +185,7 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
         s.out_y = (double*)(base + carve<double>(off, B * m));
     }
     k.n = pl.n; k.m = pl.m; k.nb = pl.nb; k.npad = pl.npad; k.nnzP = pl.nnzP; k.nnzA = pl.nnzA; k.amax = pl.amax;
-    k.gk = pl.gather_k;
+    k.gk = pl.gather_k; k.ntgt = pl.ntgt; k.term_max = pl.term_max;
     const mpcqp_settings& st = h->set;
     k.sigma = st.sigma; k.alpha = st.alpha; k.eps_abs = st.eps_abs; k.eps_rel = st.eps_rel;
     k.eps_pinf = st.eps_prim_inf; k.eps_dinf = st.eps_dual_inf; k.rho0 = st.rho;

@@ -7,7 +7,8 @@
 namespace mpcqp {
 
 constexpr int kThreads = 256;
-constexpr int kProfSlots = 8;  // factor, rhs, bt_solve, update, checks, tail, total cycles, total 100 MHz ticks  // one workgroup (4 wavefronts) per QP instance
+constexpr int kProfSlots = 12;  // factor, rhs, bt_solve, update, checks, tail, total cycles, total 100 MHz ticks,
+                                // factor split: assembly, F/S products, Gauss-Jordan, block epilogue  // one workgroup (4 wavefronts) per QP instance
 
 // status values (OSQP constants.h)
 enum : int {
@@ -25,11 +26,11 @@ enum : int {
 // Everything a kernel needs: plan (shared pattern, read-only) + per-instance
 // workspace (instance-major arrays) + settings.  Passed by value.
 struct KParams {
-    int n, m, nb, npad, nnzP, nnzA, amax, gk;
+    int n, m, nb, npad, nnzP, nnzA, amax, gk, ntgt, term_max;
     // plan
     const int *pad_var, *acsc_ptr, *acsc_row, *acsc_v, *acsr_ptr, *acsr_col, *acsr_v;
     const int *psym_ptr, *psym_col, *psym_v, *p_r, *p_c, *a_r, *a_c;
-    const int *asm_blk_ptr, *asm_tgt, *asm_term_ptr, *term_a, *term_b, *term_r, *acsr_pos, *gcol, *grow;
+    const int *asm_blk_ptr, *asm_tgt, *tterm, *acsr_pos, *gcol, *grow;
     // workspace
     double *Px, *Ax, *q, *D, *l, *u, *E, *x, *z, *y, *scal, *F, *H, *Si, *dyc, *dxc;
     double *obj, *pri, *dua, *rho_est;

@@ -228,6 +228,25 @@ std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const
     for (int e = 0; e < pl.nnzA; ++e) csc_pos[pl.acsc_v[e]] = e;
     for (size_t t = 0; t < pl.term_a.size(); ++t)
         if (pl.term_r[t] >= 0) { pl.term_a[t] = csc_pos[pl.term_a[t]]; pl.term_b[t] = csc_pos[pl.term_b[t]]; }
+    // terms in ELL order: slot j of target t at (j * ntgt + t), two ints each:
+    // (a | b << 16, r) for an A pair, (a | 0, -1) for a P value, zero padding
+    // (nnzA | nnzA << 16, 0) -- Acsc[nnzA] is the kernels' zero slot
+    pl.ntgt = (int)pl.asm_tgt.size();
+    pl.term_max = 0;
+    for (int t = 0; t < pl.ntgt; ++t) pl.term_max = std::max(pl.term_max, pl.asm_term_ptr[t + 1] - pl.asm_term_ptr[t]);
+    pl.tterm.assign((size_t)2 * pl.ntgt * pl.term_max, 0);
+    for (int t = 0; t < pl.ntgt; ++t)
+        for (int j = 0; j < pl.term_max; ++j) {
+            const int u = pl.asm_term_ptr[t] + j;
+            int* w = &pl.tterm[2 * ((size_t)j * pl.ntgt + t)];
+            if (u < pl.asm_term_ptr[t + 1]) {
+                w[0] = pl.term_a[u] | (pl.term_r[u] >= 0 ? pl.term_b[u] << 16 : 0);
+                w[1] = pl.term_r[u];
+            } else {
+                w[0] = pl.nnzA | (pl.nnzA << 16);
+                w[1] = 0;
+            }
+        }
     for (size_t t = 0; t < pl.asm_tgt.size(); ++t)
         if (pl.asm_tgt[t] >= SS) pl.amax = std::max(pl.amax, (int)((pl.asm_tgt[t] - SS) / kS) + 1);
     pl.acsr_pos.resize(pl.nnzA);

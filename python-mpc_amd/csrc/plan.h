@@ -43,6 +43,9 @@ struct Plan {
     // term: r >= 0  -> rho[r] * Acsc[a] * Acsc[b] (positions in the padded-CSC order);
     //       r == -1 -> Px[a] (user order).
     std::vector<int> asm_blk_ptr, asm_tgt, asm_term_ptr, term_a, term_b, term_r;
+    // the same terms, padded to term_max per target, in ELL order (see plan.cpp)
+    int ntgt = 0, term_max = 0;
+    std::vector<int> tterm;
     std::vector<int> csc_pos;     // [nnzA] user value index -> padded-CSC position
     std::vector<int> acsr_pos;    // [nnzA] CSR entry -> padded-CSC position of its value
     int max_level = 0;            // largest BFS level (diagnostic)

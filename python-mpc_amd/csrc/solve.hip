@@ -44,91 +44,122 @@ __device__ __forceinline__ double rho_of(signed char t, double rho) {
 
 // Assemble K's tiles for the current rho and factor them (block LDL'):
 //   S_0 = D_0,  F_k = E_k S_{k-1}^{-1},  S_k = D_k - F_k E_k',  H_{k-1} = F_k'
-// F_k, H_k, S_k^{-1} go to the per-instance workspace (Fg, Hg, Sg).
-// Returns false on a non-positive pivot (OSQP: "problem non convex").
+// E_k is nonzero only in its first amax rows (block k's first BFS level), so F_k
+// has amax nonzero rows and F_k E_k' touches only the leading amax x amax corner
+// of S_k.  F_k, H_k, S_k^{-1} go to the per-instance workspace (Fg, Hg, Sg); their
+// entries outside those rows / columns are never written (zero from allocation).
+// S_k^{-1} by Gauss-Jordan (SPD: no pivoting) on register-resident tile elements.  Returns false on a non-positive pivot (OSQP:
+// "problem non convex").
 template <class KP>
 __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, double* __restrict__ Fg,
-                          double* __restrict__ Hg, double* __restrict__ Sg) {
+                                          double* __restrict__ Hg, double* __restrict__ Sg) {
     const int tid = threadIdx.x, i = tid >> 3, jg = tid & 7;
-    const int nb = p.nb;
+    const int nb = p.nb, amax = p.amax, ntgt = p.ntgt, tmax = p.term_max;
+    const int2* __restrict__ tt = (const int2*)p.tterm;
     bool ok = true;
     double* SP = L.SP;
     double* DK = L.DK;
     double* EK = L.EK;
+#ifdef MPCQP_PHASE_PROF
+    long long tf = clock64();
+#define FPH(k) if (tid == 0) { const long long t_ = clock64(); L.pacc[k] += t_ - tf; tf = t_; }
+#else
+#define FPH(k)
+#endif
 #pragma unroll 1
     for (int k = 0; k < nb; ++k) {
         for (int e = tid; e < SS; e += T) { DK[e] = 0.0; EK[e] = 0.0; }
         __syncthreads();
         if (tid < S) DK[tid * S + tid] = p.pad_var[k * S + tid] >= 0 ? p.sigma : 1.0;
         __syncthreads();
+        // every target has one owner: its terms are summed in plan order
+#pragma unroll 1
         for (int t = p.asm_blk_ptr[k] + tid; t < p.asm_blk_ptr[k + 1]; t += T) {
             double acc = 0.0;
-            for (int u = p.asm_term_ptr[t]; u < p.asm_term_ptr[t + 1]; ++u) {
-                const int r = p.term_r[u];
-                if (r < 0) acc += L.Pv[p.term_a[u]];
-                else acc += rho_of(L.ct[r], rho) * L.Acsc[p.term_a[u]] * L.Acsc[p.term_b[u]];
+#pragma unroll 4
+            for (int j = 0; j < tmax; ++j) {
+                const int2 w = tt[(long)j * ntgt + t];
+                const int a = w.x & 0xFFFF, bb = (int)((unsigned)w.x >> 16), r = w.y;
+                acc += r < 0 ? L.Pv[a] : rho_of(L.ct[r], rho) * L.Acsc[a] * L.Acsc[bb];
             }
             const int tg = p.asm_tgt[t];
             if (tg < SS) DK[tg] += acc;
             else EK[tg - SS] += acc;
         }
         __syncthreads();
+        FPH(8)
         if (k > 0) {
+            // F_k = E_k S_{k-1}^{-1} (rows < amax), then written over S_{k-1}^{-1}'s tile
             double f[4];
-#pragma unroll
-            for (int cc = 0; cc < 4; ++cc) {
-                const int j = jg + 8 * cc;
-                double s = 0.0;
-#pragma unroll 4
-                for (int l = 0; l < S; ++l) s += EK[i * S + l] * SP[l * S + j];
-                f[cc] = s;
+            int nf = 0;
+#pragma unroll 1
+            for (int o = tid; o < amax * S; o += T, ++nf) {
+                const int r = o >> 5, j = o & (S - 1);
+                double sacc = 0.0;
+#pragma unroll 8
+                for (int l = 0; l < S; ++l) sacc += EK[r * S + l] * SP[l * S + j];
+                f[nf & 3] = sacc;
+                Fg[(long)k * SS + r * S + j] = sacc;
+                Hg[(long)(k - 1) * SS + j * S + r] = sacc;
             }
-            __syncthreads();  // every read of S_{k-1}^{-1} done: its tile now holds F_k
-#pragma unroll
-            for (int cc = 0; cc < 4; ++cc) {
-                const int j = jg + 8 * cc;
-                SP[i * S + j] = f[cc];
-                Fg[(long)k * SS + i * S + j] = f[cc];
-                Hg[(long)(k - 1) * SS + j * S + i] = f[cc];
-            }
+            __syncthreads();  // every read of S_{k-1}^{-1} done
+            nf = 0;
+#pragma unroll 1
+            for (int o = tid; o < amax * S; o += T, ++nf) SP[o] = f[nf & 3];
             __syncthreads();
-#pragma unroll
-            for (int cc = 0; cc < 4; ++cc) {
-                const int j = jg + 8 * cc;
-                double s = 0.0;
-#pragma unroll 4
-                for (int l = 0; l < S; ++l) s += SP[i * S + l] * EK[j * S + l];
-                DK[i * S + j] -= s;
+            // S_k = D_k - F_k E_k' on the leading amax x amax corner
+#pragma unroll 1
+            for (int o = tid; o < amax * amax; o += T) {
+                const int r = o / amax, c = o - r * amax;
+                double sacc = 0.0;
+#pragma unroll 8
+                for (int l = 0; l < S; ++l) sacc += SP[r * S + l] * EK[c * S + l];
+                DK[r * S + c] -= sacc;
             }
             __syncthreads();
         }
-        // in-place Gauss-Jordan inverse of the SPD tile
+        FPH(9)
+        // Gauss-Jordan inverse with the tile in registers: thread (i, jg) keeps
+        // elements [i][jg + 8c]; per pivot only its row and column go through LDS
+        // (double-buffered in EK, free by now), so each pivot costs one barrier.
+        double v[4];
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) v[cc] = DK[i * S + jg + 8 * cc];
+        double* rowbuf = EK;
+        double* colbuf = EK + 2 * S;
 #pragma unroll 1
         for (int pv = 0; pv < S; ++pv) {
-            const double piv = DK[pv * S + pv];
-            const double colv = DK[i * S + pv];
-            double rowv[4];
+            const int buf = (pv & 1) * S;
+            const int cp = pv >> 3;
+            if (i == pv) {
 #pragma unroll
-            for (int cc = 0; cc < 4; ++cc) rowv[cc] = DK[pv * S + jg + 8 * cc];
+                for (int cc = 0; cc < 4; ++cc) rowbuf[buf + jg + 8 * cc] = v[cc];
+            }
+            if (jg == (pv & 7)) colbuf[buf + i] = cp == 0 ? v[0] : cp == 1 ? v[1] : cp == 2 ? v[2] : v[3];
             __syncthreads();
+            const double piv = rowbuf[buf + pv];
+            const double colv = colbuf[buf + i];
             if (!(piv > 0.0)) ok = false;
             const double d = 1.0 / piv;
 #pragma unroll
             for (int cc = 0; cc < 4; ++cc) {
                 const int j = jg + 8 * cc;
-                double v;
-                if (i == pv) v = (j == pv) ? d : rowv[cc] * d;
-                else if (j == pv) v = -colv * d;
-                else v = DK[i * S + j] - colv * (rowv[cc] * d);
-                DK[i * S + j] = v;
+                const double rowv = rowbuf[buf + j];
+                if (i == pv) v[cc] = (j == pv) ? d : rowv * d;
+                else if (j == pv) v[cc] = -colv * d;
+                else v[cc] = v[cc] - colv * (rowv * d);
             }
-            __syncthreads();
         }
 #pragma unroll
-        for (int cc = 0; cc < 4; ++cc) Sg[(long)k * SS + i * S + jg + 8 * cc] = DK[i * S + jg + 8 * cc];
-        double* t = SP; SP = DK; DK = t;  // S_k^{-1} becomes "previous"; F_k's tile is free
+        for (int cc = 0; cc < 4; ++cc) DK[i * S + jg + 8 * cc] = v[cc];
+        FPH(10)
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) Sg[(long)k * SS + i * S + jg + 8 * cc] = v[cc];
+        double* t = SP; SP = DK; DK = t;  // S_k^{-1} becomes "previous"
         __syncthreads();
+        FPH(11)
     }
+#undef FPH
     return ok;
 }
 
@@ -295,7 +326,7 @@ struct Res {  // update_info results
 // LDS carve of the solve kernel (doubles unless noted):
 //   Acsc[nnzA] Pv[nnzP] lo[m] up[m] qv[npad] X[npad] Z[m]
 //   V = max(3 S*S, w[m] rb[npad] xt[npad] ys[m] dY[m])   (factor scratch aliases the vectors)
-//   red[128] res[16] pacc[8] ct[m bytes] flag
+//   red[128] res[16] pacc[16] ct[m bytes] flag
 // rb holds delta_x and dY delta_y of the last iteration after its update phase;
 // ys holds y whenever the out-of-line phases run.
 __host__ __device__ inline long solve_vlen(int m, int npad) {
@@ -332,7 +363,7 @@ __device__ __forceinline__ SL2 carve(const KP& p) {
     c.L.red = V + solve_vlen(m, npad);
     c.L.res = c.L.red + 128;
     c.L.pacc = (long long*)(c.L.res + 16);
-    c.L.ct = (signed char*)(c.L.pacc + 8);
+    c.L.ct = (signed char*)(c.L.pacc + 16);
     c.L.flag = (int*)(c.L.ct + ((m + 15) & ~15));
     return c;
 }
@@ -672,7 +703,7 @@ __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ 
 #ifdef MPCQP_PHASE_PROF
     long long tph = 0, t0c = 0, t0w = 0;
     const bool prof = p.prof != nullptr;
-    if (prof) { t0w = wall_clock64(); t0c = tph = clock64(); if (tid < 8) L.pacc[tid] = 0; }
+    if (prof) { t0w = wall_clock64(); t0c = tph = clock64(); if (tid < 16) L.pacc[tid] = 0; }
 #define PH(k) if (prof && tid == 0) { const long long t_ = clock64(); L.pacc[k] += t_ - tph; tph = t_; }
 #else
 #define PH(k)
@@ -858,6 +889,8 @@ __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ 
         if (tid == 0) {
 #pragma unroll
             for (int k = 0; k < 6; ++k) p.prof[b * kProfSlots + k] = L.pacc[k];
+#pragma unroll
+            for (int k = 8; k < 12; ++k) p.prof[b * kProfSlots + k] = L.pacc[k];
             p.prof[b * kProfSlots + 6] = clock64() - t0c;
             p.prof[b * kProfSlots + 7] = wall_clock64() - t0w;
         }
@@ -869,7 +902,7 @@ __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ 
 // ------------------------------------------------------------ launcher --
 size_t lds_solve_bytes(const KParams& p) {
     return sizeof(double) * ((size_t)p.nnzA + 1 + p.nnzP + 3 * (size_t)p.m + 2 * (size_t)p.npad +
-                             (size_t)solve_vlen(p.m, p.npad) + 152) +
+                             (size_t)solve_vlen(p.m, p.npad) + 160) +
            ((p.m + 15) & ~15) + 64;
 }
 

@@ -58,6 +58,8 @@ def main():
               f"  {tot / max(its, 1):.0f} cyc/iter")
         for k, nm in enumerate(names):
             print(f"   {nm:9s} {row[k]:12.0f} cyc {100 * row[k] / tot:5.1f}%  {row[k] / max(its, 1):8.0f} /iter")
+        for k, nm in zip(range(8, 12), ["f.asm", "f.F/S", "f.GJ", "f.epi"]):
+            print(f"     {nm:7s} {row[k]:12.0f} cyc")
 
 
 if __name__ == "__main__":
