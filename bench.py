@@ -48,15 +48,47 @@ def parse():
     return ap.parse_args()
 
 
+def dist_env():
+    """(world, rank, local_rank) from the torch.distributed.run environment."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def instance_seed(config, rank):
+    """Each rank solves its own shard of synthetic instances (weak scaling)."""
+    return 1000 * config + rank
+
+
+def max_over_ranks(x, world):
+    """Max of a host float over all ranks (gloo; no data-path collective)."""
+    if world <= 1:
+        return float(x)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def pmc_traffic(workload, batch):
+    """HBM bytes per k_solve launch from rocprofv3 PMC passes committed under
+    profiles/ (tools/pmc_traffic.py writes profiles/traffic_<workload>_b<B>.json:
+    FETCH_SIZE and WRITE_SIZE from separate --pmc passes, FETCH_SIZE doubled per
+    the gfx950 note of MI355X_MICROARCH.md).  {} when not measured."""
+    path = os.path.join(ROOT, "profiles", f"traffic_{workload}_b{batch}.json")
+    if not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        return json.load(f)
+
+
 def main():
     args = parse()
     import torch
     import torch.distributed as dist
     from osqp_amd import DeviceBatch, mpc, _drop_common_zeros
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = dist_env()
     if world > 1:
         dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
     torch.cuda.set_device(local)
@@ -64,7 +96,7 @@ def main():
 
     spec = mpc.CONFIGS[args.config]
     B = args.batch or (spec["B"] if args.config != 4 else spec["B"] // 8)
-    b = mpc.make_batch(args.config, B=B, seed=1000 * args.config + rank)
+    b = mpc.make_batch(args.config, B=B, seed=instance_seed(args.config, rank))
     P, Px = _drop_common_zeros(b["P"], b["Px"])
     A, Ax = _drop_common_zeros(b["A"], b["Ax"])
     settings = {k: v for k, v in b["settings"].items() if k != "verbose"}
@@ -108,11 +140,7 @@ def main():
     barrier()
     kt = solver.timing_read()
     solver.timing(False)
-    dt = t1 - t0
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    dt = max_over_ranks(t1 - t0, world)
 
     value = world * B * args.steps / dt
     nnzP, nnzA = P.nnz, A.nnz
@@ -126,6 +154,8 @@ def main():
     S = info["block"]
     flop_iter = 2 * (3 * info["nb"] * S * S + 2 * nnzA) + 12 * (n + m)
     fp64_tflops = flop_iter * float(iters.astype(np.float64).sum()) / (solve_ms * 1e-3) / 1e12
+
+    traffic = pmc_traffic(spec["name"], B)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -173,7 +203,8 @@ def main():
                        "solved_frac": float(np.mean(status == 1)),
                        "plan": {"nb": info["nb"], "block": S, "lds_bytes": info["lds_bytes_solve"]}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic.get("bytes_per_launch"),
+                         "traffic_source": traffic.get("source"),
                          "kernel": "mpcqp::k_solve", "kernel_ms": solve_ms, "setup_kernel_ms": setup_ms,
                          "bytes_per_solve": bytes_per_solve, "launch_instances": B,
                          "fp64_tflops_model": fp64_tflops, "fp64_peak_tflops": FP64_PEAK_TFLOPS},

@@ -1,0 +1,115 @@
+"""Host-side checks of the C-ABI library (no GPU needed).
+
+* libmpcqp.so loads and exports every function include/mpcqp.h declares;
+* default settings are OSQP 0.6's (settings in force);
+* the symbolic plan (mpcqp_analyze) puts K = P + sigma I + A' diag(rho) A into
+  block-tridiagonal form with blocks <= the tile size, for every reference layout;
+* argument / settings / sparsity validation raise the osqp-python exception
+  types before any device is touched, and without a GPU the solver refuses to
+  run (no CPU fallback).
+"""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+import scipy.sparse as sparse
+
+import osqp_amd
+from osqp_amd import mpc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "mpcqp.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(mpcqp_\w+)\s*\(", text)))
+
+
+def test_library_exports_header_symbols():
+    names = header_functions()
+    assert len(names) >= 20
+    lib = C.CDLL(osqp_amd.LIB_PATH)
+    missing = [nm for nm in names if not hasattr(lib, nm)]
+    assert not missing, missing
+
+
+def test_default_settings_are_osqp_06():
+    s = osqp_amd._Settings()
+    osqp_amd.lib().mpcqp_default_settings(C.byref(s))
+    assert (s.rho, s.sigma, s.alpha) == (0.1, 1e-6, 1.6)
+    assert (s.eps_abs, s.eps_rel, s.eps_prim_inf, s.eps_dual_inf) == (1e-3, 1e-3, 1e-4, 1e-4)
+    assert (s.max_iter, s.scaling, s.check_termination, s.warm_start) == (4000, 10, 25, 1)
+    assert (s.adaptive_rho, s.adaptive_rho_tolerance, s.polish) == (1, 5.0, 0)
+
+
+def _kkt_pattern(P, A):
+    P = sparse.csc_matrix(P)
+    A = sparse.csc_matrix(A)
+    K = (abs(P) + abs(P).T + abs(A).T @ abs(A)).tocoo()
+    return K.row, K.col
+
+
+@pytest.mark.parametrize("cfg", [1, 2, 3, 5])
+def test_plan_is_block_tridiagonal(cfg):
+    b = mpc.make_batch(cfg, B=2, seed=3)
+    P, _ = osqp_amd._drop_common_zeros(b["P"], b["Px"])
+    A, _ = osqp_amd._drop_common_zeros(b["A"], b["Ax"])
+    nb, blk, var_pad, bsize = osqp_amd.analyze(P, A)
+    n = P.shape[0]
+    assert blk == 32 and nb >= 1
+    assert np.all(bsize >= 1) and np.all(bsize <= blk)
+    assert len(np.unique(var_pad)) == n and var_pad.min() >= 0 and var_pad.max() < nb * blk
+    block = var_pad // blk
+    assert np.all(np.bincount(block, minlength=nb) == bsize)
+    r, c = _kkt_pattern(P, A)
+    assert np.max(np.abs(block[r] - block[c])) <= 1
+
+
+@pytest.mark.parametrize("name", ["slack_n20", "vanilla_n20", "dyn_incr_n50", "kin_incr_n40"])
+def test_plan_on_reference_fixtures(golden, name):
+    g = golden(name + ".npz")
+    P, A = g["P"], g["A"]
+    nb, blk, var_pad, bsize = osqp_amd.analyze(P, A)
+    block = var_pad // blk
+    r, c = _kkt_pattern(osqp_amd.canonical_data(P, A)[0], A)
+    assert np.max(np.abs(block[r] - block[c])) <= 1
+    assert bsize.sum() == P.shape[0]
+
+
+def test_dense_row_is_unsupported():
+    n = 20
+    P = sparse.eye(n, format="csc")
+    A = sparse.csc_matrix(np.ones((1, n)))  # one row with 20 > 16 nonzeros
+    with pytest.raises(NotImplementedError):
+        osqp_amd.analyze(P, A)
+
+
+def _tiny():
+    P = sparse.diags([2.0, 1.0], format="csc")
+    A = sparse.csc_matrix(np.array([[1.0, 1.0], [1.0, 0.0], [0.0, 1.0]]))
+    return P, np.array([1.0, 1.0]), A, np.array([1.0, 0.0, 0.0]), np.array([1.0, 0.7, 0.7])
+
+
+def test_setup_validation_errors():
+    P, q, A, l, u = _tiny()
+    with pytest.raises(ValueError):
+        osqp_amd.OSQP().setup(P, q, A, l, u, alpha=2.5)
+    with pytest.raises(ValueError):
+        osqp_amd.OSQP().setup(P, q, A, l, u, max_iter=0)
+    with pytest.raises(ValueError):
+        osqp_amd.OSQP().setup(P, q[:1], A, l, u)
+    with pytest.raises(NotImplementedError):
+        osqp_amd.OSQP().setup(P, q, A, l, u, polish=True)
+
+
+def test_no_cpu_fallback_without_device():
+    torch = pytest.importorskip("torch")
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    P, q, A, l, u = _tiny()
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        osqp_amd.OSQP().setup(P, q, A, l, u, verbose=False)

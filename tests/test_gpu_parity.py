@@ -139,3 +139,40 @@ def test_dual_infeasible_status():
     g = OSQP(); g.setup(P, q, A, l, u); rg = g.solve()
     assert ro.info.status == "dual infeasible"
     assert rg.info.status == ro.info.status and rg.info.iter == ro.info.iter
+
+
+def _slack_closed_loop(osqp_mod, steps=60, N=20):
+    """BASELINE.json configs[0] plumbing: the slack script's receding-horizon loop
+    (vehicle_lateral_mpc_slack_increment.py:121-269 at N=20): setup once with
+    warm_start, then per step update(l=, u=) with the new initial state (and the
+    e_y bound regime switch of :158-172) + solve, apply du_0 = x[(N+1)*nx] to the
+    augmented lateral model."""
+    x = np.array([0.0, 0.0, 5 * mpc.DEG, 3.0, 0.0])
+    P, q, A, l, u = mpc.slack_qp(N, x)
+    prob = osqp_mod.OSQP()
+    prob.setup(P, q, A, l, u, warm_start=True, verbose=False)
+    At, Bt = mpc.augment(mpc.LATERAL_AD, mpc.LATERAL_BD)
+    nx = At.shape[0]
+    out = []
+    for i in range(steps):
+        res = prob.solve()
+        assert res.info.status == "solved"
+        du = res.x[(N + 1) * nx]
+        out.append((du, res.info.iter))
+        x = At @ x + Bt[:, 0] * du
+        _, _, _, l, u = mpc.slack_qp(N, x, regime=1 if 20 <= i < 40 else 0)
+        prob.update(l=l, u=u)
+    return np.array(out)
+
+
+def test_shim_closed_loop_matches_oracle():
+    import importlib.util
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("osqp", os.path.join(root, "python-mpc_amd", "shim", "osqp.py"))
+    shim = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(shim)
+    g = _slack_closed_loop(shim)
+    o = _slack_closed_loop(pyoracle)
+    assert np.all(g[:, 1] == o[:, 1])
+    assert np.abs(g[:, 0] - o[:, 0]).max() < U_TOL
