@@ -87,7 +87,7 @@ int upload_plan(const Plan& pl, Shard& s) {
     std::vector<const std::vector<int>*> parts = {
         &pl.pad_var, &pl.acsc_ptr, &pl.acsc_row, &pl.acsc_v, &pl.acsr_ptr, &pl.acsr_col, &pl.acsr_v,
         &pl.psym_ptr, &pl.psym_col, &pl.psym_v, &pl.p_r, &pl.p_c, &pl.a_r, &pl.a_c,
-        &pl.asm_blk_ptr, &pl.asm_tgt, &pl.tterm, &pl.acsr_pos, &pl.gcol, &pl.grow};
+        &pl.asm_blk_ptr, &pl.asm_tgt, &pl.tterm, &pl.acsr_pos, &pl.gcol, &pl.grow, &pl.gpsym};
     std::vector<size_t> offs;
     std::vector<int> flat;
     for (auto* v : parts) {
@@ -101,7 +101,7 @@ int upload_plan(const Plan& pl, Shard& s) {
                          &s.kp.acsr_col, &s.kp.acsr_v, &s.kp.psym_ptr, &s.kp.psym_col, &s.kp.psym_v,
                          &s.kp.p_r, &s.kp.p_c, &s.kp.a_r, &s.kp.a_c, &s.kp.asm_blk_ptr, &s.kp.asm_tgt,
                          &s.kp.tterm, &s.kp.acsr_pos,
-                         &s.kp.gcol, &s.kp.grow};
+                         &s.kp.gcol, &s.kp.grow, &s.kp.gpsym};
     for (size_t i = 0; i < parts.size(); ++i) *dst[i] = s.dplan + offs[i];
     return 0;
 }
@@ -185,7 +185,7 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
         s.out_y = (double*)(base + carve<double>(off, B * m));
     }
     k.n = pl.n; k.m = pl.m; k.nb = pl.nb; k.npad = pl.npad; k.nnzP = pl.nnzP; k.nnzA = pl.nnzA; k.amax = pl.amax;
-    k.gk = pl.gather_k; k.ntgt = pl.ntgt; k.term_max = pl.term_max;
+    k.gk = pl.gather_k; k.pk = pl.p_k; k.ntgt = pl.ntgt; k.term_max = pl.term_max;
     const mpcqp_settings& st = h->set;
     k.sigma = st.sigma; k.alpha = st.alpha; k.eps_abs = st.eps_abs; k.eps_rel = st.eps_rel;
     k.eps_pinf = st.eps_prim_inf; k.eps_dinf = st.eps_dual_inf; k.rho0 = st.rho;
@@ -195,10 +195,17 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
     int interval = st.adaptive_rho_interval;
     if (st.adaptive_rho && interval == 0) interval = st.check_termination ? 4 * st.check_termination : 100;
     k.rho_interval = interval;
-    k.self = (const KParams*)(base + carve<KParams>(off, 1));
-    HIPCHK(hipMemcpy((void*)k.self, &k, sizeof(KParams), hipMemcpyHostToDevice));
     if (solve_variant(k) < 0)
         return fail(MPCQP_EUNSUPPORTED, "problem shape outside the solve kernel's instantiations (n=%d m=%d)", pl.n, pl.m);
+    k.variant = solve_variant(k);
+    if (const char* ev = getenv("MPCQP_VARIANT"); ev && *ev) {  // diagnostic override (A/B timing)
+        const int v = atoi(ev);
+        if (!variant_fits(k, v)) return fail(MPCQP_EUNSUPPORTED, "MPCQP_VARIANT=%d does not fit this plan", v);
+        k.variant = v;
+    }
+    k.mode = solve_mode(k.variant);
+    k.self = (const KParams*)(base + carve<KParams>(off, 1));
+    HIPCHK(hipMemcpy((void*)k.self, &k, sizeof(KParams), hipMemcpyHostToDevice));
     if (size_t lds = lds_solve_bytes(k); lds > 160 * 1024)
         return fail(MPCQP_EUNSUPPORTED, "problem needs %zu bytes of LDS per instance (> 160 KiB)", lds);
     return 0;

@@ -39,14 +39,14 @@ __device__ __forceinline__ double limit_scaling(double d) {
     return d > MAX_SCALING ? MAX_SCALING : d;
 }
 
-// DPP lane permutation of a double (two 32-bit moves; all lanes valid for the
-// controls used here).  CTRL: 0xB1 quad_perm[1,0,3,2], 0x4E quad_perm[2,3,0,1],
-// 0x141 row_half_mirror, 0x140 row_mirror.
+// DPP lane permutation of a double: two v_mov_b32_dpp, bound_ctrl set so no copy
+// of the old value is needed.  CTRL: 0xB1 quad_perm[1,0,3,2], 0x4E quad_perm[2,3,0,1],
+// 0x141 row_half_mirror, 0x140 row_mirror (every lane has a valid source).
 template <int CTRL>
 __device__ __forceinline__ double dpp(double v) {
     int lo = __double2loint(v), hi = __double2hiint(v);
-    lo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, 0xF, 0xF, false);
-    hi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, 0xF, 0xF, false);
+    lo = __builtin_amdgcn_mov_dpp(lo, CTRL, 0xF, 0xF, true);
+    hi = __builtin_amdgcn_mov_dpp(hi, CTRL, 0xF, 0xF, true);
     return __hiloint2double(hi, lo);
 }
 
@@ -67,12 +67,13 @@ __device__ __forceinline__ double reduce16(double v) {
     return v;
 }
 
-// DPP with a row mask: rows outside `RM` receive 0
+// DPP with a row mask: rows outside `RM` get an unspecified value (callers only
+// read lanes of the written rows)
 template <int CTRL, int RM>
 __device__ __forceinline__ double dpp_rows(double v) {
     int lo = __double2loint(v), hi = __double2hiint(v);
-    lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, RM, 0xF, false);
-    hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, RM, 0xF, false);
+    lo = __builtin_amdgcn_mov_dpp(lo, CTRL, RM, 0xF, true);
+    hi = __builtin_amdgcn_mov_dpp(hi, CTRL, RM, 0xF, true);
     return __hiloint2double(hi, lo);
 }
 
@@ -85,14 +86,8 @@ __device__ __forceinline__ double reduce32_hi(double v) {
 }
 
 // Wave-wide reductions by DPP (rows of 16, then row_bcast:15 / row_bcast:31);
-// the result is read from lane 63 into a scalar register.
-template <int CTRL, int RM>
-__device__ __forceinline__ double dpp_keep(double v) {  // rows outside RM keep v
-    int lo = __double2loint(v), hi = __double2hiint(v);
-    lo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, RM, 0xF, false);
-    hi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, RM, 0xF, false);
-    return __hiloint2double(hi, lo);
-}
+// the result is read from lane 63 (only lanes of the written rows are valid after
+// the broadcasts) into a scalar register.
 __device__ __forceinline__ double lane63(double v) {
     return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 63),
                             __builtin_amdgcn_readlane(__double2loint(v), 63));
@@ -102,8 +97,8 @@ __device__ __forceinline__ double wave_max(double v) {
     v = cmax(v, dpp<0x4E>(v));
     v = cmax(v, dpp<0x141>(v));
     v = cmax(v, dpp<0x140>(v));
-    v = cmax(v, dpp_keep<0x142, 0xA>(v));
-    v = cmax(v, dpp_keep<0x143, 0xC>(v));
+    v = cmax(v, dpp_rows<0x142, 0xA>(v));
+    v = cmax(v, dpp_rows<0x143, 0xC>(v));
     return lane63(v);
 }
 __device__ __forceinline__ double wave_sum(double v) {

@@ -26,11 +26,13 @@ enum : int {
 // Everything a kernel needs: plan (shared pattern, read-only) + per-instance
 // workspace (instance-major arrays) + settings.  Passed by value.
 struct KParams {
-    int n, m, nb, npad, nnzP, nnzA, amax, gk, ntgt, term_max;
+    int n, m, nb, npad, nnzP, nnzA, amax, gk, pk, ntgt, term_max;
+    int variant;  // solve-kernel instantiation (solve.hip: launch_solve)
+    int mode;     // factor storage of that variant (solve.hip: factorize)
     // plan
     const int *pad_var, *acsc_ptr, *acsc_row, *acsc_v, *acsr_ptr, *acsr_col, *acsr_v;
     const int *psym_ptr, *psym_col, *psym_v, *p_r, *p_c, *a_r, *a_c;
-    const int *asm_blk_ptr, *asm_tgt, *tterm, *acsr_pos, *gcol, *grow;
+    const int *asm_blk_ptr, *asm_tgt, *tterm, *acsr_pos, *gcol, *grow, *gpsym;
     // workspace
     double *Px, *Ax, *q, *D, *l, *u, *E, *x, *z, *y, *scal, *F, *H, *Si, *dyc, *dxc;
     double *obj, *pri, *dua, *rho_est;
@@ -51,6 +53,8 @@ hipError_t launch_update(const KParams& p, long B, const double* q, const double
                          hipStream_t st);
 hipError_t launch_warm(const KParams& p, long B, const double* x, const double* y, hipStream_t st);
 int solve_variant(const KParams& p);  // -1: no instantiation fits the plan
+int solve_mode(int variant);
+bool variant_fits(const KParams& p, int variant);
 hipError_t launch_solve(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st);
 
 }  // namespace mpcqp

@@ -262,6 +262,15 @@ std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const
     for (int pc = 0; pc < pl.npad; ++pc)
         for (int e = pl.acsc_ptr[pc], k = 0; e < pl.acsc_ptr[pc + 1]; ++e, ++k)
             pl.gcol[(size_t)pc * kGS + k] = e | (pl.acsc_row[e] << 16);
+    // P by padded column (full symmetric), padded with (nnzP | 0): Pv[nnzP] is a zero slot
+    pl.p_k = 0;
+    for (int r = 0; r < pl.npad; ++r) pl.p_k = std::max(pl.p_k, pl.psym_ptr[r + 1] - pl.psym_ptr[r]);
+    if (pl.p_k > kGS) return "unsupported sparsity: a column of P has more than 16 nonzeros";
+    if (pl.nnzP >= 65535) return "unsupported size: nnz(P) must be < 65535";
+    pl.gpsym.assign((size_t)pl.npad * kGS, pl.nnzP);
+    for (int r = 0; r < pl.npad; ++r)
+        for (int e = pl.psym_ptr[r], k = 0; e < pl.psym_ptr[r + 1]; ++e, ++k)
+            pl.gpsym[(size_t)r * kGS + k] = pl.psym_v[e] | (pl.psym_col[e] << 16);
     pl.grow.assign((size_t)m * kGS, pad);
     for (int r = 0; r < m; ++r)
         for (int e = pl.acsr_ptr[r], k = 0; e < pl.acsr_ptr[r + 1]; ++e, ++k)

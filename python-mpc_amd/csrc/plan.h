@@ -54,6 +54,8 @@ struct Plan {
     // packed gather lists: [npad*kGS] by padded column (A' w), [m*kGS] by row (A x):
     // (position of the value in the padded-CSC order) | (vector index << 16), padding (nnzA | 0)
     std::vector<int> gcol, grow;
+    int p_k = 0;                  // max nonzeros per column of the symmetric P
+    std::vector<int> gpsym;       // [npad*kGS] P by padded column: (Pv index) | (padded column << 16)
     int amax = 0;                 // max over k of (last nonzero local row of E_k) + 1: F_k rows / H_{k-1} cols
 };
 

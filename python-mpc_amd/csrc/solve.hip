@@ -22,6 +22,8 @@
 // algorithm on the CPU and tests/test_gpu_parity.py compares the two.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "device_common.h"
 
 namespace mpcqp {
@@ -30,6 +32,8 @@ namespace mpcqp {
 struct SLds {
     double *Acsc, *Pv, *lo, *up, *qv;
     double *w, *rb, *xt, *ys;        // per-iteration vectors (aliased by the factor scratch)
+    double* dx;                      // delta x of the last iteration (rb, or xt in mode 2)
+    double* cor;                     // three-phase solve corrections (nb * S, rows < A used)
     double *SP, *EK, *DK;            // factorisation scratch (3 tiles)
     double* red;
     double* res;                     // last update_info results (14 doubles)
@@ -48,13 +52,19 @@ __device__ __forceinline__ double rho_of(signed char t, double rho) {
 // has amax nonzero rows and F_k E_k' touches only the leading amax x amax corner
 // of S_k.  F_k, H_k, S_k^{-1} go to the per-instance workspace (Fg, Hg, Sg); their
 // entries outside those rows / columns are never written (zero from allocation).
-// S_k^{-1} by Gauss-Jordan (SPD: no pivoting) on register-resident tile elements.  Returns false on a non-positive pivot (OSQP:
-// "problem non convex").
+// S_k^{-1} by Gauss-Jordan (SPD: no pivoting) on register-resident tile elements.
+// What else is stored depends on the solve variant (KParams::mode):
+//   0: F_k and H_k = F_k' as full tiles (solves reading the tiles from the workspace)
+//   1: F_k only (register sweep; H is loaded as F transposed)
+//   2: the blocks of L^{-1}:  G_kj = (-1)^{k-j} F_k F_{k-1} .. F_{j+1}  (j < k), amax x 32
+//      each, in Hg at pair (k, j) -> k(k-1)/2 + j, row stride 32 (three-phase solve).
+// Returns false on a non-positive pivot (OSQP: "problem non convex").
 template <class KP>
 __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, double* __restrict__ Fg,
                                           double* __restrict__ Hg, double* __restrict__ Sg) {
     const int tid = threadIdx.x, i = tid >> 3, jg = tid & 7;
-    const int nb = p.nb, amax = p.amax, ntgt = p.ntgt, tmax = p.term_max;
+    const int nb = p.nb, amax = p.amax, ntgt = p.ntgt, tmax = p.term_max, mode = p.mode;
+    const long gstride = (long)amax * S;
     const int2* __restrict__ tt = (const int2*)p.tterm;
     bool ok = true;
     double* SP = L.SP;
@@ -99,14 +109,30 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
 #pragma unroll 8
                 for (int l = 0; l < S; ++l) sacc += EK[r * S + l] * SP[l * S + j];
                 f[nf & 3] = sacc;
-                Fg[(long)k * SS + r * S + j] = sacc;
-                Hg[(long)(k - 1) * SS + j * S + r] = sacc;
+                if (mode < 2) Fg[(long)k * SS + r * S + j] = sacc;
+                if (mode == 0) Hg[(long)(k - 1) * SS + j * S + r] = sacc;
+                if (mode == 2) Hg[(long)(k * (k - 1) / 2 + k - 1) * gstride + o] = -sacc;
             }
             __syncthreads();  // every read of S_{k-1}^{-1} done
             nf = 0;
 #pragma unroll 1
             for (int o = tid; o < amax * S; o += T, ++nf) SP[o] = f[nf & 3];
             __syncthreads();
+            if (mode == 2) {  // G_kj = -F_k G_{k-1,j} (G_{k-1,j} has amax nonzero rows)
+#pragma unroll 1
+                for (int j = 0; j < k - 1; ++j) {
+                    const double* Gp = Hg + (long)((k - 1) * (k - 2) / 2 + j) * gstride;
+                    double* Gk = Hg + (long)(k * (k - 1) / 2 + j) * gstride;
+#pragma unroll 1
+                    for (int o = tid; o < amax * S; o += T) {
+                        const int r = o >> 5, c = o & (S - 1);
+                        double sacc = 0.0;
+#pragma unroll 1
+                        for (int l = 0; l < amax; ++l) sacc += SP[r * S + l] * Gp[l * S + c];
+                        Gk[o] = -sacc;
+                    }
+                }
+            }
             // S_k = D_k - F_k E_k' on the leading amax x amax corner
 #pragma unroll 1
             for (int o = tid; o < amax * amax; o += T) {
@@ -184,13 +210,12 @@ struct RegFactor {
             }
             if (k + 1 < nb && k < NB - 1) {
                 const double* Fk = Fg + (long)(k + 1) * SS;
-                const double* Hk = Hg + (long)k * SS;
 #pragma unroll
                 for (int c = 0; c < NF; ++c) {
                     if constexpr (A == 8) F[k][c] = Fk[(tid >> 5) * S + (tid & 31)];
                     else if constexpr (A == 16) F[k][c] = Fk[(tid >> 4) * S + (tid & 15) + 16 * c];
                     else F[k][c] = Fk[i * S + jg + 8 * c];
-                    H[k][c] = Hk[i * S + jg + 8 * c];
+                    H[k][c] = Fk[(jg + 8 * c) * S + i];  // H_k = F_{k+1}'
                 }
             }
         }
@@ -280,6 +305,112 @@ __device__ __forceinline__ void bt_solve(const KParams& p, const RegFactor<NB, A
     }
 }
 
+// Three-phase solve (mode 2, NB <= 4):  K^{-1} = L^{-T} D^{-1} L^{-1}  with the
+// blocks of L^{-1} precomputed (G_kj, factorize), so that x~ = K^{-1} b takes three
+// parallel phases instead of a 2*nb-1 step sweep:
+//   A: c_k = sum_{j<k} G_kj b_j          (rows < amax of block k)
+//   B: t_k = S_k^{-1} (b_k + c_k)
+//   C: x_k = t_k + sum_{j>k} G_jk' t_j
+// Thread layouts:  Si as RegFactor;  GL[pair][e] = G_kj[r][c] with r = t / LPR,
+// c = t % LPR + LPR e (LPR = 256 / A lanes per row);  GU[pair][e] = G_jk[r][i] with
+// i = t / 8, r = t % 8 + 8 e.
+template <int NB, int A>
+struct RegFactor3 {
+    static_assert(NB * 64 <= T, "one wave per diagonal block");
+    static constexpr int NP = NB * (NB - 1) / 2 > 0 ? NB * (NB - 1) / 2 : 1;
+    static constexpr int LPR = T / A;
+    static constexpr int EL = A / 8;
+    // Sw: wave w owns block w: thread t keeps S_w^{-1}[i][16 h + c], i = (t/2) % 32, h = t % 2
+    double Sw[16], GL[NP][EL], GU[NP][EL];
+    __device__ __forceinline__ void load(int amax, const double* Gg, const double* Sg) {
+        const int tid = threadIdx.x, i = tid >> 3, jg = tid & 7;
+        const long gs = (long)amax * S;
+        {
+            const int kb = tid >> 6, ib = (tid >> 1) & (S - 1), hb = tid & 1;
+#pragma unroll
+            for (int c = 0; c < 16; ++c) Sw[c] = kb < NB ? Sg[(long)kb * SS + ib * S + 16 * hb + c] : 0.0;
+        }
+        const int r = tid / LPR;
+#pragma unroll
+        for (int q = 0; q < NB * (NB - 1) / 2; ++q)
+#pragma unroll
+            for (int e = 0; e < EL; ++e) {
+                const int c = tid % LPR + LPR * e, ru = jg + 8 * e;
+                GL[q][e] = r < amax ? Gg[q * gs + r * S + c] : 0.0;
+                GU[q][e] = ru < amax ? Gg[q * gs + ru * S + i] : 0.0;
+            }
+    }
+};
+
+// reduction over the LPR lanes of one G row (A = 8: 32 lanes, result in the upper 16)
+template <int A>
+__device__ __forceinline__ double reduce_lpr(double v) {
+    if constexpr (A == 8) return reduce32_hi(v);
+    else if constexpr (A == 16) return reduce16(v);
+    else return reduce8(v);
+}
+template <int A>
+__device__ __forceinline__ bool lpr_writer(int tid) {
+    if constexpr (A == 8) return (tid & 31) == 31;
+    else if constexpr (A == 16) return (tid & 15) == 0;
+    else return (tid & 7) == 0;
+}
+
+// b in rb on entry; x~ in rb on exit (t in xt, corrections in cor).  3 barriers.
+template <int NB, int A>
+__device__ __forceinline__ void tri_solve(const RegFactor3<NB, A>& R, double* rb, double* xt, double* cor) {
+    int opq = 0;
+    asm volatile("" : "+s"(opq));
+    const int tid = threadIdx.x, i = tid >> 3, jg = (tid & 7) + opq;
+    constexpr int LPR = RegFactor3<NB, A>::LPR, EL = RegFactor3<NB, A>::EL;
+    // A
+    {
+        const int r = tid / LPR, c0 = tid % LPR + opq;
+#pragma unroll
+        for (int k = 1; k < NB; ++k) {
+            double acc = 0.0;
+#pragma unroll
+            for (int j = 0; j < k; ++j)
+#pragma unroll
+                for (int e = 0; e < EL; ++e) acc += R.GL[k * (k - 1) / 2 + j][e] * rb[j * S + c0 + LPR * e];
+            const double sacc = reduce_lpr<A>(acc);
+            if (lpr_writer<A>(tid)) cor[k * S + r] = sacc;
+        }
+    }
+    __syncthreads();
+    // B: wave k computes t_k; lanes (2i, 2i+1) split row i in halves (one DPP step)
+    {
+        const int kb = tid >> 6, ib = (tid >> 1) & (S - 1), hb = tid & 1;
+        const double* wk = rb + kb * S + 16 * hb + opq;
+        const double* ck = cor + kb * S + 16 * hb + opq;
+        double a[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            double v0 = wk[4 * q], v1 = wk[4 * q + 1], v2 = wk[4 * q + 2], v3 = wk[4 * q + 3];
+            if (4 * q < A && kb > 0 && hb == 0) {
+                v0 += ck[4 * q]; v1 += ck[4 * q + 1]; v2 += ck[4 * q + 2]; v3 += ck[4 * q + 3];
+            }
+            a[q] = (R.Sw[4 * q] * v0 + R.Sw[4 * q + 1] * v1) + (R.Sw[4 * q + 2] * v2 + R.Sw[4 * q + 3] * v3);
+        }
+        double sacc = (a[0] + a[1]) + (a[2] + a[3]);
+        sacc += dpp<0xB1>(sacc);
+        if (kb < NB && hb == 0) xt[kb * S + ib] = sacc;
+    }
+    __syncthreads();
+    // C
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+        double acc = 0.0;
+#pragma unroll
+        for (int j = k + 1; j < NB; ++j)
+#pragma unroll
+            for (int e = 0; e < EL; ++e) acc += R.GU[j * (j - 1) / 2 + k][e] * xt[j * S + jg + 8 * e];
+        const double sacc = k + 1 < NB ? reduce8(acc) : 0.0;
+        if ((tid & 7) == 0) rb[k * S + i] = xt[k * S + i] + sacc;
+    }
+    __syncthreads();
+}
+
 // Gather list of one column (A' w) or row (A x) of A: K packed entries
 // (value position in the padded-CSC copy of A in LDS | vector index << 16), padded
 // with the zero slot Acsc[nnzA] -- no per-entry branches, all 2K LDS reads in flight.
@@ -301,7 +432,10 @@ struct Gather {
         asm volatile("" : "+s"(opq));
         double t[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) t[k] = A[(e[k] & 0xFFFFu) + opq] * vec[(e[k] >> 16) + opq];
+        for (int k = 0; k < K; ++k) {
+            const unsigned ek = e[k] + (unsigned)opq;  // unpacked inside the loop: the packed
+            t[k] = A[ek & 0xFFFFu] * vec[ek >> 16];    // word is the only register it costs
+        }
 #pragma unroll
         for (int w = 1; w < K; w *= 2)
 #pragma unroll
@@ -324,9 +458,9 @@ struct Res {  // update_info results
 };
 
 // LDS carve of the solve kernel (doubles unless noted):
-//   Acsc[nnzA] Pv[nnzP] lo[m] up[m] qv[npad] X[npad] Z[m]
+//   Acsc[nnzA+1] Pv[nnzP+1] lo[m] up[m] qv[npad] X[npad] Z[m]
 //   V = max(3 S*S, w[m] rb[npad] xt[npad] ys[m] dY[m])   (factor scratch aliases the vectors)
-//   red[128] res[16] pacc[16] ct[m bytes] flag
+//   red[128] res[16] pacc[16] cor[nb*S] ct[m bytes] flag
 // rb holds delta_x and dY delta_y of the last iteration after its update phase;
 // ys holds y whenever the out-of-line phases run.
 __host__ __device__ inline long solve_vlen(int m, int npad) {
@@ -346,7 +480,7 @@ __device__ __forceinline__ SL2 carve(const KP& p) {
     const int m = p.m, npad = p.npad;
     c.L.Acsc = sm;
     c.L.Pv = c.L.Acsc + p.nnzA + 1;  // Acsc[nnzA] = 0: gather padding
-    c.L.lo = c.L.Pv + p.nnzP;
+    c.L.lo = c.L.Pv + p.nnzP + 1;  // Pv[nnzP] = 0: P-list padding
     c.L.up = c.L.lo + m;
     c.L.qv = c.L.up + m;
     c.X = c.L.qv + npad;
@@ -363,7 +497,9 @@ __device__ __forceinline__ SL2 carve(const KP& p) {
     c.L.red = V + solve_vlen(m, npad);
     c.L.res = c.L.red + 128;
     c.L.pacc = (long long*)(c.L.res + 16);
-    c.L.ct = (signed char*)(c.L.pacc + 16);
+    c.L.cor = (double*)(c.L.pacc + 16);
+    c.L.dx = p.mode == 2 ? c.L.xt : c.L.rb;
+    c.L.ct = (signed char*)(c.L.cor + p.nb * S);
     c.L.flag = (int*)(c.L.ct + ((m + 15) & ~15));
     return c;
 }
@@ -375,23 +511,27 @@ struct Shared {
 };
 
 // ---- out-of-line phases: everything they need is in LDS or in the plan ----
+// dot of a packed gather list (value index | vector index << 16) with cnt entries
+__device__ __forceinline__ double list_dot(const int* __restrict__ list, int cnt, const double* V, const double* v) {
+    double acc = 0.0;
+#pragma unroll 4
+    for (int k = 0; k < cnt; ++k) {
+        const unsigned e = (unsigned)list[k];
+        acc += V[e & 0xFFFFu] * v[e >> 16];
+    }
+    return acc;
+}
 template <class KP>
 __device__ __forceinline__ double row_dot(const KP& p, const double* A, const double* v, int i) {
-    double acc = 0.0;
-    for (int e = p.acsr_ptr[i]; e < p.acsr_ptr[i + 1]; ++e) acc += A[p.acsr_pos[e]] * v[p.acsr_col[e]];
-    return acc;
+    return list_dot(p.grow + (long)i * kGS, p.gk, A, v);
 }
 template <class KP>
 __device__ __forceinline__ double col_dot(const KP& p, const double* A, const double* v, int pc) {
-    double acc = 0.0;
-    for (int e = p.acsc_ptr[pc]; e < p.acsc_ptr[pc + 1]; ++e) acc += A[e] * v[p.acsc_row[e]];
-    return acc;
+    return list_dot(p.gcol + (long)pc * kGS, p.gk, A, v);
 }
 template <class KP>
 __device__ __forceinline__ double psym_dot(const KP& p, const double* Pv, const double* v, int pc) {
-    double acc = 0.0;
-    for (int e = p.psym_ptr[pc]; e < p.psym_ptr[pc + 1]; ++e) acc += Pv[p.psym_v[e]] * v[p.psym_col[e]];
-    return acc;
+    return list_dot(p.gpsym + (long)pc * kGS, p.pk, Pv, v);
 }
 
 // update_info: residuals and the norms of their tolerances (OSQP compute_pri_res /
@@ -489,7 +629,7 @@ __device__ bool primal_infeasible(const KP& p, SL2& c, long b, double eps) {
     return na[0] < eps * norm_dy;
 }
 
-// is_dual_infeasible (delta_x in rb)
+// is_dual_infeasible (delta_x in dx)
 template <class KP>
 __device__ bool dual_infeasible(const KP& p, SL2& c, long b, double cs_, double eps) {
     const int tid = threadIdx.x, m = p.m, npad = p.npad;
@@ -501,7 +641,7 @@ __device__ bool dual_infeasible(const KP& p, SL2& c, long b, double cs_, double 
     #pragma unroll 1
     for (int pc = tid; pc < npad; pc += T) {
         if (p.pad_var[pc] < 0) continue;
-        const double dx = c.L.rb[pc];
+        const double dx = c.L.dx[pc];
         v[0] = cmax(v[0], fabs(unscale ? Dg[pc] * dx : dx));
         sum[0] += c.L.qv[pc] * dx;
     }
@@ -514,7 +654,7 @@ __device__ bool dual_infeasible(const KP& p, SL2& c, long b, double cs_, double 
     #pragma unroll 1
     for (int pc = tid; pc < npad; pc += T) {
         if (p.pad_var[pc] < 0) continue;
-        double a = psym_dot(p, c.L.Pv, c.L.rb, pc);
+        double a = psym_dot(p, c.L.Pv, c.L.dx, pc);
         if (unscale) a *= 1.0 / Dg[pc];
         np[0] = cmax(np[0], fabs(a));
     }
@@ -523,7 +663,7 @@ __device__ bool dual_infeasible(const KP& p, SL2& c, long b, double cs_, double 
     bool viol = false;
     #pragma unroll 1
     for (int i = tid; i < m; i += T) {
-        double a = row_dot(p, c.L.Acsc, c.L.rb, i);
+        double a = row_dot(p, c.L.Acsc, c.L.dx, i);
         if (unscale) a *= 1.0 / Eg[i];
         if ((c.L.up[i] < OSQP_INFTY * MIN_SCALING && a > eps * norm_dx) ||
             (c.L.lo[i] > -OSQP_INFTY * MIN_SCALING && a < -eps * norm_dx))
@@ -627,9 +767,9 @@ __device__ __noinline__ void finalize_nl(const KParams* gp, long b, double* __re
     double nrm[2] = {0.0, 0.0};
     #pragma unroll 1
     for (int pc = tid; pc < npad; pc += T) {
-        double dx = c.L.rb[pc];
+        double dx = c.L.dx[pc];
         if (dx_scaled) dx *= Dg[pc];
-        c.L.rb[pc] = dx;
+        c.L.dx[pc] = dx;
         nrm[1] = cmax(nrm[1], fabs(dx));
     }
     #pragma unroll 1
@@ -646,7 +786,7 @@ __device__ __noinline__ void finalize_nl(const KParams* gp, long b, double* __re
         const double xv = c.X[pc];
         if (j >= 0) {
             if (xo) xo[b * n + j] = has_sol ? (p.scaling ? Dg[pc] * xv : xv) : __builtin_nan("");
-            p.dxc[b * n + j] = dinf ? c.L.rb[pc] * (1.0 / nrm[1]) : c.L.rb[pc];
+            p.dxc[b * n + j] = dinf ? c.L.dx[pc] * (1.0 / nrm[1]) : c.L.dx[pc];
         }
         p.x[b * npad + pc] = has_sol ? xv : 0.0;
     }
@@ -677,7 +817,7 @@ __device__ __noinline__ bool factorize_nl(const KParams* gp, long b, double rho)
                      p.Si + b * (long)p.nb * SS);
 }
 
-template <int NB, int A, int K, int CS, int RS, int W>
+template <int NB, int A, int K, int CS, int RS, int W, bool TRI>
 __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ xo, double* __restrict__ yo,
                                                 int factor_only) {
     const int tid = threadIdx.x;
@@ -691,6 +831,10 @@ __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ 
     const double* Fg = p.F + b * (long)p.nb * SS;
     const double* Hg = p.H + b * (long)p.nb * SS;
     const double* Sg = p.Si + b * (long)p.nb * SS;
+    // TRI: three-phase solve (x~ lands in rb, delta x goes to xt); else the sweep (x~ in xt, delta x in rb)
+    static_assert(!TRI || (NB > 0 && NB <= 4), "three-phase solve needs a register factor of <= 4 blocks");
+    double* const XT = TRI ? L.rb : L.xt;
+    double* const DX = TRI ? L.xt : L.rb;
 
     if (p.err[b]) {  // invalid data (flagged by setup/update): NaN outputs
         for (int j = tid; j < n; j += T) if (xo) xo[b * n + j] = __builtin_nan("");
@@ -716,6 +860,7 @@ __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ 
     for (int e = tid; e < nnzA; e += T) L.Acsc[e] = p.Ax[b * nnzA + p.acsc_v[e]];
     if (tid == 0) L.Acsc[nnzA] = 0.0;  // the gather lists' padding slot
     for (int v = tid; v < nnzP; v += T) L.Pv[v] = p.Px[b * nnzP + v];
+    if (tid == 0) L.Pv[nnzP] = 0.0;
     for (int i = tid; i < m; i += T) {
         L.lo[i] = p.l[b * m + i];
         L.up[i] = p.u[b * m + i];
@@ -766,8 +911,9 @@ __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ 
             PH(0)
         }
         // ---- run state ----
-        RegFactor<NB, A> RF;
-        if constexpr (NB > 0) RF.load(NB, Fg, Hg, Sg);
+        std::conditional_t<TRI, RegFactor3<NB, A>, RegFactor<NB, A>> RF;
+        if constexpr (TRI) RF.load(p.amax, Hg, Sg);
+        else if constexpr (NB > 0) RF.load(NB, Fg, Hg, Sg);
         int cvar[CS];
         Gather<K> cg[CS];
 #pragma unroll
@@ -794,28 +940,38 @@ __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ 
         if (p.adaptive_rho && p.rho_interval) stop_at = min(stop_at, (iter / p.rho_interval + 1) * p.rho_interval);
         __syncthreads();
         PH(5)
+        // rho_vec / rho_inv_vec of the three row classes (OSQP keeps 1/rho_i precomputed)
+        const double r_hi = RHO_EQ_OVER_RHO_INEQ * rho;
+        const double ri_lo = 1.0 / RHO_MIN, ri_mid = 1.0 / rho, ri_hi = 1.0 / r_hi;
         while (iter < stop_at) {
             ++iter;
+            // an opaque zero keeps per-thread LDS addresses out of the register budget
+            int opq = 0;
+            asm volatile("" : "+s"(opq));
+            const int tido = tid + opq;
             // rhs = sigma x_prev - q + A' (rho z_prev - y)
 #pragma unroll
             for (int s = 0; s < CS; ++s) {
-                const int pc = tid + s * T;
+                const int pc = tido + s * T;
                 if (pc < npad)
                     L.rb[pc] = cvar[s] >= 0 ? (sigma * X[pc] - L.qv[pc]) + cg[s].dot(L.Acsc, L.w) : 0.0;
             }
             __syncthreads();
             PH(1)
-            bt_solve<NB, A>(p, RF, Fg, Hg, Sg, L.rb, L.xt);
+            if constexpr (TRI) tri_solve<NB, A>(RF, L.rb, L.xt, L.cor);
+            else bt_solve<NB, A>(p, RF, Fg, Hg, Sg, L.rb, L.xt);
             PH(2)
             // z~ = A x~ ; relaxed + projected z ; y ; next w.   x update; deltas for the checks.
 #pragma unroll
             for (int s = 0; s < RS; ++s) {
-                const int i = tid + s * T;
+                const int i = tido + s * T;
                 if (i < m) {
-                    const double zt = rg[s].dot(L.Acsc, L.xt);
-                    const double rv = rho_of(L.ct[i], rho);
+                    const double zt = rg[s].dot(L.Acsc, XT);
+                    const signed char cl = L.ct[i];
+                    const double rv = cl < 0 ? RHO_MIN : (cl > 0 ? r_hi : rho);
+                    const double rvi = cl < 0 ? ri_lo : (cl > 0 ? ri_hi : ri_mid);
                     const double zr = alpha * zt + (1.0 - alpha) * Z[i];
-                    const double zn = cmin(cmax(zr + (1.0 / rv) * y[s], L.lo[i]), L.up[i]);
+                    const double zn = cmin(cmax(zr + rvi * y[s], L.lo[i]), L.up[i]);
                     const double d = rv * (zr - zn);
                     Z[i] = zn;
                     dY[i] = d;
@@ -825,12 +981,12 @@ __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ 
             }
 #pragma unroll
             for (int s = 0; s < CS; ++s) {
-                const int pc = tid + s * T;
+                const int pc = tido + s * T;
                 if (pc < npad) {
                     const double xold = X[pc];
-                    const double xn = alpha * L.xt[pc] + (1.0 - alpha) * xold;
+                    const double xn = alpha * XT[pc] + (1.0 - alpha) * xold;
                     X[pc] = xn;
-                    L.rb[pc] = xn - xold;
+                    DX[pc] = xn - xold;
                 }
             }
             __syncthreads();
@@ -901,14 +1057,14 @@ __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ 
 
 // ------------------------------------------------------------ launcher --
 size_t lds_solve_bytes(const KParams& p) {
-    return sizeof(double) * ((size_t)p.nnzA + 1 + p.nnzP + 3 * (size_t)p.m + 2 * (size_t)p.npad +
-                             (size_t)solve_vlen(p.m, p.npad) + 160) +
+    return sizeof(double) * ((size_t)p.nnzA + 1 + p.nnzP + 1 + 3 * (size_t)p.m + 2 * (size_t)p.npad +
+                             (size_t)solve_vlen(p.m, p.npad) + 160 + (size_t)p.nb * S) +
            ((p.m + 15) & ~15) + 64;
 }
 
-template <int NB, int A, int K, int CS, int RS, int W>
+template <int NB, int A, int K, int CS, int RS, int W, bool TRI = false>
 static hipError_t go(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st, size_t lds) {
-    auto k = k_solve<NB, A, K, CS, RS, W>;
+    auto k = k_solve<NB, A, K, CS, RS, W, TRI>;
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(T), lds, st, p, xo, yo, fo);
@@ -917,29 +1073,48 @@ static hipError_t go(const KParams& p, long B, double* xo, double* yo, int fo, h
 
 // Instantiations: NB = register-resident factor blocks (0: tiles read from the
 // workspace), A = coupling rows of F_k, K = gather-list length, CS / RS = columns /
-// rows per thread, W = waves per SIMD the register budget is sized for.
-int solve_variant(const KParams& p) {
+// rows per thread, W = waves per SIMD the register budget is sized for, TRI =
+// three-phase solve.  variant_fits() is the exact precondition of each.
+bool variant_fits(const KParams& p, int v) {
     const int cs = (p.npad + T - 1) / T, rs = (p.m + T - 1) / T;
-    if (p.nb == 4 && p.amax <= 8 && p.gk <= 6 && cs <= 1 && rs <= 1) return 0;
-    if (p.nb == 8 && p.amax <= 8 && p.gk <= 8 && cs <= 1 && rs <= 1) return 1;
-    if (p.nb == 8 && p.amax <= 16 && p.gk <= 8 && cs <= 1 && rs <= 1) return 2;
-    if (p.nb == 8 && p.amax <= 16 && p.gk <= 8 && cs <= 1 && rs <= 2) return 3;
-    if (p.gk <= 8 && cs <= 2 && rs <= 4) return 4;
-    if (p.gk <= 8 && cs <= 4 && rs <= 4) return 5;
-    if (cs <= 8 && rs <= 8) return 6;
+    switch (v) {
+        case 0: case 7: return p.nb == 4 && p.amax <= 8 && p.gk <= 6 && cs <= 1 && rs <= 1;
+        case 1: return p.nb == 8 && p.amax <= 8 && p.gk <= 8 && cs <= 1 && rs <= 1;
+        case 2: return p.nb == 8 && p.amax <= 16 && p.gk <= 8 && cs <= 1 && rs <= 1;
+        case 3: return p.nb == 8 && p.amax <= 16 && p.gk <= 8 && cs <= 1 && rs <= 2;
+        case 4: return p.gk <= 8 && cs <= 2 && rs <= 4;
+        case 5: return p.gk <= 8 && cs <= 4 && rs <= 4;
+        case 6: return p.gk <= 16 && cs <= 8 && rs <= 8;
+        default: return false;
+    }
+}
+
+int solve_variant(const KParams& p) {
+    static const int order[] = {0, 1, 2, 3, 4, 5, 6};
+    for (int v : order)
+        if (variant_fits(p, v)) return v;
     return -1;
+}
+
+int solve_mode(int variant) {  // what factorize stores for the variant (KParams::mode)
+    switch (variant) {
+        case 0: return 2;
+        case 1: case 2: case 3: case 7: return 1;
+        default: return 0;
+    }
 }
 
 hipError_t launch_solve(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st) {
     const size_t lds = lds_solve_bytes(p);
-    switch (solve_variant(p)) {
-        case 0: return go<4, 8, 6, 1, 1, 4>(p, B, xo, yo, factor_only, st, lds);
+    switch (p.variant) {
+        case 0: return go<4, 8, 6, 1, 1, 4, true>(p, B, xo, yo, factor_only, st, lds);
         case 1: return go<8, 8, 8, 1, 1, 4>(p, B, xo, yo, factor_only, st, lds);
         case 2: return go<8, 16, 8, 1, 1, 2>(p, B, xo, yo, factor_only, st, lds);
         case 3: return go<8, 16, 8, 1, 2, 2>(p, B, xo, yo, factor_only, st, lds);
         case 4: return go<0, 32, 8, 2, 4, 2>(p, B, xo, yo, factor_only, st, lds);
         case 5: return go<0, 32, 8, 4, 4, 2>(p, B, xo, yo, factor_only, st, lds);
         case 6: return go<0, 32, 16, 8, 8, 1>(p, B, xo, yo, factor_only, st, lds);
+        case 7: return go<4, 8, 6, 1, 1, 4, false>(p, B, xo, yo, factor_only, st, lds);
         default: return hipErrorInvalidValue;
     }
 }
