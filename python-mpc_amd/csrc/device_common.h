@@ -108,26 +108,39 @@ __device__ __forceinline__ double wave_sum(double v) {
     return lane63(v);
 }
 
-// block-wide max / sum of K values (OSQP c_max semantics per comparison)
-template <int K>
+// Workgroup-wide max / sum of K values over TT threads (OSQP c_max semantics per
+// comparison).  A one-wave workgroup (TT = 64) reduces in registers only; wider
+// ones go through red[] (TT/64 * K slots).
+template <int TT, int K>
 __device__ __forceinline__ void block_max(double (&v)[K], double* red) {
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if constexpr (TT == 64) {
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const double r = wave_max(v[k]);
-        if (lane == 0) red[wid * K + k] = r;
+        for (int k = 0; k < K; ++k) v[k] = wave_max(v[k]);
+    } else {
+        constexpr int NW = TT / 64;
+        const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const double r = wave_max(v[k]);
+            if (lane == 0) red[wid * K + k] = r;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            double r = red[k];
+#pragma unroll
+            for (int w = 1; w < NW; ++w) r = cmax(r, red[w * K + k]);
+            v[k] = r;
+        }
+        __syncthreads();
     }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-        v[k] = cmax(cmax(red[k], red[K + k]), cmax(red[2 * K + k], red[3 * K + k]));
-    __syncthreads();
 }
 
 // block-wide max of K values into out[0..K) (LDS), computed by threads k < K;
-// visible to every thread after the trailing barrier.  red needs 4*K slots.
-template <int K>
+// visible to every thread after the trailing barrier.  red needs TT/64*K slots.
+template <int TT, int K>
 __device__ __forceinline__ void block_max_to(const double (&v)[K], double* red, double* out) {
+    constexpr int NW = TT / 64;
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, t = threadIdx.x;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -135,32 +148,57 @@ __device__ __forceinline__ void block_max_to(const double (&v)[K], double* red, 
         if (lane == 0) red[wid * K + k] = r;
     }
     __syncthreads();
-    if (t < K) out[t] = cmax(cmax(red[t], red[K + t]), cmax(red[2 * K + t], red[3 * K + t]));
-    __syncthreads();
-}
-
-template <int K>
-__device__ __forceinline__ void block_sum(double (&v)[K], double* red) {
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (t < K) {
+        double r = red[t];
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const double r = wave_sum(v[k]);
-        if (lane == 0) red[wid * K + k] = r;
+        for (int w = 1; w < NW; ++w) r = cmax(r, red[w * K + t]);
+        out[t] = r;
     }
     __syncthreads();
-#pragma unroll
-    for (int k = 0; k < K; ++k) v[k] = (red[k] + red[K + k]) + (red[2 * K + k] + red[3 * K + k]);
-    __syncthreads();
 }
 
+template <int TT, int K>
+__device__ __forceinline__ void block_sum(double (&v)[K], double* red) {
+    if constexpr (TT == 64) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k] = wave_sum(v[k]);
+    } else {
+        constexpr int NW = TT / 64;
+        const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const double r = wave_sum(v[k]);
+            if (lane == 0) red[wid * K + k] = r;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            double r = red[k];
+            if constexpr (NW == 4) {
+                r = (red[k] + red[K + k]) + (red[2 * K + k] + red[3 * K + k]);
+            } else {
+#pragma unroll
+                for (int w = 1; w < NW; ++w) r += red[w * K + k];
+            }
+            v[k] = r;
+        }
+        __syncthreads();
+    }
+}
+
+template <int TT>
 __device__ __forceinline__ bool block_any(bool f, int* flag) {
-    if (threadIdx.x == 0) *flag = 0;
-    __syncthreads();
-    if (f) *flag = 1;
-    __syncthreads();
-    bool r = *flag != 0;
-    __syncthreads();
-    return r;
+    if constexpr (TT == 64) {
+        return __builtin_amdgcn_ballot_w64(f) != 0;
+    } else {
+        if (threadIdx.x == 0) *flag = 0;
+        __syncthreads();
+        if (f) *flag = 1;
+        __syncthreads();
+        bool r = *flag != 0;
+        __syncthreads();
+        return r;
+    }
 }
 
 }  // namespace mpcqp

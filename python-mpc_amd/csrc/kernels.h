@@ -7,8 +7,9 @@
 namespace mpcqp {
 
 constexpr int kThreads = 256;
-constexpr int kProfSlots = 12;  // factor, rhs, bt_solve, update, checks, tail, total cycles, total 100 MHz ticks,
-                                // factor split: assembly, F/S products, Gauss-Jordan, block epilogue  // one workgroup (4 wavefronts) per QP instance
+constexpr int kProfSlots = 16;  // factor, rhs, bt_solve, update, checks, tail, total cycles, total 100 MHz ticks,
+                                // factor split: assembly, F/S products, Gauss-Jordan, block epilogue,
+                                // solve split (wave kernels): phase A, phase B, phase C, spare
 
 // status values (OSQP constants.h)
 enum : int {
@@ -56,5 +57,7 @@ int solve_variant(const KParams& p);  // -1: no instantiation fits the plan
 int solve_mode(int variant);
 bool variant_fits(const KParams& p, int variant);
 hipError_t launch_solve(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st);
+// one-wave-per-QP kernel (solve_wave.hip), variants 8 and 9
+hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st);
 
 }  // namespace mpcqp

@@ -95,8 +95,8 @@ __global__ __launch_bounds__(T) void k_setup(KParams p, const double* __restrict
             acc[0] += d1;
             mq[0] = cmax(mq[0], fabs(qv[pc]));
         }
-        block_sum(acc, red);
-        block_max(mq, red);
+        block_sum<T>(acc, red);
+        block_max<T>(mq, red);
         double ct = acc[0] / (double)n;
         double nq = limit_scaling(mq[0]);
         ct = limit_scaling(cmax(ct, nq));
@@ -127,7 +127,7 @@ __global__ __launch_bounds__(T) void k_setup(KParams p, const double* __restrict
         p.z[b * m + i] = 0.0;
         p.y[b * m + i] = 0.0;
     }
-    bad = block_any(bad, flag);
+    bad = block_any<T>(bad, flag);
     for (int i = tid; i < nnzP; i += T) p.Px[b * nnzP + i] = Pv[i];
     for (int i = tid; i < nnzA; i += T) p.Ax[b * nnzA + i] = Av[i];
     for (int pc = tid; pc < npad; pc += T) {
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(T) void k_update(KParams p, const double* __restric
             p.ct[b * m + i] = t;
         }
     }
-    bad = block_any(bad, flag);
+    bad = block_any<T>(bad, flag);
     if (tid == 0) {
         p.status[b] = MPCQP_UNSOLVED_;
         if (l_in || u_in) p.err[b] = bad ? 1 : 0;

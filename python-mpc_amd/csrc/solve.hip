@@ -24,170 +24,10 @@
 
 #include <type_traits>
 
-#include "device_common.h"
+#include "solve_phases.h"
 
 namespace mpcqp {
 
-
-struct SLds {
-    double *Acsc, *Pv, *lo, *up, *qv;
-    double *w, *rb, *xt, *ys;        // per-iteration vectors (aliased by the factor scratch)
-    double* dx;                      // delta x of the last iteration (rb, or xt in mode 2)
-    double* cor;                     // three-phase solve corrections (nb * S, rows < A used)
-    double *SP, *EK, *DK;            // factorisation scratch (3 tiles)
-    double* red;
-    double* res;                     // last update_info results (14 doubles)
-    long long* pacc;                 // phase timers (diagnostic)
-    signed char* ct;
-    int* flag;
-};
-
-__device__ __forceinline__ double rho_of(signed char t, double rho) {
-    return t < 0 ? RHO_MIN : (t > 0 ? RHO_EQ_OVER_RHO_INEQ * rho : rho);
-}
-
-// Assemble K's tiles for the current rho and factor them (block LDL'):
-//   S_0 = D_0,  F_k = E_k S_{k-1}^{-1},  S_k = D_k - F_k E_k',  H_{k-1} = F_k'
-// E_k is nonzero only in its first amax rows (block k's first BFS level), so F_k
-// has amax nonzero rows and F_k E_k' touches only the leading amax x amax corner
-// of S_k.  F_k, H_k, S_k^{-1} go to the per-instance workspace (Fg, Hg, Sg); their
-// entries outside those rows / columns are never written (zero from allocation).
-// S_k^{-1} by Gauss-Jordan (SPD: no pivoting) on register-resident tile elements.
-// What else is stored depends on the solve variant (KParams::mode):
-//   0: F_k and H_k = F_k' as full tiles (solves reading the tiles from the workspace)
-//   1: F_k only (register sweep; H is loaded as F transposed)
-//   2: the blocks of L^{-1}:  G_kj = (-1)^{k-j} F_k F_{k-1} .. F_{j+1}  (j < k), amax x 32
-//      each, in Hg at pair (k, j) -> k(k-1)/2 + j, row stride 32 (three-phase solve).
-// Returns false on a non-positive pivot (OSQP: "problem non convex").
-template <class KP>
-__device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, double* __restrict__ Fg,
-                                          double* __restrict__ Hg, double* __restrict__ Sg) {
-    const int tid = threadIdx.x, i = tid >> 3, jg = tid & 7;
-    const int nb = p.nb, amax = p.amax, ntgt = p.ntgt, tmax = p.term_max, mode = p.mode;
-    const long gstride = (long)amax * S;
-    const int2* __restrict__ tt = (const int2*)p.tterm;
-    bool ok = true;
-    double* SP = L.SP;
-    double* DK = L.DK;
-    double* EK = L.EK;
-#ifdef MPCQP_PHASE_PROF
-    long long tf = clock64();
-#define FPH(k) if (tid == 0) { const long long t_ = clock64(); L.pacc[k] += t_ - tf; tf = t_; }
-#else
-#define FPH(k)
-#endif
-#pragma unroll 1
-    for (int k = 0; k < nb; ++k) {
-        for (int e = tid; e < SS; e += T) { DK[e] = 0.0; EK[e] = 0.0; }
-        __syncthreads();
-        if (tid < S) DK[tid * S + tid] = p.pad_var[k * S + tid] >= 0 ? p.sigma : 1.0;
-        __syncthreads();
-        // every target has one owner: its terms are summed in plan order
-#pragma unroll 1
-        for (int t = p.asm_blk_ptr[k] + tid; t < p.asm_blk_ptr[k + 1]; t += T) {
-            double acc = 0.0;
-#pragma unroll 4
-            for (int j = 0; j < tmax; ++j) {
-                const int2 w = tt[(long)j * ntgt + t];
-                const int a = w.x & 0xFFFF, bb = (int)((unsigned)w.x >> 16), r = w.y;
-                acc += r < 0 ? L.Pv[a] : rho_of(L.ct[r], rho) * L.Acsc[a] * L.Acsc[bb];
-            }
-            const int tg = p.asm_tgt[t];
-            if (tg < SS) DK[tg] += acc;
-            else EK[tg - SS] += acc;
-        }
-        __syncthreads();
-        FPH(8)
-        if (k > 0) {
-            // F_k = E_k S_{k-1}^{-1} (rows < amax), then written over S_{k-1}^{-1}'s tile
-            double f[4];
-            int nf = 0;
-#pragma unroll 1
-            for (int o = tid; o < amax * S; o += T, ++nf) {
-                const int r = o >> 5, j = o & (S - 1);
-                double sacc = 0.0;
-#pragma unroll 8
-                for (int l = 0; l < S; ++l) sacc += EK[r * S + l] * SP[l * S + j];
-                f[nf & 3] = sacc;
-                if (mode < 2) Fg[(long)k * SS + r * S + j] = sacc;
-                if (mode == 0) Hg[(long)(k - 1) * SS + j * S + r] = sacc;
-                if (mode == 2) Hg[(long)(k * (k - 1) / 2 + k - 1) * gstride + o] = -sacc;
-            }
-            __syncthreads();  // every read of S_{k-1}^{-1} done
-            nf = 0;
-#pragma unroll 1
-            for (int o = tid; o < amax * S; o += T, ++nf) SP[o] = f[nf & 3];
-            __syncthreads();
-            if (mode == 2) {  // G_kj = -F_k G_{k-1,j} (G_{k-1,j} has amax nonzero rows)
-#pragma unroll 1
-                for (int j = 0; j < k - 1; ++j) {
-                    const double* Gp = Hg + (long)((k - 1) * (k - 2) / 2 + j) * gstride;
-                    double* Gk = Hg + (long)(k * (k - 1) / 2 + j) * gstride;
-#pragma unroll 1
-                    for (int o = tid; o < amax * S; o += T) {
-                        const int r = o >> 5, c = o & (S - 1);
-                        double sacc = 0.0;
-#pragma unroll 1
-                        for (int l = 0; l < amax; ++l) sacc += SP[r * S + l] * Gp[l * S + c];
-                        Gk[o] = -sacc;
-                    }
-                }
-            }
-            // S_k = D_k - F_k E_k' on the leading amax x amax corner
-#pragma unroll 1
-            for (int o = tid; o < amax * amax; o += T) {
-                const int r = o / amax, c = o - r * amax;
-                double sacc = 0.0;
-#pragma unroll 8
-                for (int l = 0; l < S; ++l) sacc += SP[r * S + l] * EK[c * S + l];
-                DK[r * S + c] -= sacc;
-            }
-            __syncthreads();
-        }
-        FPH(9)
-        // Gauss-Jordan inverse with the tile in registers: thread (i, jg) keeps
-        // elements [i][jg + 8c]; per pivot only its row and column go through LDS
-        // (double-buffered in EK, free by now), so each pivot costs one barrier.
-        double v[4];
-#pragma unroll
-        for (int cc = 0; cc < 4; ++cc) v[cc] = DK[i * S + jg + 8 * cc];
-        double* rowbuf = EK;
-        double* colbuf = EK + 2 * S;
-#pragma unroll 1
-        for (int pv = 0; pv < S; ++pv) {
-            const int buf = (pv & 1) * S;
-            const int cp = pv >> 3;
-            if (i == pv) {
-#pragma unroll
-                for (int cc = 0; cc < 4; ++cc) rowbuf[buf + jg + 8 * cc] = v[cc];
-            }
-            if (jg == (pv & 7)) colbuf[buf + i] = cp == 0 ? v[0] : cp == 1 ? v[1] : cp == 2 ? v[2] : v[3];
-            __syncthreads();
-            const double piv = rowbuf[buf + pv];
-            const double colv = colbuf[buf + i];
-            if (!(piv > 0.0)) ok = false;
-            const double d = 1.0 / piv;
-#pragma unroll
-            for (int cc = 0; cc < 4; ++cc) {
-                const int j = jg + 8 * cc;
-                const double rowv = rowbuf[buf + j];
-                if (i == pv) v[cc] = (j == pv) ? d : rowv * d;
-                else if (j == pv) v[cc] = -colv * d;
-                else v[cc] = v[cc] - colv * (rowv * d);
-            }
-        }
-#pragma unroll
-        for (int cc = 0; cc < 4; ++cc) DK[i * S + jg + 8 * cc] = v[cc];
-        FPH(10)
-#pragma unroll
-        for (int cc = 0; cc < 4; ++cc) Sg[(long)k * SS + i * S + jg + 8 * cc] = v[cc];
-        double* t = SP; SP = DK; DK = t;  // S_k^{-1} becomes "previous"
-        __syncthreads();
-        FPH(11)
-    }
-#undef FPH
-    return ok;
-}
 
 // Register-resident factor.  F_k = E_k S_{k-1}^{-1} is nonzero only in the rows of
 // block k that couple to block k-1 (its first BFS level, local rows < A), and
@@ -411,412 +251,6 @@ __device__ __forceinline__ void tri_solve(const RegFactor3<NB, A>& R, double* rb
     __syncthreads();
 }
 
-// Gather list of one column (A' w) or row (A x) of A: K packed entries
-// (value position in the padded-CSC copy of A in LDS | vector index << 16), padded
-// with the zero slot Acsc[nnzA] -- no per-entry branches, all 2K LDS reads in flight.
-template <int K>
-struct Gather {
-    unsigned e[K];
-    __device__ __forceinline__ void load(const int* list) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) e[k] = (unsigned)list[k];
-    }
-    __device__ __forceinline__ void clear(int zero_pos) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) e[k] = (unsigned)zero_pos;
-    }
-    // an opaque zero offset keeps the LDS addresses from being hoisted into
-    // registers across the ADMM loop
-    __device__ __forceinline__ double dot(const double* A, const double* vec) const {
-        int opq = 0;
-        asm volatile("" : "+s"(opq));
-        double t[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const unsigned ek = e[k] + (unsigned)opq;  // unpacked inside the loop: the packed
-            t[k] = A[ek & 0xFFFFu] * vec[ek >> 16];    // word is the only register it costs
-        }
-#pragma unroll
-        for (int w = 1; w < K; w *= 2)
-#pragma unroll
-            for (int k = 0; k + w < K; k += 2 * w) t[k] += t[k + w];
-        return t[0];
-    }
-};
-
-struct Res {  // update_info results
-    double pri, dua, nz, nax, nq, naty, npx;    // termination (unscaled)
-    double rpri, rdua, rz, rax, rq, raty, rpx;  // rho estimate (scaled space)
-    __device__ __forceinline__ void save(double* d) const {
-        d[0] = pri; d[1] = dua; d[2] = nz; d[3] = nax; d[4] = nq; d[5] = naty; d[6] = npx;
-        d[7] = rpri; d[8] = rdua; d[9] = rz; d[10] = rax; d[11] = rq; d[12] = raty; d[13] = rpx;
-    }
-    __device__ __forceinline__ void restore(const double* d) {
-        pri = d[0]; dua = d[1]; nz = d[2]; nax = d[3]; nq = d[4]; naty = d[5]; npx = d[6];
-        rpri = d[7]; rdua = d[8]; rz = d[9]; rax = d[10]; rq = d[11]; raty = d[12]; rpx = d[13];
-    }
-};
-
-// LDS carve of the solve kernel (doubles unless noted):
-//   Acsc[nnzA+1] Pv[nnzP+1] lo[m] up[m] qv[npad] X[npad] Z[m]
-//   V = max(3 S*S, w[m] rb[npad] xt[npad] ys[m] dY[m])   (factor scratch aliases the vectors)
-//   red[128] res[16] pacc[16] cor[nb*S] ct[m bytes] flag
-// rb holds delta_x and dY delta_y of the last iteration after its update phase;
-// ys holds y whenever the out-of-line phases run.
-__host__ __device__ inline long solve_vlen(int m, int npad) {
-    const long a = 3L * m + 2L * npad, b = 3L * SS;
-    return a > b ? a : b;
-}
-
-struct SL2 {  // full carve (SLds + the solve-kernel-only arrays)
-    SLds L;
-    double *X, *Z, *dY;
-};
-
-template <class KP>
-__device__ __forceinline__ SL2 carve(const KP& p) {
-    extern __shared__ __attribute__((aligned(16))) double sm[];
-    SL2 c;
-    const int m = p.m, npad = p.npad;
-    c.L.Acsc = sm;
-    c.L.Pv = c.L.Acsc + p.nnzA + 1;  // Acsc[nnzA] = 0: gather padding
-    c.L.lo = c.L.Pv + p.nnzP + 1;  // Pv[nnzP] = 0: P-list padding
-    c.L.up = c.L.lo + m;
-    c.L.qv = c.L.up + m;
-    c.X = c.L.qv + npad;
-    c.Z = c.X + npad;
-    double* V = c.Z + m;
-    c.L.w = V;
-    c.L.rb = c.L.w + m;
-    c.L.xt = c.L.rb + npad;
-    c.L.ys = c.L.xt + npad;
-    c.dY = c.L.ys + m;
-    c.L.SP = V;
-    c.L.EK = c.L.SP + SS;
-    c.L.DK = c.L.EK + SS;
-    c.L.red = V + solve_vlen(m, npad);
-    c.L.res = c.L.red + 128;
-    c.L.pacc = (long long*)(c.L.res + 16);
-    c.L.cor = (double*)(c.L.pacc + 16);
-    c.L.dx = p.mode == 2 ? c.L.xt : c.L.rb;
-    c.L.ct = (signed char*)(c.L.cor + p.nb * S);
-    c.L.flag = (int*)(c.L.ct + ((m + 15) & ~15));
-    return c;
-}
-
-// LDS scalar slots (in res[14..15] and flag[1..]): shared outcome of the out-of-line phases
-struct Shared {
-    double* res;  // [0..13] Res, [14] obj, [15] new rho
-    int* flag;    // [0] scratch, [1] status, [2] dx_scaled, [3] dy_scaled
-};
-
-// ---- out-of-line phases: everything they need is in LDS or in the plan ----
-// dot of a packed gather list (value index | vector index << 16) with cnt entries
-__device__ __forceinline__ double list_dot(const int* __restrict__ list, int cnt, const double* V, const double* v) {
-    double acc = 0.0;
-#pragma unroll 4
-    for (int k = 0; k < cnt; ++k) {
-        const unsigned e = (unsigned)list[k];
-        acc += V[e & 0xFFFFu] * v[e >> 16];
-    }
-    return acc;
-}
-template <class KP>
-__device__ __forceinline__ double row_dot(const KP& p, const double* A, const double* v, int i) {
-    return list_dot(p.grow + (long)i * kGS, p.gk, A, v);
-}
-template <class KP>
-__device__ __forceinline__ double col_dot(const KP& p, const double* A, const double* v, int pc) {
-    return list_dot(p.gcol + (long)pc * kGS, p.gk, A, v);
-}
-template <class KP>
-__device__ __forceinline__ double psym_dot(const KP& p, const double* Pv, const double* v, int pc) {
-    return list_dot(p.gpsym + (long)pc * kGS, p.pk, Pv, v);
-}
-
-// update_info: residuals and the norms of their tolerances (OSQP compute_pri_res /
-// compute_dua_res / compute_pri_tol / compute_dua_tol, scaled and unscaled)
-__device__ __noinline__ void update_info_nl(const KParams* gp, long b, double cinv) {
-    KPc& p = kconst(gp);
-    SL2 c = carve(p);
-    const int tid = threadIdx.x, m = p.m, npad = p.npad;
-    const double* Eg = p.E + b * m;
-    const double* Dg = p.D + b * npad;
-    double v[14];
-#pragma unroll
-    for (int k = 0; k < 14; ++k) v[k] = 0.0;
-    #pragma unroll 1
-    for (int i = tid; i < m; i += T) {
-        const double ax = row_dot(p, c.L.Acsc, c.X, i);
-        const double zi = c.Z[i];
-        const double pr = ax - zi;
-        const double ei = 1.0 / Eg[i];
-        v[0] = cmax(v[0], fabs(ei * pr));
-        v[2] = cmax(v[2], fabs(ei * zi));
-        v[3] = cmax(v[3], fabs(ei * ax));
-        v[7] = cmax(v[7], fabs(pr));
-        v[9] = cmax(v[9], fabs(zi));
-        v[10] = cmax(v[10], fabs(ax));
-    }
-    #pragma unroll 1
-    for (int pc = tid; pc < npad; pc += T) {
-        if (p.pad_var[pc] < 0) continue;
-        const double px = psym_dot(p, c.L.Pv, c.X, pc);
-        const double aty = col_dot(p, c.L.Acsc, c.L.ys, pc);
-        const double q = c.L.qv[pc];
-        const double d = (q + px) + aty;
-        const double di = 1.0 / Dg[pc];
-        v[1] = cmax(v[1], fabs(di * d));
-        v[4] = cmax(v[4], fabs(di * q));
-        v[5] = cmax(v[5], fabs(di * aty));
-        v[6] = cmax(v[6], fabs(di * px));
-        v[8] = cmax(v[8], fabs(d));
-        v[11] = cmax(v[11], fabs(q));
-        v[12] = cmax(v[12], fabs(aty));
-        v[13] = cmax(v[13], fabs(px));
-    }
-    double* r = c.L.red + 64;
-    block_max_to(v, c.L.red, r);
-    if (tid == 0) {
-        Res R;
-        if (p.scaling && !p.scaled_term) {
-            R.pri = r[0]; R.dua = cinv * r[1];
-            R.nz = r[2]; R.nax = r[3]; R.nq = r[4]; R.naty = r[5]; R.npx = r[6];
-        } else {
-            R.pri = r[7]; R.dua = r[8];
-            R.nz = r[9]; R.nax = r[10]; R.nq = r[11]; R.naty = r[12]; R.npx = r[13];
-        }
-        R.rpri = r[7]; R.rdua = r[8]; R.rz = r[9]; R.rax = r[10]; R.rq = r[11]; R.raty = r[12]; R.rpx = r[13];
-        if (m == 0) R.pri = 0.0;
-        R.save(c.L.res);
-    }
-    __syncthreads();
-}
-
-// is_primal_infeasible (delta_y in dY, projected in place as OSQP does)
-template <class KP>
-__device__ bool primal_infeasible(const KP& p, SL2& c, long b, double eps) {
-    const int tid = threadIdx.x, m = p.m, npad = p.npad;
-    const bool unscale = p.scaling && !p.scaled_term;
-    const double* Eg = p.E + b * m;
-    const double* Dg = p.D + b * npad;
-    double nd[1] = {0.0};
-    #pragma unroll 1
-    for (int i = tid; i < m; i += T) {
-        double d = c.dY[i];
-        if (c.L.up[i] > OSQP_INFTY * MIN_SCALING) d = (c.L.lo[i] < -OSQP_INFTY * MIN_SCALING) ? 0.0 : cmin(d, 0.0);
-        else if (c.L.lo[i] < -OSQP_INFTY * MIN_SCALING) d = cmax(d, 0.0);
-        c.dY[i] = d;
-        nd[0] = cmax(nd[0], fabs(unscale ? Eg[i] * d : d));
-    }
-    block_max(nd, c.L.red);
-    const double norm_dy = nd[0];
-    if (!(norm_dy > eps)) return false;
-    double sum[1] = {0.0};
-    #pragma unroll 1
-    for (int i = tid; i < m; i += T) sum[0] += c.L.up[i] * cmax(c.dY[i], 0.0) + c.L.lo[i] * cmin(c.dY[i], 0.0);
-    block_sum(sum, c.L.red);
-    if (!(sum[0] < eps * norm_dy)) return false;
-    double na[1] = {0.0};
-    #pragma unroll 1
-    for (int pc = tid; pc < npad; pc += T) {
-        if (p.pad_var[pc] < 0) continue;
-        double a = col_dot(p, c.L.Acsc, c.dY, pc);
-        if (unscale) a *= 1.0 / Dg[pc];
-        na[0] = cmax(na[0], fabs(a));
-    }
-    block_max(na, c.L.red);
-    return na[0] < eps * norm_dy;
-}
-
-// is_dual_infeasible (delta_x in dx)
-template <class KP>
-__device__ bool dual_infeasible(const KP& p, SL2& c, long b, double cs_, double eps) {
-    const int tid = threadIdx.x, m = p.m, npad = p.npad;
-    const bool unscale = p.scaling && !p.scaled_term;
-    const double* Eg = p.E + b * m;
-    const double* Dg = p.D + b * npad;
-    const double cs = unscale ? cs_ : 1.0;
-    double v[1] = {0.0}, sum[1] = {0.0};
-    #pragma unroll 1
-    for (int pc = tid; pc < npad; pc += T) {
-        if (p.pad_var[pc] < 0) continue;
-        const double dx = c.L.dx[pc];
-        v[0] = cmax(v[0], fabs(unscale ? Dg[pc] * dx : dx));
-        sum[0] += c.L.qv[pc] * dx;
-    }
-    block_max(v, c.L.red);
-    const double norm_dx = v[0];
-    if (!(norm_dx > eps)) return false;
-    block_sum(sum, c.L.red);
-    if (!(sum[0] < cs * eps * norm_dx)) return false;
-    double np[1] = {0.0};
-    #pragma unroll 1
-    for (int pc = tid; pc < npad; pc += T) {
-        if (p.pad_var[pc] < 0) continue;
-        double a = psym_dot(p, c.L.Pv, c.L.dx, pc);
-        if (unscale) a *= 1.0 / Dg[pc];
-        np[0] = cmax(np[0], fabs(a));
-    }
-    block_max(np, c.L.red);
-    if (!(np[0] < cs * eps * norm_dx)) return false;
-    bool viol = false;
-    #pragma unroll 1
-    for (int i = tid; i < m; i += T) {
-        double a = row_dot(p, c.L.Acsc, c.L.dx, i);
-        if (unscale) a *= 1.0 / Eg[i];
-        if ((c.L.up[i] < OSQP_INFTY * MIN_SCALING && a > eps * norm_dx) ||
-            (c.L.lo[i] > -OSQP_INFTY * MIN_SCALING && a < -eps * norm_dx))
-            viol = true;
-    }
-    return !block_any(viol, c.L.flag);
-}
-
-// check_termination on the Res in LDS; status / obj / certificate flags in LDS.
-__device__ __noinline__ int check_termination_nl(const KParams* gp, long b, double cval, double cinv,
-                                                 int approximate) {
-    KPc& p = kconst(gp);
-    SL2 c = carve(p);
-    Res R;
-    R.restore(c.L.res);
-    double eps_abs = p.eps_abs, eps_rel = p.eps_rel, eps_pinf = p.eps_pinf, eps_dinf = p.eps_dinf;
-    int st = MPCQP_UNSOLVED_;
-    double obj = c.L.res[14];
-    bool done = false;
-    if (R.pri > OSQP_INFTY || R.dua > OSQP_INFTY) {
-        st = MPCQP_NON_CVX_;
-        obj = __builtin_nan("");
-        done = true;
-    } else {
-        if (approximate) { eps_abs *= 10; eps_rel *= 10; eps_pinf *= 10; eps_dinf *= 10; }
-        bool prim_ok = false, dual_ok = false, prim_inf = false, dual_inf = false;
-        const bool unscale = p.scaling && !p.scaled_term;
-        if (p.m == 0) prim_ok = true;
-        else {
-            const double ep = eps_abs + eps_rel * cmax(R.nz, R.nax);
-            if (R.pri < ep) prim_ok = true;
-            else prim_inf = primal_infeasible(p, c, b, eps_pinf);
-        }
-        double mx = cmax(cmax(R.nq, R.naty), R.npx);
-        if (unscale) mx *= cinv;
-        if (R.dua < eps_abs + eps_rel * mx) dual_ok = true;
-        else dual_inf = dual_infeasible(p, c, b, cval, eps_dinf);
-        if (prim_ok && dual_ok) {
-            st = approximate ? MPCQP_SOLVED_INACCURATE_ : MPCQP_SOLVED_;
-            done = true;
-        } else if (prim_inf) {
-            st = approximate ? MPCQP_PRIMAL_INFEASIBLE_INACCURATE_ : MPCQP_PRIMAL_INFEASIBLE_;
-            obj = OSQP_INFTY;
-            if (threadIdx.x == 0) c.L.flag[3] = unscale;
-            done = true;
-        } else if (dual_inf) {
-            st = approximate ? MPCQP_DUAL_INFEASIBLE_INACCURATE_ : MPCQP_DUAL_INFEASIBLE_;
-            obj = -OSQP_INFTY;
-            if (threadIdx.x == 0) c.L.flag[2] = unscale;
-            done = true;
-        }
-    }
-    __syncthreads();
-    if (done && threadIdx.x == 0) { c.L.flag[1] = st; c.L.res[14] = obj; }
-    __syncthreads();
-    return done ? st : MPCQP_UNSOLVED_;
-}
-
-// compute_obj_val (needs X)
-__device__ __noinline__ void objective_nl(const KParams* gp, double cinv) {
-    KPc& p = kconst(gp);
-    SL2 c = carve(p);
-    const int tid = threadIdx.x;
-    double sacc[1] = {0.0};
-    #pragma unroll 1
-    for (int v = tid; v < p.nnzP; v += T) {
-        const int r = p.p_r[v], cc = p.p_c[v];
-        sacc[0] += (r == cc) ? 0.5 * c.L.Pv[v] * c.X[r] * c.X[r] : c.L.Pv[v] * c.X[r] * c.X[cc];
-    }
-    #pragma unroll 1
-    for (int pc = tid; pc < p.npad; pc += T) sacc[0] += c.L.qv[pc] * c.X[pc];
-    block_sum(sacc, c.L.red);
-    if (tid == 0) c.L.res[14] = p.scaling ? sacc[0] * cinv : sacc[0];
-    __syncthreads();
-}
-
-// store_solution + info (y is in ys)
-__device__ __noinline__ void finalize_nl(const KParams* gp, long b, double* __restrict__ xo,
-                                         double* __restrict__ yo, double cinv, double rho, int status,
-                                         int info_iter, int rho_updates) {
-    KPc& p = kconst(gp);
-    SL2 c = carve(p);
-    const int tid = threadIdx.x, n = p.n, m = p.m, npad = p.npad;
-    const double* Eg = p.E + b * m;
-    const double* Dg = p.D + b * npad;
-    Res R;
-    R.restore(c.L.res);
-    const double obj = c.L.res[14];
-    double rho_est;
-    {
-        const double pr = R.rpri / (cmax(R.rz, R.rax) + DIVISION_TOL);
-        const double du = R.rdua / (cmax(cmax(R.rq, R.raty), R.rpx) + DIVISION_TOL);
-        rho_est = cmin(cmax(rho * sqrt(pr / (du + DIVISION_TOL)), RHO_MIN), RHO_MAX);
-    }
-    const bool has_sol = !(status == MPCQP_PRIMAL_INFEASIBLE_ || status == MPCQP_PRIMAL_INFEASIBLE_INACCURATE_ ||
-                           status == MPCQP_DUAL_INFEASIBLE_ || status == MPCQP_DUAL_INFEASIBLE_INACCURATE_ ||
-                           status == MPCQP_NON_CVX_);
-    const bool pinf = status == MPCQP_PRIMAL_INFEASIBLE_ || status == MPCQP_PRIMAL_INFEASIBLE_INACCURATE_;
-    const bool dinf = status == MPCQP_DUAL_INFEASIBLE_ || status == MPCQP_DUAL_INFEASIBLE_INACCURATE_;
-    const bool dx_scaled = c.L.flag[2] != 0, dy_scaled = c.L.flag[3] != 0;
-    double nrm[2] = {0.0, 0.0};
-    #pragma unroll 1
-    for (int pc = tid; pc < npad; pc += T) {
-        double dx = c.L.dx[pc];
-        if (dx_scaled) dx *= Dg[pc];
-        c.L.dx[pc] = dx;
-        nrm[1] = cmax(nrm[1], fabs(dx));
-    }
-    #pragma unroll 1
-    for (int i = tid; i < m; i += T) {
-        double dy = c.dY[i];
-        if (dy_scaled) dy *= Eg[i];
-        c.dY[i] = dy;
-        nrm[0] = cmax(nrm[0], fabs(dy));
-    }
-    block_max(nrm, c.L.red);
-    #pragma unroll 1
-    for (int pc = tid; pc < npad; pc += T) {
-        const int j = p.pad_var[pc];
-        const double xv = c.X[pc];
-        if (j >= 0) {
-            if (xo) xo[b * n + j] = has_sol ? (p.scaling ? Dg[pc] * xv : xv) : __builtin_nan("");
-            p.dxc[b * n + j] = dinf ? c.L.dx[pc] * (1.0 / nrm[1]) : c.L.dx[pc];
-        }
-        p.x[b * npad + pc] = has_sol ? xv : 0.0;
-    }
-    #pragma unroll 1
-    for (int i = tid; i < m; i += T) {
-        const double yv = c.L.ys[i];
-        if (yo) yo[b * m + i] = has_sol ? (p.scaling ? (Eg[i] * yv) * cinv : yv) : __builtin_nan("");
-        p.dyc[b * m + i] = pinf ? c.dY[i] * (1.0 / nrm[0]) : c.dY[i];
-        p.y[b * m + i] = has_sol ? yv : 0.0;
-        p.z[b * m + i] = has_sol ? c.Z[i] : 0.0;
-    }
-    if (tid == 0) {
-        p.status[b] = status;
-        p.iter[b] = info_iter;
-        p.rho_upd[b] = rho_updates;
-        p.obj[b] = obj;
-        p.pri[b] = R.pri;
-        p.dua[b] = R.dua;
-        p.rho_est[b] = rho_est;
-        p.scal[b * 4 + 2] = rho;
-    }
-}
-
-__device__ __noinline__ bool factorize_nl(const KParams* gp, long b, double rho) {
-    KPc& p = kconst(gp);
-    SL2 c = carve(p);
-    return factorize(p, c.L, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
-                     p.Si + b * (long)p.nb * SS);
-}
-
 template <int NB, int A, int K, int CS, int RS, int W, bool TRI>
 __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ xo, double* __restrict__ yo,
                                                 int factor_only) {
@@ -895,7 +329,7 @@ __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ 
         __syncthreads();
         if (need_factor) {  // start, and after a rho change
             need_factor = false;
-            const bool ok = factorize_nl(p.self, b, rho);
+            const bool ok = factorize_nl<T>(p.self, b, rho);
             if (!ok) {
                 if (iter == 0) {
                     for (int j = tid; j < n; j += T) if (xo) xo[b * n + j] = __builtin_nan("");
@@ -999,11 +433,11 @@ __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ 
         can_check = p.check_term && (iter % p.check_term == 0);
         const bool do_rho = p.adaptive_rho && p.rho_interval && (iter % p.rho_interval == 0);
         if (!can_check && !do_rho) break;  // max_iter reached
-        update_info_nl(p.self, b, cinv);
+        update_info_nl<T>(p.self, b, cinv);
         info_iter = iter;
         bool stop = false;
         if (can_check) {
-            status = check_termination_nl(p.self, b, cval, cinv, 0);
+            status = check_termination_nl<T>(p.self, b, cval, cinv, 0);
             stop = status != MPCQP_UNSOLVED_;
         }
         if (!stop && do_rho) {
@@ -1025,19 +459,19 @@ __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ 
     }
     // ys holds y here
     if (!can_check && status == MPCQP_UNSOLVED_) {
-        update_info_nl(p.self, b, cinv);
+        update_info_nl<T>(p.self, b, cinv);
         info_iter = iter;
-        status = check_termination_nl(p.self, b, cval, cinv, 0);
+        status = check_termination_nl<T>(p.self, b, cval, cinv, 0);
     }
     const bool has_sol = !(status == MPCQP_PRIMAL_INFEASIBLE_ || status == MPCQP_PRIMAL_INFEASIBLE_INACCURATE_ ||
                            status == MPCQP_DUAL_INFEASIBLE_ || status == MPCQP_DUAL_INFEASIBLE_INACCURATE_ ||
                            status == MPCQP_NON_CVX_);
-    if (has_sol) objective_nl(p.self, cinv);
+    if (has_sol) objective_nl<T>(p.self, cinv);
     if (status == MPCQP_UNSOLVED_) {
-        status = check_termination_nl(p.self, b, cval, cinv, 1);
+        status = check_termination_nl<T>(p.self, b, cval, cinv, 1);
         if (status == MPCQP_UNSOLVED_) status = MPCQP_MAX_ITER_REACHED_;
     }
-    finalize_nl(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates);
+    finalize_nl<T>(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates);
 #ifdef MPCQP_PHASE_PROF
     if (prof) {
         __syncthreads();
@@ -1057,9 +491,11 @@ __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ 
 
 // ------------------------------------------------------------ launcher --
 size_t lds_solve_bytes(const KParams& p) {
-    return sizeof(double) * ((size_t)p.nnzA + 1 + p.nnzP + 1 + 3 * (size_t)p.m + 2 * (size_t)p.npad +
-                             (size_t)solve_vlen(p.m, p.npad) + 160 + (size_t)p.nb * S) +
-           ((p.m + 15) & ~15) + 64;
+    const size_t mp = (size_t)solve_mpad(p.m);
+    return sizeof(double) * ((size_t)al2(p.nnzA + 1) + (size_t)al2(p.nnzP + 1) + 3 * mp + 2 * (size_t)p.npad +
+                             (size_t)solve_vlen(p.m, p.npad, p.nb, p.amax, p.mode) + 160 + (size_t)p.nb * S +
+                             (size_t)p.npad) +
+           mp + 64;
 }
 
 template <int NB, int A, int K, int CS, int RS, int W, bool TRI = false>
@@ -1085,12 +521,15 @@ bool variant_fits(const KParams& p, int v) {
         case 4: return p.gk <= 8 && cs <= 2 && rs <= 4;
         case 5: return p.gk <= 8 && cs <= 4 && rs <= 4;
         case 6: return p.gk <= 16 && cs <= 8 && rs <= 8;
+        case 8: return p.nb == 4 && p.amax <= 8 && p.gk <= 6 && p.m <= 3 * 64 && lds_solve_bytes(p) < 65536;
+        case 9: return p.nb == 4 && p.amax <= 8 && p.gk <= 8 && p.m <= 4 * 64 && lds_solve_bytes(p) < 65536;
+        case 10: return p.nb == 4 && p.amax <= 8 && p.gk <= 6 && p.m <= 2 * 128 && lds_solve_bytes(p) < 65536;
         default: return false;
     }
 }
 
 int solve_variant(const KParams& p) {
-    static const int order[] = {0, 1, 2, 3, 4, 5, 6};
+    static const int order[] = {10, 8, 9, 0, 1, 2, 3, 4, 5, 6};
     for (int v : order)
         if (variant_fits(p, v)) return v;
     return -1;
@@ -1098,7 +537,7 @@ int solve_variant(const KParams& p) {
 
 int solve_mode(int variant) {  // what factorize stores for the variant (KParams::mode)
     switch (variant) {
-        case 0: return 2;
+        case 0: case 8: case 9: case 10: return 2;
         case 1: case 2: case 3: case 7: return 1;
         default: return 0;
     }
@@ -1115,6 +554,7 @@ hipError_t launch_solve(const KParams& p, long B, double* xo, double* yo, int fa
         case 5: return go<0, 32, 8, 4, 4, 2>(p, B, xo, yo, factor_only, st, lds);
         case 6: return go<0, 32, 16, 8, 8, 1>(p, B, xo, yo, factor_only, st, lds);
         case 7: return go<4, 8, 6, 1, 1, 4, false>(p, B, xo, yo, factor_only, st, lds);
+        case 8: case 9: case 10: return launch_solve_wave(p, B, xo, yo, factor_only, st);
         default: return hipErrorInvalidValue;
     }
 }

@@ -1,0 +1,630 @@
+// solve_phases.h -- the parts of the ADMM solve shared by its two kernel shapes
+// (solve.hip: one 256-thread workgroup per QP; solve_wave.hip: one 64-lane wave per
+// QP): the LDS carve, the in-kernel factorisation of K, the packed gather lists
+// and the out-of-line phases (update_info, check_termination with the
+// infeasibility certificates, objective, store_solution).  Everything is templated
+// on TT, the number of threads working on one QP.
+//
+// Reference semantics: OSQP 0.6 as called at vehicle_lateral_mpc_slack_increment.py:248
+// and Control/MPC/mpc_dynamics.py:396; oracle/osqp_oracle.c restates the same
+// algorithm on the CPU.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "device_common.h"
+
+namespace mpcqp {
+
+struct SLds {
+    double *Acsc, *Pv, *lo, *up, *qv;
+    double *w, *rb, *xt, *ys;        // per-iteration vectors (aliased by the factor scratch)
+    double* dx;                      // delta x of the last iteration (rb, or xt in mode 2)
+    double* cor;                     // three-phase solve corrections (nb * S, rows < A used)
+    double* tv;                      // three-phase solve: D^{-1} L^{-1} b of the wave kernel (npad)
+    double* gl;                      // wave kernel: LDS copy of the G blocks (after the vectors in V)
+    double *SP, *EK, *DK;            // factorisation scratch (3 tiles)
+    double* red;
+    double* res;                     // last update_info results (14 doubles)
+    long long* pacc;                 // phase timers (diagnostic)
+    signed char* ct;
+    int* flag;
+};
+
+__device__ __forceinline__ double rho_of(signed char t, double rho) {
+    return t < 0 ? RHO_MIN : (t > 0 ? RHO_EQ_OVER_RHO_INEQ * rho : rho);
+}
+
+// Assemble K's tiles for the current rho and factor them (block LDL'):
+//   S_0 = D_0,  F_k = E_k S_{k-1}^{-1},  S_k = D_k - F_k E_k',  H_{k-1} = F_k'
+// E_k is nonzero only in its first amax rows (block k's first BFS level), so F_k
+// has amax nonzero rows and F_k E_k' touches only the leading amax x amax corner
+// of S_k.  F_k, H_k, S_k^{-1} go to the per-instance workspace (Fg, Hg, Sg); their
+// entries outside those rows / columns are never written (zero from allocation).
+// S_k^{-1} by Gauss-Jordan (SPD: no pivoting) on register-resident tile elements.
+// What else is stored depends on the solve variant (KParams::mode):
+//   0: F_k and H_k = F_k' as full tiles (solves reading the tiles from the workspace)
+//   1: F_k only (register sweep; H is loaded as F transposed)
+//   2: the blocks of L^{-1}:  G_kj = (-1)^{k-j} F_k F_{k-1} .. F_{j+1}  (j < k), amax x 32
+//      each, in Hg at pair (k, j) -> k(k-1)/2 + j, row stride 32 (three-phase solve).
+// Returns false on a non-positive pivot (OSQP: "problem non convex").
+template <int TT, class KP>
+__device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, double* __restrict__ Fg,
+                                          double* __restrict__ Hg, double* __restrict__ Sg) {
+    constexpr int NI = 256 / TT;  // Gauss-Jordan tile rows per thread
+    const int tid = threadIdx.x, i0 = tid >> 3, jg = tid & 7;
+    const int nb = p.nb, amax = p.amax, ntgt = p.ntgt, tmax = p.term_max, mode = p.mode;
+    const long gstride = (long)amax * S;
+    const int2* __restrict__ tt = (const int2*)p.tterm;
+    bool ok = true;
+    double* SP = L.SP;
+    double* DK = L.DK;
+    double* EK = L.EK;
+#ifdef MPCQP_PHASE_PROF
+    long long tf = clock64();
+#define FPH(k) if (tid == 0) { const long long t_ = clock64(); L.pacc[k] += t_ - tf; tf = t_; }
+#else
+#define FPH(k)
+#endif
+#pragma unroll 1
+    for (int k = 0; k < nb; ++k) {
+        for (int e = tid; e < SS; e += TT) { DK[e] = 0.0; EK[e] = 0.0; }
+        __syncthreads();
+        if (tid < S) DK[tid * S + tid] = p.pad_var[k * S + tid] >= 0 ? p.sigma : 1.0;
+        __syncthreads();
+        // every target has one owner: its terms are summed in plan order
+#pragma unroll 1
+        for (int t = p.asm_blk_ptr[k] + tid; t < p.asm_blk_ptr[k + 1]; t += TT) {
+            double acc = 0.0;
+#pragma unroll 4
+            for (int j = 0; j < tmax; ++j) {
+                const int2 w = tt[(long)j * ntgt + t];
+                const int a = w.x & 0xFFFF, bb = (int)((unsigned)w.x >> 16), r = w.y;
+                acc += r < 0 ? L.Pv[a] : rho_of(L.ct[r], rho) * L.Acsc[a] * L.Acsc[bb];
+            }
+            const int tg = p.asm_tgt[t];
+            if (tg < SS) DK[tg] += acc;
+            else EK[tg - SS] += acc;
+        }
+        __syncthreads();
+        FPH(8)
+        if (k > 0) {
+            // F_k = E_k S_{k-1}^{-1} (rows < amax), then written over S_{k-1}^{-1}'s tile
+            constexpr int NF = SS / TT;  // per-thread F buffer (dynamically indexed)
+            double f[NF];
+            int nf = 0;
+#pragma unroll 1
+            for (int o = tid; o < amax * S; o += TT, ++nf) {
+                const int r = o >> 5, j = o & (S - 1);
+                double sacc = 0.0;
+#pragma unroll 8
+                for (int l = 0; l < S; ++l) sacc += EK[r * S + l] * SP[l * S + j];
+                f[nf & (NF - 1)] = sacc;
+                if (mode < 2) Fg[(long)k * SS + r * S + j] = sacc;
+                if (mode == 0) Hg[(long)(k - 1) * SS + j * S + r] = sacc;
+                if (mode == 2) Hg[(long)(k * (k - 1) / 2 + k - 1) * gstride + o] = -sacc;
+            }
+            __syncthreads();  // every read of S_{k-1}^{-1} done
+            nf = 0;
+#pragma unroll 1
+            for (int o = tid; o < amax * S; o += TT, ++nf) SP[o] = f[nf & (NF - 1)];
+            __syncthreads();
+            if (mode == 2) {  // G_kj = -F_k G_{k-1,j} (G_{k-1,j} has amax nonzero rows)
+#pragma unroll 1
+                for (int j = 0; j < k - 1; ++j) {
+                    const double* Gp = Hg + (long)((k - 1) * (k - 2) / 2 + j) * gstride;
+                    double* Gk = Hg + (long)(k * (k - 1) / 2 + j) * gstride;
+#pragma unroll 1
+                    for (int o = tid; o < amax * S; o += TT) {
+                        const int r = o >> 5, c = o & (S - 1);
+                        double sacc = 0.0;
+#pragma unroll 1
+                        for (int l = 0; l < amax; ++l) sacc += SP[r * S + l] * Gp[l * S + c];
+                        Gk[o] = -sacc;
+                    }
+                }
+            }
+            // S_k = D_k - F_k E_k' on the leading amax x amax corner
+#pragma unroll 1
+            for (int o = tid; o < amax * amax; o += TT) {
+                const int r = o / amax, c = o - r * amax;
+                double sacc = 0.0;
+#pragma unroll 8
+                for (int l = 0; l < S; ++l) sacc += SP[r * S + l] * EK[c * S + l];
+                DK[r * S + c] -= sacc;
+            }
+            __syncthreads();
+        }
+        FPH(9)
+        // Gauss-Jordan inverse with the tile in registers: thread (i0 + TT/8 * ii, jg)
+        // keeps elements [i][jg + 8c]; per pivot only its row and column go through
+        // LDS (double-buffered in EK, free by now), so each pivot costs one barrier.
+        double v[NI][4];
+#pragma unroll
+        for (int ii = 0; ii < NI; ++ii)
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) v[ii][cc] = DK[(i0 + TT / 8 * ii) * S + jg + 8 * cc];
+        double* rowbuf = EK;
+        double* colbuf = EK + 2 * S;
+#pragma unroll 1
+        for (int pv = 0; pv < S; ++pv) {
+            const int buf = (pv & 1) * S;
+            const int cp = pv >> 3;
+#pragma unroll
+            for (int ii = 0; ii < NI; ++ii) {
+                const int i = i0 + TT / 8 * ii;
+                if (i == pv) {
+#pragma unroll
+                    for (int cc = 0; cc < 4; ++cc) rowbuf[buf + jg + 8 * cc] = v[ii][cc];
+                }
+                if (jg == (pv & 7))
+                    colbuf[buf + i] = cp == 0 ? v[ii][0] : cp == 1 ? v[ii][1] : cp == 2 ? v[ii][2] : v[ii][3];
+            }
+            __syncthreads();
+            const double piv = rowbuf[buf + pv];
+            if (!(piv > 0.0)) ok = false;
+            const double d = 1.0 / piv;
+            double rowv[4];
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) rowv[cc] = rowbuf[buf + jg + 8 * cc];
+#pragma unroll
+            for (int ii = 0; ii < NI; ++ii) {
+                const int i = i0 + TT / 8 * ii;
+                const double colv = colbuf[buf + i];
+#pragma unroll
+                for (int cc = 0; cc < 4; ++cc) {
+                    const int j = jg + 8 * cc;
+                    if (i == pv) v[ii][cc] = (j == pv) ? d : rowv[cc] * d;
+                    else if (j == pv) v[ii][cc] = -colv * d;
+                    else v[ii][cc] = v[ii][cc] - colv * (rowv[cc] * d);
+                }
+            }
+        }
+#pragma unroll
+        for (int ii = 0; ii < NI; ++ii)
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) DK[(i0 + TT / 8 * ii) * S + jg + 8 * cc] = v[ii][cc];
+        FPH(10)
+#pragma unroll
+        for (int ii = 0; ii < NI; ++ii)
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc)
+                Sg[(long)k * SS + (i0 + TT / 8 * ii) * S + jg + 8 * cc] = v[ii][cc];
+        double* t = SP; SP = DK; DK = t;  // S_k^{-1} becomes "previous"
+        __syncthreads();
+        FPH(11)
+    }
+#undef FPH
+    return ok;
+}
+
+// Gather list of one column (A' w) or row (A x) of A: K packed entries
+// (value position in the padded-CSC copy of A in LDS | vector index << 16), padded
+// with the zero slot Acsc[nnzA] -- no per-entry branches, all 2K LDS reads in flight.
+template <int K>
+struct Gather {
+    unsigned e[K];
+    __device__ __forceinline__ void load(const int* list) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) e[k] = (unsigned)list[k];
+    }
+    __device__ __forceinline__ void clear(int zero_pos) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) e[k] = (unsigned)zero_pos;
+    }
+    // an opaque zero offset keeps the LDS addresses from being hoisted into
+    // registers across the ADMM loop
+    __device__ __forceinline__ double dot(const double* A, const double* vec) const {
+        int opq = 0;
+        asm volatile("" : "+s"(opq));
+        double t[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const unsigned ek = e[k] + (unsigned)opq;  // unpacked inside the loop: the packed
+            t[k] = A[ek & 0xFFFFu] * vec[ek >> 16];    // word is the only register it costs
+        }
+#pragma unroll
+        for (int w = 1; w < K; w *= 2)
+#pragma unroll
+            for (int k = 0; k + w < K; k += 2 * w) t[k] += t[k + w];
+        return t[0];
+    }
+};
+
+struct Res {  // update_info results
+    double pri, dua, nz, nax, nq, naty, npx;    // termination (unscaled)
+    double rpri, rdua, rz, rax, rq, raty, rpx;  // rho estimate (scaled space)
+    __device__ __forceinline__ void save(double* d) const {
+        d[0] = pri; d[1] = dua; d[2] = nz; d[3] = nax; d[4] = nq; d[5] = naty; d[6] = npx;
+        d[7] = rpri; d[8] = rdua; d[9] = rz; d[10] = rax; d[11] = rq; d[12] = raty; d[13] = rpx;
+    }
+    __device__ __forceinline__ void restore(const double* d) {
+        pri = d[0]; dua = d[1]; nz = d[2]; nax = d[3]; nq = d[4]; naty = d[5]; npx = d[6];
+        rpri = d[7]; rdua = d[8]; rz = d[9]; rax = d[10]; rq = d[11]; raty = d[12]; rpx = d[13];
+    }
+};
+
+// LDS carve of the solve kernel (doubles unless noted):
+//   Acsc[nnzA+1] Pv[nnzP+1] lo[mp] up[mp] qv[npad] X[npad] Z[mp]   (mp = m rounded up to 64)
+//   V = max(3 S*S, w[mp] rb[npad] xt[npad] ys[mp] dY[mp] gl[...])   (factor scratch aliases the vectors;
+//       ys is saved to the workspace around a refactorisation)
+//   red[128] res[16] pacc[16] cor[nb*S] tv[npad] ct[mp bytes] flag
+// rb holds delta_x and dY delta_y of the last iteration after its update phase;
+// ys holds y whenever the out-of-line phases run.
+// V holds the per-iteration vectors, then (mode 2) an LDS copy of the G blocks for
+// the wave kernel; the factorisation's three scratch tiles alias all of it.
+__host__ __device__ inline long solve_glen(int nb, int amax, int mode) {
+    return mode == 2 ? ((long)nb * (nb - 1) / 2 + 1) * (amax > 8 ? amax : 8) * S : 0;  // rows padded to >= 8, + a zero pair
+}
+// row arrays are padded to whole waves (the wave kernel's rows i = lane + 64 s are
+// then all in range; padded rows are inert: l = u = 0, empty gather list)
+__host__ __device__ inline int solve_mpad(int m) { return (m + 63) & ~63; }
+__host__ __device__ inline long solve_vlen(int m, int npad, int nb, int amax, int mode) {
+    const long a = 3L * solve_mpad(m) + 2L * npad + solve_glen(nb, amax, mode), b = 3L * SS;
+    return a > b ? a : b;
+}
+
+struct SL2 {  // full carve (SLds + the solve-kernel-only arrays)
+    SLds L;
+    double *X, *Z, *dY;
+};
+
+// every array starts on a 16-byte boundary (the wave kernels' broadcast reads are
+// ds_read_b128); A16 tells the compiler so
+__host__ __device__ inline long al2(long x) { return (x + 1) & ~1L; }
+#define A16(ptr) ((double*)__builtin_assume_aligned((ptr), 16))
+
+template <class KP>
+__device__ __forceinline__ SL2 carve(const KP& p) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    SL2 c;
+    const int mp = solve_mpad(p.m), npad = p.npad;
+    c.L.Acsc = A16(sm);
+    c.L.Pv = A16(c.L.Acsc + al2(p.nnzA + 1));  // Acsc[nnzA] = 0: gather padding
+    c.L.lo = A16(c.L.Pv + al2(p.nnzP + 1));    // Pv[nnzP] = 0: P-list padding
+    c.L.up = A16(c.L.lo + mp);
+    c.L.qv = A16(c.L.up + mp);
+    c.X = A16(c.L.qv + npad);
+    c.Z = A16(c.X + npad);
+    double* V = A16(c.Z + mp);
+    c.L.w = V;
+    c.L.rb = A16(c.L.w + mp);
+    c.L.xt = A16(c.L.rb + npad);
+    c.L.ys = A16(c.L.xt + npad);
+    c.dY = A16(c.L.ys + mp);
+    c.L.SP = V;
+    c.L.EK = A16(c.L.SP + SS);
+    c.L.DK = A16(c.L.EK + SS);
+    c.L.gl = A16(c.dY + mp);
+    c.L.red = A16(V + solve_vlen(p.m, npad, p.nb, p.amax, p.mode));
+    c.L.res = A16(c.L.red + 128);
+    c.L.pacc = (long long*)(c.L.res + 16);
+    c.L.cor = A16((double*)(c.L.pacc + 16));
+    c.L.dx = p.mode == 2 ? c.L.xt : c.L.rb;
+    c.L.tv = A16(c.L.cor + p.nb * S);
+    c.L.ct = (signed char*)(c.L.tv + npad);
+    c.L.flag = (int*)(c.L.ct + mp);
+    return c;
+}
+
+// LDS scalar slots (in res[14..15] and flag[1..]): shared outcome of the out-of-line phases
+struct Shared {
+    double* res;  // [0..13] Res, [14] obj, [15] new rho
+    int* flag;    // [0] scratch, [1] status, [2] dx_scaled, [3] dy_scaled
+};
+
+// ---- out-of-line phases: everything they need is in LDS or in the plan ----
+// dot of a packed gather list (value index | vector index << 16) with cnt entries
+__device__ __forceinline__ double list_dot(const int* __restrict__ list, int cnt, const double* V, const double* v) {
+    double acc = 0.0;
+#pragma unroll 4
+    for (int k = 0; k < cnt; ++k) {
+        const unsigned e = (unsigned)list[k];
+        acc += V[e & 0xFFFFu] * v[e >> 16];
+    }
+    return acc;
+}
+template <class KP>
+__device__ __forceinline__ double row_dot(const KP& p, const double* A, const double* v, int i) {
+    return list_dot(p.grow + (long)i * kGS, p.gk, A, v);
+}
+template <class KP>
+__device__ __forceinline__ double col_dot(const KP& p, const double* A, const double* v, int pc) {
+    return list_dot(p.gcol + (long)pc * kGS, p.gk, A, v);
+}
+template <class KP>
+__device__ __forceinline__ double psym_dot(const KP& p, const double* Pv, const double* v, int pc) {
+    return list_dot(p.gpsym + (long)pc * kGS, p.pk, Pv, v);
+}
+
+// update_info: residuals and the norms of their tolerances (OSQP compute_pri_res /
+// compute_dua_res / compute_pri_tol / compute_dua_tol, scaled and unscaled)
+template <int TT>
+__device__ __noinline__ void update_info_nl(const KParams* gp, long b, double cinv) {
+    KPc& p = kconst(gp);
+    SL2 c = carve(p);
+    const int tid = threadIdx.x, m = p.m, npad = p.npad;
+    const double* Eg = p.E + b * m;
+    const double* Dg = p.D + b * npad;
+    double v[14];
+#pragma unroll
+    for (int k = 0; k < 14; ++k) v[k] = 0.0;
+    #pragma unroll 1
+    for (int i = tid; i < m; i += TT) {
+        const double ax = row_dot(p, c.L.Acsc, c.X, i);
+        const double zi = c.Z[i];
+        const double pr = ax - zi;
+        const double ei = 1.0 / Eg[i];
+        v[0] = cmax(v[0], fabs(ei * pr));
+        v[2] = cmax(v[2], fabs(ei * zi));
+        v[3] = cmax(v[3], fabs(ei * ax));
+        v[7] = cmax(v[7], fabs(pr));
+        v[9] = cmax(v[9], fabs(zi));
+        v[10] = cmax(v[10], fabs(ax));
+    }
+    #pragma unroll 1
+    for (int pc = tid; pc < npad; pc += TT) {
+        if (p.pad_var[pc] < 0) continue;
+        const double px = psym_dot(p, c.L.Pv, c.X, pc);
+        const double aty = col_dot(p, c.L.Acsc, c.L.ys, pc);
+        const double q = c.L.qv[pc];
+        const double d = (q + px) + aty;
+        const double di = 1.0 / Dg[pc];
+        v[1] = cmax(v[1], fabs(di * d));
+        v[4] = cmax(v[4], fabs(di * q));
+        v[5] = cmax(v[5], fabs(di * aty));
+        v[6] = cmax(v[6], fabs(di * px));
+        v[8] = cmax(v[8], fabs(d));
+        v[11] = cmax(v[11], fabs(q));
+        v[12] = cmax(v[12], fabs(aty));
+        v[13] = cmax(v[13], fabs(px));
+    }
+    double* r = c.L.red + 64;
+    block_max_to<TT>(v, c.L.red, r);
+    if (tid == 0) {
+        Res R;
+        if (p.scaling && !p.scaled_term) {
+            R.pri = r[0]; R.dua = cinv * r[1];
+            R.nz = r[2]; R.nax = r[3]; R.nq = r[4]; R.naty = r[5]; R.npx = r[6];
+        } else {
+            R.pri = r[7]; R.dua = r[8];
+            R.nz = r[9]; R.nax = r[10]; R.nq = r[11]; R.naty = r[12]; R.npx = r[13];
+        }
+        R.rpri = r[7]; R.rdua = r[8]; R.rz = r[9]; R.rax = r[10]; R.rq = r[11]; R.raty = r[12]; R.rpx = r[13];
+        if (m == 0) R.pri = 0.0;
+        R.save(c.L.res);
+    }
+    __syncthreads();
+}
+
+// is_primal_infeasible (delta_y in dY, projected in place as OSQP does)
+template <int TT, class KP>
+__device__ bool primal_infeasible(const KP& p, SL2& c, long b, double eps) {
+    const int tid = threadIdx.x, m = p.m, npad = p.npad;
+    const bool unscale = p.scaling && !p.scaled_term;
+    const double* Eg = p.E + b * m;
+    const double* Dg = p.D + b * npad;
+    double nd[1] = {0.0};
+    #pragma unroll 1
+    for (int i = tid; i < m; i += TT) {
+        double d = c.dY[i];
+        if (c.L.up[i] > OSQP_INFTY * MIN_SCALING) d = (c.L.lo[i] < -OSQP_INFTY * MIN_SCALING) ? 0.0 : cmin(d, 0.0);
+        else if (c.L.lo[i] < -OSQP_INFTY * MIN_SCALING) d = cmax(d, 0.0);
+        c.dY[i] = d;
+        nd[0] = cmax(nd[0], fabs(unscale ? Eg[i] * d : d));
+    }
+    block_max<TT>(nd, c.L.red);
+    const double norm_dy = nd[0];
+    if (!(norm_dy > eps)) return false;
+    double sum[1] = {0.0};
+    #pragma unroll 1
+    for (int i = tid; i < m; i += TT) sum[0] += c.L.up[i] * cmax(c.dY[i], 0.0) + c.L.lo[i] * cmin(c.dY[i], 0.0);
+    block_sum<TT>(sum, c.L.red);
+    if (!(sum[0] < eps * norm_dy)) return false;
+    double na[1] = {0.0};
+    #pragma unroll 1
+    for (int pc = tid; pc < npad; pc += TT) {
+        if (p.pad_var[pc] < 0) continue;
+        double a = col_dot(p, c.L.Acsc, c.dY, pc);
+        if (unscale) a *= 1.0 / Dg[pc];
+        na[0] = cmax(na[0], fabs(a));
+    }
+    block_max<TT>(na, c.L.red);
+    return na[0] < eps * norm_dy;
+}
+
+// is_dual_infeasible (delta_x in dx)
+template <int TT, class KP>
+__device__ bool dual_infeasible(const KP& p, SL2& c, long b, double cs_, double eps) {
+    const int tid = threadIdx.x, m = p.m, npad = p.npad;
+    const bool unscale = p.scaling && !p.scaled_term;
+    const double* Eg = p.E + b * m;
+    const double* Dg = p.D + b * npad;
+    const double cs = unscale ? cs_ : 1.0;
+    double v[1] = {0.0}, sum[1] = {0.0};
+    #pragma unroll 1
+    for (int pc = tid; pc < npad; pc += TT) {
+        if (p.pad_var[pc] < 0) continue;
+        const double dx = c.L.dx[pc];
+        v[0] = cmax(v[0], fabs(unscale ? Dg[pc] * dx : dx));
+        sum[0] += c.L.qv[pc] * dx;
+    }
+    block_max<TT>(v, c.L.red);
+    const double norm_dx = v[0];
+    if (!(norm_dx > eps)) return false;
+    block_sum<TT>(sum, c.L.red);
+    if (!(sum[0] < cs * eps * norm_dx)) return false;
+    double np[1] = {0.0};
+    #pragma unroll 1
+    for (int pc = tid; pc < npad; pc += TT) {
+        if (p.pad_var[pc] < 0) continue;
+        double a = psym_dot(p, c.L.Pv, c.L.dx, pc);
+        if (unscale) a *= 1.0 / Dg[pc];
+        np[0] = cmax(np[0], fabs(a));
+    }
+    block_max<TT>(np, c.L.red);
+    if (!(np[0] < cs * eps * norm_dx)) return false;
+    bool viol = false;
+    #pragma unroll 1
+    for (int i = tid; i < m; i += TT) {
+        double a = row_dot(p, c.L.Acsc, c.L.dx, i);
+        if (unscale) a *= 1.0 / Eg[i];
+        if ((c.L.up[i] < OSQP_INFTY * MIN_SCALING && a > eps * norm_dx) ||
+            (c.L.lo[i] > -OSQP_INFTY * MIN_SCALING && a < -eps * norm_dx))
+            viol = true;
+    }
+    return !block_any<TT>(viol, c.L.flag);
+}
+
+// check_termination on the Res in LDS; status / obj / certificate flags in LDS.
+template <int TT>
+__device__ __noinline__ int check_termination_nl(const KParams* gp, long b, double cval, double cinv,
+                                                 int approximate) {
+    KPc& p = kconst(gp);
+    SL2 c = carve(p);
+    Res R;
+    R.restore(c.L.res);
+    double eps_abs = p.eps_abs, eps_rel = p.eps_rel, eps_pinf = p.eps_pinf, eps_dinf = p.eps_dinf;
+    int st = MPCQP_UNSOLVED_;
+    double obj = c.L.res[14];
+    bool done = false;
+    if (R.pri > OSQP_INFTY || R.dua > OSQP_INFTY) {
+        st = MPCQP_NON_CVX_;
+        obj = __builtin_nan("");
+        done = true;
+    } else {
+        if (approximate) { eps_abs *= 10; eps_rel *= 10; eps_pinf *= 10; eps_dinf *= 10; }
+        bool prim_ok = false, dual_ok = false, prim_inf = false, dual_inf = false;
+        const bool unscale = p.scaling && !p.scaled_term;
+        if (p.m == 0) prim_ok = true;
+        else {
+            const double ep = eps_abs + eps_rel * cmax(R.nz, R.nax);
+            if (R.pri < ep) prim_ok = true;
+            else prim_inf = primal_infeasible<TT>(p, c, b, eps_pinf);
+        }
+        double mx = cmax(cmax(R.nq, R.naty), R.npx);
+        if (unscale) mx *= cinv;
+        if (R.dua < eps_abs + eps_rel * mx) dual_ok = true;
+        else dual_inf = dual_infeasible<TT>(p, c, b, cval, eps_dinf);
+        if (prim_ok && dual_ok) {
+            st = approximate ? MPCQP_SOLVED_INACCURATE_ : MPCQP_SOLVED_;
+            done = true;
+        } else if (prim_inf) {
+            st = approximate ? MPCQP_PRIMAL_INFEASIBLE_INACCURATE_ : MPCQP_PRIMAL_INFEASIBLE_;
+            obj = OSQP_INFTY;
+            if (threadIdx.x == 0) c.L.flag[3] = unscale;
+            done = true;
+        } else if (dual_inf) {
+            st = approximate ? MPCQP_DUAL_INFEASIBLE_INACCURATE_ : MPCQP_DUAL_INFEASIBLE_;
+            obj = -OSQP_INFTY;
+            if (threadIdx.x == 0) c.L.flag[2] = unscale;
+            done = true;
+        }
+    }
+    __syncthreads();
+    if (done && threadIdx.x == 0) { c.L.flag[1] = st; c.L.res[14] = obj; }
+    __syncthreads();
+    return done ? st : MPCQP_UNSOLVED_;
+}
+
+// compute_obj_val (needs X)
+template <int TT>
+__device__ __noinline__ void objective_nl(const KParams* gp, double cinv) {
+    KPc& p = kconst(gp);
+    SL2 c = carve(p);
+    const int tid = threadIdx.x;
+    double sacc[1] = {0.0};
+    #pragma unroll 1
+    for (int v = tid; v < p.nnzP; v += TT) {
+        const int r = p.p_r[v], cc = p.p_c[v];
+        sacc[0] += (r == cc) ? 0.5 * c.L.Pv[v] * c.X[r] * c.X[r] : c.L.Pv[v] * c.X[r] * c.X[cc];
+    }
+    #pragma unroll 1
+    for (int pc = tid; pc < p.npad; pc += TT) sacc[0] += c.L.qv[pc] * c.X[pc];
+    block_sum<TT>(sacc, c.L.red);
+    if (tid == 0) c.L.res[14] = p.scaling ? sacc[0] * cinv : sacc[0];
+    __syncthreads();
+}
+
+// store_solution + info (y is in ys)
+template <int TT>
+__device__ __noinline__ void finalize_nl(const KParams* gp, long b, double* __restrict__ xo,
+                                         double* __restrict__ yo, double cinv, double rho, int status,
+                                         int info_iter, int rho_updates) {
+    KPc& p = kconst(gp);
+    SL2 c = carve(p);
+    const int tid = threadIdx.x, n = p.n, m = p.m, npad = p.npad;
+    const double* Eg = p.E + b * m;
+    const double* Dg = p.D + b * npad;
+    Res R;
+    R.restore(c.L.res);
+    const double obj = c.L.res[14];
+    double rho_est;
+    {
+        const double pr = R.rpri / (cmax(R.rz, R.rax) + DIVISION_TOL);
+        const double du = R.rdua / (cmax(cmax(R.rq, R.raty), R.rpx) + DIVISION_TOL);
+        rho_est = cmin(cmax(rho * sqrt(pr / (du + DIVISION_TOL)), RHO_MIN), RHO_MAX);
+    }
+    const bool has_sol = !(status == MPCQP_PRIMAL_INFEASIBLE_ || status == MPCQP_PRIMAL_INFEASIBLE_INACCURATE_ ||
+                           status == MPCQP_DUAL_INFEASIBLE_ || status == MPCQP_DUAL_INFEASIBLE_INACCURATE_ ||
+                           status == MPCQP_NON_CVX_);
+    const bool pinf = status == MPCQP_PRIMAL_INFEASIBLE_ || status == MPCQP_PRIMAL_INFEASIBLE_INACCURATE_;
+    const bool dinf = status == MPCQP_DUAL_INFEASIBLE_ || status == MPCQP_DUAL_INFEASIBLE_INACCURATE_;
+    const bool dx_scaled = c.L.flag[2] != 0, dy_scaled = c.L.flag[3] != 0;
+    double nrm[2] = {0.0, 0.0};
+    #pragma unroll 1
+    for (int pc = tid; pc < npad; pc += TT) {
+        double dx = c.L.dx[pc];
+        if (dx_scaled) dx *= Dg[pc];
+        c.L.dx[pc] = dx;
+        nrm[1] = cmax(nrm[1], fabs(dx));
+    }
+    #pragma unroll 1
+    for (int i = tid; i < m; i += TT) {
+        double dy = c.dY[i];
+        if (dy_scaled) dy *= Eg[i];
+        c.dY[i] = dy;
+        nrm[0] = cmax(nrm[0], fabs(dy));
+    }
+    block_max<TT>(nrm, c.L.red);
+    #pragma unroll 1
+    for (int pc = tid; pc < npad; pc += TT) {
+        const int j = p.pad_var[pc];
+        const double xv = c.X[pc];
+        if (j >= 0) {
+            if (xo) xo[b * n + j] = has_sol ? (p.scaling ? Dg[pc] * xv : xv) : __builtin_nan("");
+            p.dxc[b * n + j] = dinf ? c.L.dx[pc] * (1.0 / nrm[1]) : c.L.dx[pc];
+        }
+        p.x[b * npad + pc] = has_sol ? xv : 0.0;
+    }
+    #pragma unroll 1
+    for (int i = tid; i < m; i += TT) {
+        const double yv = c.L.ys[i];
+        if (yo) yo[b * m + i] = has_sol ? (p.scaling ? (Eg[i] * yv) * cinv : yv) : __builtin_nan("");
+        p.dyc[b * m + i] = pinf ? c.dY[i] * (1.0 / nrm[0]) : c.dY[i];
+        p.y[b * m + i] = has_sol ? yv : 0.0;
+        p.z[b * m + i] = has_sol ? c.Z[i] : 0.0;
+    }
+    if (tid == 0) {
+        p.status[b] = status;
+        p.iter[b] = info_iter;
+        p.rho_upd[b] = rho_updates;
+        p.obj[b] = obj;
+        p.pri[b] = R.pri;
+        p.dua[b] = R.dua;
+        p.rho_est[b] = rho_est;
+        p.scal[b * 4 + 2] = rho;
+    }
+}
+
+template <int TT>
+__device__ __noinline__ bool factorize_nl(const KParams* gp, long b, double rho) {
+    KPc& p = kconst(gp);
+    SL2 c = carve(p);
+    return factorize<TT>(p, c.L, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
+                     p.Si + b * (long)p.nb * SS);
+}
+
+
+size_t lds_solve_bytes(const KParams& p);
+
+}  // namespace mpcqp

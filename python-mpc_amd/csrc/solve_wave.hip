@@ -1,0 +1,830 @@
+// solve_wave.hip -- the ADMM kernel with ONE 64-lane wavefront per QP instance.
+//
+// Why a wave and not a workgroup: one ADMM iteration of a cfg-2 QP (SURVEY.md §8,
+// n = 104, m = 188) is ~7 kFLOP of dependent phases (rhs gather, block solve, row
+// update).  Spread over a 256-thread workgroup (solve.hip) every phase boundary
+// is an s_barrier between four waves and the iteration costs ~7,000 cycles, almost
+// all of it barrier and LDS round trips.  Inside a single wave the phases are
+// ordered by the wave's own instruction stream: the compiler drops s_barrier for a
+// 64-thread workgroup (it emits only the LDS waitcnt), so a phase boundary costs one
+// LDS round trip, and each wave is an independent QP that the four SIMDs of a CU
+// run side by side.
+//
+// Work decomposition (NB <= 4 blocks of S = 32 variables, amax <= 8 coupling rows):
+//   lane = (h, r) = (lane / 32, lane % 32) owns the padded columns
+//     pc_e = kb_e * 32 + r,  kb_0 = h, kb_1 = 3 - h   (blocks {0,3} / {1,2}: balanced
+//     phase-C work), with x, x_prev, q and its column gather lists in registers;
+//   constraint rows i = lane + 64 s (s < RS) with y, z, their row gather lists;
+//   the factor, in the three-phase form K^{-1} = L^{-T} D^{-1} L^{-1}
+//   (solve_phases.h::factorize, mode 2):
+//     SB[e][c] = S_{kb_e}^{-1}[r][c]                        (phase B, 64 doubles)
+//     GA[q][e] = G_q[lane / 8][4 (lane % 8) + e]            (phase A, pair q = k(k-1)/2 + j)
+//     GC[s][q] = G_{j_s, kb_s}[q][r]                        (phase C, transposed use)
+// One iteration:
+//   rhs   b = sigma x - q + A'(rho z - y)                   -> rb   (LDS)
+//   A     c_k = sum_{j<k} G_kj b_j   (8-lane DPP sums)      -> cor  (LDS)
+//   B     t_k = S_k^{-1} (b_k + c_k)                        -> tv   (LDS)
+//   C     x~_k = t_k + sum_{j>k} G_jk' t_j                  -> xt   (LDS)
+//   rows  z~ = A x~, relaxation, projection, y update, w = rho z - y -> w (LDS)
+// Reference semantics as solve.hip (OSQP 0.6 osqp_solve, behind
+// vehicle_lateral_mpc_slack_increment.py:248 / Control/MPC/mpc_dynamics.py:396).
+#include <hip/hip_runtime.h>
+
+#include "solve_phases.h"
+
+namespace mpcqp {
+
+constexpr int TW = 64;
+
+// S^{-1} rows of the lane's two blocks, SB[e][c] = S_{kb_e}^{-1}[r][c] (128 VGPRs)
+struct WaveFactor {
+    double SB[2][S];
+    __device__ __forceinline__ void load(const double* __restrict__ Sg) {
+        const int lane = threadIdx.x, h = lane >> 5, r = lane & 31;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const double* src = Sg + (long)(e ? 3 - h : h) * SS + r * S;
+#pragma unroll
+            for (int c = 0; c < S; ++c) SB[e][c] = src[c];
+        }
+    }
+};
+
+// Gather list with absolute LDS byte addresses: (vector address << 16) | (A value
+// address); one v_and / v_lshrrev per operand (the wave kernel's LDS is < 64 KiB).
+// Built at run start from the plan's (vector index << 16) | (A position) lists.
+template <int K>
+struct GatherW {
+    unsigned e[K];
+    __device__ __forceinline__ void load(const int* list, unsigned abase, unsigned vbase) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const unsigned raw = (unsigned)list[k];
+            e[k] = (((raw >> 16) * 8u + vbase) << 16) | ((raw & 0xFFFFu) * 8u + abase);
+        }
+    }
+    __device__ __forceinline__ void clear(unsigned zero_addr, unsigned vbase) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) e[k] = (vbase << 16) | zero_addr;
+    }
+};
+// 16-byte LDS reads (ds_read_b128) of two consecutive doubles at a 16-byte aligned address
+__device__ __forceinline__ void ld2(const double* p, double& a, double& b) {
+    const double2 v = *(const double2*)p;
+    a = v.x;
+    b = v.y;
+}
+typedef __attribute__((address_space(3))) const double lds_cdouble;
+typedef __attribute__((address_space(3))) const char lds_cchar;
+__device__ __forceinline__ double lds_at(unsigned byte_addr) { return *(lds_cdouble*)(unsigned long)byte_addr; }
+struct alignas(16) dpair { double x, y; };
+__device__ __forceinline__ void lds_at2(unsigned byte_addr, double& a, double& b) {
+    __attribute__((address_space(3))) const dpair* v = (__attribute__((address_space(3))) const dpair*)(unsigned long)byte_addr;
+    a = v->x;
+    b = v->y;
+}
+__device__ __forceinline__ unsigned lds_addr(const void* p) {  // LDS byte address of a shared pointer
+    return (unsigned)(unsigned long)(lds_cchar*)p;
+}
+
+template <int K, int RS>
+__global__ __launch_bounds__(TW, 1) void k_solve_w(KParams p, double* __restrict__ xo, double* __restrict__ yo,
+                                                   int factor_only) {
+    const int lane = threadIdx.x;
+    const int h = lane >> 5, r = lane & 31, rr = lane >> 3, ch = lane & 7;
+    const int kb0 = h, kb1 = 3 - h;
+    constexpr int NB = 4, NP = NB * (NB - 1) / 2;  // exactly four blocks (solve.hip::variant_fits)
+    const long b = blockIdx.x;
+    const int n = p.n, m = p.m, npad = p.npad, nnzP = p.nnzP, nnzA = p.nnzA;
+    SL2 C = carve(p);
+    SLds& L = C.L;
+    const double* Hg = p.H + b * (long)p.nb * SS;
+    const double* Sg = p.Si + b * (long)p.nb * SS;
+
+    if (p.err[b]) {  // invalid data (flagged by setup/update): NaN outputs
+        for (int j = lane; j < n; j += TW) if (xo) xo[b * n + j] = __builtin_nan("");
+        for (int i = lane; i < m; i += TW) if (yo) yo[b * m + i] = __builtin_nan("");
+        if (lane == 0) p.status[b] = MPCQP_NON_CVX_;
+        return;
+    }
+
+#ifdef MPCQP_PHASE_PROF
+    long long tph = 0, t0c = 0, t0w = 0;
+    const bool prof = p.prof != nullptr;
+    if (prof) { t0w = wall_clock64(); t0c = tph = clock64(); if (lane < 16) L.pacc[lane] = 0; }
+#define PH(k) if (prof && lane == 0) { const long long t_ = clock64(); L.pacc[k] += t_ - tph; tph = t_; }
+#else
+#define PH(k)
+#endif
+
+    const double cval = p.scal[b * 4 + 0], cinv = p.scal[b * 4 + 1];
+    double rho = p.scal[b * 4 + 2];
+    const double sigma = p.sigma, alpha = p.alpha;
+    const bool warm = p.warm_start != 0;
+    for (int e = lane; e < nnzA; e += TW) L.Acsc[e] = p.Ax[b * nnzA + p.acsc_v[e]];
+    if (lane == 0) L.Acsc[nnzA] = 0.0;  // the gather lists' padding slot
+    for (int v = lane; v < nnzP; v += TW) L.Pv[v] = p.Px[b * nnzP + v];
+    if (lane == 0) L.Pv[nnzP] = 0.0;
+    const int mp = solve_mpad(m);
+    for (int i = lane; i < mp; i += TW) {  // rows >= m: inert padding (l = u = 0, z = 0)
+        const bool in = i < m;
+        L.lo[i] = in ? p.l[b * m + i] : 0.0;
+        L.up[i] = in ? p.u[b * m + i] : 0.0;
+        L.ct[i] = in ? p.ct[b * m + i] : 0;
+        C.Z[i] = (in && warm) ? p.z[b * m + i] : 0.0;
+    }
+    for (int pc = lane; pc < npad; pc += TW) {
+        L.qv[pc] = p.q[b * npad + pc];
+        C.X[pc] = warm ? p.x[b * npad + pc] : 0.0;
+    }
+    if (lane < S) L.cor[lane] = 0.0;  // block 0 has no phase-A correction
+    if (lane < 16) L.res[lane] = 0.0;
+    if (lane < 4) L.flag[lane] = 0;
+
+    int status = MPCQP_UNSOLVED_, rho_updates = 0, iter = 0, info_iter = 0;
+    bool can_check = false, need_factor = true;
+    PH(5)
+    // Runs of ADMM iterations up to the next termination / rho-adaptation point
+    // alternate with the out-of-line phases; the run state lives in registers and
+    // is re-derived from LDS and the workspace at every run start (nothing but
+    // scalars is live across a call).
+    for (;;) {
+        __syncthreads();
+        if (need_factor) {  // start, and after a rho change
+            need_factor = false;
+            // the factorisation scratch aliases ys (and dY, rb, xt, w): y waits in the
+            // workspace's y array (the warm-start input at the first factorisation)
+            if (iter > 0)
+                for (int i = lane; i < m; i += TW) p.y[b * m + i] = L.ys[i];
+            const bool ok = factorize_nl<TW>(p.self, b, rho);
+            if (!ok) {
+                if (iter == 0) {
+                    for (int j = lane; j < n; j += TW) if (xo) xo[b * n + j] = __builtin_nan("");
+                    for (int i = lane; i < m; i += TW) if (yo) yo[b * m + i] = __builtin_nan("");
+                    if (lane == 0) p.status[b] = MPCQP_NON_CVX_;
+                    return;
+                }
+                status = MPCQP_NON_CVX_;
+                can_check = true;  // skip the final check_termination
+                break;
+            }
+            if (factor_only) return;
+            __syncthreads();
+            const bool have_y = iter > 0 || warm;
+            for (int i = lane; i < mp; i += TW) L.ys[i] = (have_y && i < m) ? p.y[b * m + i] : 0.0;
+            // G blocks -> LDS, rows padded to 8 with zeros: gl[pair][row < 8][32]
+            for (int o = lane; o < NP * 8 * S; o += TW) {
+                const int q = o >> 8, t = (o >> 5) & 7;
+                L.gl[o] = t < p.amax ? Hg[(long)q * p.amax * S + (o & 255)] : 0.0;
+            }
+            PH(0)
+        }
+        // ---- run state ----
+        WaveFactor RF;
+        RF.load(Sg);
+        int pcs[2];
+        bool cv[2];
+        double X[2], Q[2], DX[2];
+        // LDS byte addresses of the gathered arrays
+        const unsigned abase = lds_addr(L.Acsc), wbase = lds_addr(L.w), xbase = lds_addr(L.xt);
+        GatherW<K> cg[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int pc = (e ? kb1 : kb0) * S + r;  // < npad = 4 S
+            pcs[e] = pc;
+            cv[e] = p.pad_var[pc] >= 0;
+            X[e] = C.X[pc];
+            Q[e] = L.qv[pc];
+            DX[e] = 0.0;
+            cg[e].load(p.gcol + (long)pc * kGS, abase, wbase);
+        }
+        GatherW<K> rg[RS];
+        double y[RS], Z[RS], dy[RS], rv[RS], rvi[RS];
+        const double r_hi = RHO_EQ_OVER_RHO_INEQ * rho;
+#pragma unroll
+        for (int s = 0; s < RS; ++s) {
+            const int i = lane + s * TW;  // < mp
+            dy[s] = 0.0;
+            if (i < m) rg[s].load(p.grow + (long)i * kGS, abase, xbase);
+            else rg[s].clear(abase + 8u * nnzA, xbase);
+            y[s] = L.ys[i];
+            Z[s] = C.Z[i];
+            const signed char cl = L.ct[i];  // OSQP rho_vec / rho_inv_vec of the row
+            rv[s] = cl < 0 ? RHO_MIN : (cl > 0 ? r_hi : rho);
+            rvi[s] = cl < 0 ? 1.0 / RHO_MIN : (cl > 0 ? 1.0 / r_hi : 1.0 / rho);
+            L.w[i] = rv[s] * Z[s] - y[s];  // w = rho z_prev - y (rho may be new)
+        }
+        int stop_at = p.max_iter;
+        if (p.check_term) stop_at = min(stop_at, (iter / p.check_term + 1) * p.check_term);
+        if (p.adaptive_rho && p.rho_interval) stop_at = min(stop_at, (iter / p.rho_interval + 1) * p.rho_interval);
+        __syncthreads();
+        PH(5)
+        while (iter < stop_at) {
+            ++iter;
+            int opq = 0;
+            asm volatile("" : "+s"(opq));  // keeps per-lane LDS addresses out of the register budget
+            double* const rb = L.rb + opq;
+            double* const cor = L.cor + opq;
+            double* const tv = L.tv + opq;
+            double* const xt = L.xt + opq;
+            // rhs = sigma x_prev - q + A' (rho z_prev - y)
+            {
+                double av[2][K], wv[2][K];
+#pragma unroll
+                for (int e = 0; e < 2; ++e)
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        av[e][k] = lds_at(cg[e].e[k] & 0xFFFFu);
+                        wv[e][k] = lds_at(cg[e].e[k] >> 16);
+                    }
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    double v = sigma * X[e] - Q[e];
+#pragma unroll
+                    for (int k = 0; k < K; ++k) v += av[e][k] * wv[e][k];
+                    rb[pcs[e]] = cv[e] ? v : 0.0;
+                }
+            }
+            __syncthreads();
+            PH(1)
+            // A: c_k = sum_{j<k} G_kj b_j on rows < 8: lane (rr, ch) takes columns
+            // [4 ch, 4 ch + 4) of every pair, 8-lane DPP sums over ch (every lane of
+            // the group holds the sum and writes it)
+            {
+                const double* gq = L.gl + opq + rr * S + 4 * ch;
+                double bj[NB - 1][4], ga[NP][4];
+#pragma unroll
+                for (int j = 0; j < NB - 1; ++j)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) bj[j][e] = rb[j * S + 4 * ch + e];
+#pragma unroll
+                for (int q = 0; q < NP; ++q)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) ga[q][e] = gq[q * 8 * S + e];
+#pragma unroll
+                for (int k = 1; k < NB; ++k) {
+                    double acc = 0.0;
+#pragma unroll
+                    for (int j = 0; j < k; ++j)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) acc += ga[k * (k - 1) / 2 + j][e] * bj[j][e];
+                    cor[k * S + rr] = reduce8(acc);
+                }
+            }
+            __syncthreads();
+            // B: t_kb = S_kb^{-1} (b_kb + c_kb), one full row per lane and block
+            double t[2];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int kb = e ? kb1 : kb0;
+                const double* bv = rb + kb * S;
+                const double* cb = cor + kb * S;
+                double v[S], cc[8];
+#pragma unroll
+                for (int c = 0; c < S; ++c) v[c] = bv[c];
+#pragma unroll
+                for (int c = 0; c < 8; ++c) cc[c] = cb[c];
+#pragma unroll
+                for (int c = 0; c < 8; ++c) v[c] += cc[c];
+                double a[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int c = 0; c < S; ++c) a[c & 3] += RF.SB[e][c] * v[c];
+                t[e] = (a[0] + a[1]) + (a[2] + a[3]);
+            }
+            tv[kb0 * S + r] = t[0];
+            tv[kb1 * S + r] = t[1];
+            __syncthreads();
+            // C: x~_kb = t_kb + sum_{j>kb} G_{j,kb}' t_j  (t_j rows < 8); the lane's
+            // pairs: h = 0: (1,0) (2,0) (3,0);  h = 1: (2,1) (3,1) (3,2)
+            double xn[2];
+            {
+                double d[3], gv[3][8], tq[3][8];
+#pragma unroll
+                for (int s = 0; s < 3; ++s) {
+                    const int j = s < 2 ? s + 1 + h : 3;
+                    const int kb = s < 2 ? h : 2 * h;
+                    const double* tj = tv + j * S;
+                    const double* gc = L.gl + opq + (j * (j - 1) / 2 + kb) * 8 * S + r;
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) { gv[s][q] = gc[q * S]; tq[s][q] = tj[q]; }
+                }
+#pragma unroll
+                for (int s = 0; s < 3; ++s) {
+                    double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+                    for (int q = 0; q < 8; q += 2) {
+                        a0 += gv[s][q] * tq[s][q];
+                        a1 += gv[s][q + 1] * tq[s][q + 1];
+                    }
+                    d[s] = a0 + a1;
+                }
+                xn[0] = t[0] + (d[0] + d[1]) + (h ? 0.0 : d[2]);
+                xn[1] = t[1] + (h ? d[2] : 0.0);
+            }
+            xt[kb0 * S + r] = xn[0];
+            xt[kb1 * S + r] = xn[1];
+            // x update (own columns, registers)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const double xnew = alpha * xn[e] + (1.0 - alpha) * X[e];
+                DX[e] = xnew - X[e];
+                X[e] = xnew;
+            }
+            __syncthreads();
+            PH(2)
+            // z~ = A x~ ; relaxed + projected z ; y ; next w   (padded rows stay 0)
+            double zts[RS];
+            {
+                double av[RS][K], xv[RS][K];
+#pragma unroll
+                for (int s = 0; s < RS; ++s)
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        av[s][k] = lds_at(rg[s].e[k] & 0xFFFFu);
+                        xv[s][k] = lds_at(rg[s].e[k] >> 16);
+                    }
+#pragma unroll
+                for (int s = 0; s < RS; ++s) {
+                    double v = av[s][0] * xv[s][0];
+#pragma unroll
+                    for (int k = 1; k < K; ++k) v += av[s][k] * xv[s][k];
+                    zts[s] = v;
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < RS; ++s) {
+                const int i = lane + opq + s * TW;
+                const double zt = zts[s];
+                const double zr = alpha * zt + (1.0 - alpha) * Z[s];
+                const double zn = __builtin_fmin(__builtin_fmax(zr + rvi[s] * y[s], L.lo[i]), L.up[i]);
+                const double dd = rv[s] * (zr - zn);
+                Z[s] = zn;
+                dy[s] = dd;
+                y[s] += dd;
+                L.w[i] = rv[s] * zn - y[s];
+            }
+            __syncthreads();
+            PH(3)
+        }
+        // run state back to LDS for the out-of-line phases
+#pragma unroll
+        for (int e = 0; e < 2; ++e) { C.X[pcs[e]] = X[e]; L.dx[pcs[e]] = DX[e]; }
+#pragma unroll
+        for (int s = 0; s < RS; ++s) {
+            const int i = lane + s * TW;
+            L.ys[i] = y[s]; C.Z[i] = Z[s]; C.dY[i] = dy[s];
+        }
+        __syncthreads();
+        // ---- out-of-line phases (only scalars live across these calls) ----
+        can_check = p.check_term && (iter % p.check_term == 0);
+        const bool do_rho = p.adaptive_rho && p.rho_interval && (iter % p.rho_interval == 0);
+        if (!can_check && !do_rho) break;  // max_iter reached
+        update_info_nl<TW>(p.self, b, cinv);
+        info_iter = iter;
+        bool stop = false;
+        if (can_check) {
+            status = check_termination_nl<TW>(p.self, b, cval, cinv, 0);
+            stop = status != MPCQP_UNSOLVED_;
+        }
+        if (!stop && do_rho) {
+            Res R;
+            R.restore(L.res);
+            const double pr = R.rpri / (cmax(R.rz, R.rax) + DIVISION_TOL);
+            const double du = R.rdua / (cmax(cmax(R.rq, R.raty), R.rpx) + DIVISION_TOL);
+            double rn = rho * sqrt(pr / (du + DIVISION_TOL));
+            rn = cmin(cmax(rn, RHO_MIN), RHO_MAX);
+            if (rn > rho * p.rho_tol || rn < rho / p.rho_tol) {
+                rho = cmin(cmax(rn, RHO_MIN), RHO_MAX);
+                rho_updates++;
+                need_factor = true;
+            }
+        }
+        __syncthreads();
+        PH(4)
+        if (stop || iter >= p.max_iter) break;
+    }
+    if (!can_check && status == MPCQP_UNSOLVED_) {
+        update_info_nl<TW>(p.self, b, cinv);
+        info_iter = iter;
+        status = check_termination_nl<TW>(p.self, b, cval, cinv, 0);
+    }
+    const bool has_sol = !(status == MPCQP_PRIMAL_INFEASIBLE_ || status == MPCQP_PRIMAL_INFEASIBLE_INACCURATE_ ||
+                           status == MPCQP_DUAL_INFEASIBLE_ || status == MPCQP_DUAL_INFEASIBLE_INACCURATE_ ||
+                           status == MPCQP_NON_CVX_);
+    if (has_sol) objective_nl<TW>(p.self, cinv);
+    if (status == MPCQP_UNSOLVED_) {
+        status = check_termination_nl<TW>(p.self, b, cval, cinv, 1);
+        if (status == MPCQP_UNSOLVED_) status = MPCQP_MAX_ITER_REACHED_;
+    }
+    finalize_nl<TW>(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates);
+#ifdef MPCQP_PHASE_PROF
+    if (prof) {
+        __syncthreads();
+        PH(5)
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) p.prof[b * kProfSlots + k] = L.pacc[k];
+#pragma unroll
+            for (int k = 8; k < 12; ++k) p.prof[b * kProfSlots + k] = L.pacc[k];
+            p.prof[b * kProfSlots + 6] = clock64() - t0c;
+            p.prof[b * kProfSlots + 7] = wall_clock64() - t0w;
+        }
+    }
+#endif
+#undef PH
+}
+
+// ---------------------------------------------------------------------------
+// Two-wave variant: one 128-thread workgroup (2 waves, on 2 SIMDs) per QP.
+// Wave w owns blocks {0, 3} (w = 0) or {1, 2} (w = 1), one block row per lane
+// (lane = (h, r): block kb = w ? 1 + h : 3 h, row r), so each wave issues half the
+// work of the one-wave kernel with half its registers.  The waves meet at three
+// workgroup barriers per iteration (after rhs, after x~, after the row update);
+// the cross-block terms of the solve that a wave needs from the other wave's
+// blocks (c_k of phase A, and the rows < 8 of t_j that phase C reads) are
+// recomputed inside the wave instead of exchanged: phase A is done by both
+// waves, and wave 0 recomputes t_1, t_2 (rows < 8), wave 1 recomputes t_3.
+// Per-wave LDS for those: cw[w][block][8] (in cor), tw[w][block][8] (in tv).
+constexpr int T2 = 128;
+
+template <int K, int RS>
+__global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restrict__ xo, double* __restrict__ yo,
+                                                    int factor_only) {
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int h = lane >> 5, r = lane & 31, rr = lane >> 3, ch = lane & 7;
+    const int kb = w ? 1 + h : 3 * h;          // own block
+    const int jr = w ? 3 : 1 + h;              // block of the recomputed t rows
+    const int rq = r >> 2, cq = r & 3;         // recomputed row / column chunk
+    constexpr int NB = 4, NP = NB * (NB - 1) / 2;  // exactly four blocks (solve.hip::variant_fits)
+    const long b = blockIdx.x;
+    const int n = p.n, m = p.m, npad = p.npad, nnzP = p.nnzP, nnzA = p.nnzA;
+    SL2 C = carve(p);
+    SLds& L = C.L;
+    const double* Hg = p.H + b * (long)p.nb * SS;
+    const double* Sg = p.Si + b * (long)p.nb * SS;
+
+    if (p.err[b]) {  // invalid data (flagged by setup/update): NaN outputs
+        for (int j = tid; j < n; j += T2) if (xo) xo[b * n + j] = __builtin_nan("");
+        for (int i = tid; i < m; i += T2) if (yo) yo[b * m + i] = __builtin_nan("");
+        if (tid == 0) p.status[b] = MPCQP_NON_CVX_;
+        return;
+    }
+
+#ifdef MPCQP_PHASE_PROF
+    long long tph = 0, t0c = 0, t0w = 0;
+    const bool prof = p.prof != nullptr;
+    if (prof) { t0w = wall_clock64(); t0c = tph = clock64(); if (tid < 16) L.pacc[tid] = 0; }
+#define PH(k) if (prof && tid == 0) { const long long t_ = clock64(); L.pacc[k] += t_ - tph; tph = t_; }
+#else
+#define PH(k)
+#endif
+
+    const double cval = p.scal[b * 4 + 0], cinv = p.scal[b * 4 + 1];
+    double rho = p.scal[b * 4 + 2];
+    const double sigma = p.sigma, alpha = p.alpha;
+    const bool warm = p.warm_start != 0;
+    for (int e = tid; e < nnzA; e += T2) L.Acsc[e] = p.Ax[b * nnzA + p.acsc_v[e]];
+    if (tid == 0) L.Acsc[nnzA] = 0.0;  // the gather lists' padding slot
+    for (int v = tid; v < nnzP; v += T2) L.Pv[v] = p.Px[b * nnzP + v];
+    if (tid == 0) L.Pv[nnzP] = 0.0;
+    const int mp = solve_mpad(m);
+    for (int i = tid; i < mp; i += T2) {  // rows >= m: inert padding (l = u = 0, z = 0)
+        const bool in = i < m;
+        L.lo[i] = in ? p.l[b * m + i] : 0.0;
+        L.up[i] = in ? p.u[b * m + i] : 0.0;
+        L.ct[i] = in ? p.ct[b * m + i] : 0;
+        C.Z[i] = (in && warm) ? p.z[b * m + i] : 0.0;
+    }
+    for (int pc = tid; pc < npad; pc += T2) {
+        L.qv[pc] = p.q[b * npad + pc];
+        C.X[pc] = warm ? p.x[b * npad + pc] : 0.0;
+    }
+    if (tid < 16) L.cor[(tid >> 3) * 32 + (tid & 7)] = 0.0;  // cw[w][0][*]: block 0 has no correction
+    if (tid < 16) L.res[tid] = 0.0;
+    if (tid < 4) L.flag[tid] = 0;
+
+    int status = MPCQP_UNSOLVED_, rho_updates = 0, iter = 0, info_iter = 0;
+    bool can_check = false, need_factor = true;
+    PH(5)
+    for (;;) {
+        __syncthreads();
+        if (need_factor) {  // start, and after a rho change
+            need_factor = false;
+            // the factorisation scratch aliases ys: y waits in the workspace's y array
+            if (iter > 0)
+                for (int i = tid; i < m; i += T2) p.y[b * m + i] = L.ys[i];
+            const bool ok = factorize_nl<T2>(p.self, b, rho);
+            if (!ok) {
+                if (iter == 0) {
+                    for (int j = tid; j < n; j += T2) if (xo) xo[b * n + j] = __builtin_nan("");
+                    for (int i = tid; i < m; i += T2) if (yo) yo[b * m + i] = __builtin_nan("");
+                    if (tid == 0) p.status[b] = MPCQP_NON_CVX_;
+                    return;
+                }
+                status = MPCQP_NON_CVX_;
+                can_check = true;  // skip the final check_termination
+                break;
+            }
+            if (factor_only) return;
+            __syncthreads();
+            const bool have_y = iter > 0 || warm;
+            for (int i = tid; i < mp; i += T2) L.ys[i] = (have_y && i < m) ? p.y[b * m + i] : 0.0;
+            // G blocks -> LDS, rows padded to 8 with zeros, plus one all-zero pair (index NP):
+            // gl[pair][row < 8][32]
+            for (int o = tid; o < (NP + 1) * 8 * S; o += T2) {
+                const int q = o >> 8, t = (o >> 5) & 7;
+                L.gl[o] = (q < NP && t < p.amax) ? Hg[(long)q * p.amax * S + (o & 255)] : 0.0;
+            }
+            PH(0)
+        }
+        // ---- run state ----
+        double SB[S], SR[8];
+        {
+            const double* src = Sg + (long)kb * SS + r * S;
+#pragma unroll
+            for (int c = 0; c < S; ++c) SB[c] = src[c];
+            const double* srr = Sg + (long)jr * SS + rq * S + 8 * cq;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) SR[i] = srr[i];
+        }
+        const int pc = kb * S + r;
+        const bool cv = p.pad_var[pc] >= 0;
+        double X = C.X[pc], DX = 0.0;
+        const double Q = L.qv[pc];
+        const unsigned abase = lds_addr(L.Acsc), wbase = lds_addr(L.w), xbase = lds_addr(L.xt);
+        GatherW<K> cg;
+        cg.load(p.gcol + (long)pc * kGS, abase, wbase);
+        // phase-C slots (pair, j) of the lane; pair NP is the zero block
+        int gslot[3], tslot[3];
+        {
+            int pr[3], jj[3];
+            if (w == 0 && h == 0) { pr[0] = 0; jj[0] = 1; pr[1] = 1; jj[1] = 2; pr[2] = 3; jj[2] = 3; }
+            else if (w == 0)      { pr[0] = NP; jj[0] = 3; pr[1] = NP; jj[1] = 3; pr[2] = NP; jj[2] = 3; }
+            else if (h == 0)      { pr[0] = 2; jj[0] = 2; pr[1] = 4; jj[1] = 3; pr[2] = NP; jj[2] = 3; }
+            else                  { pr[0] = 5; jj[0] = 3; pr[1] = NP; jj[1] = 3; pr[2] = NP; jj[2] = 3; }
+#pragma unroll
+            for (int s = 0; s < 3; ++s) {
+                gslot[s] = lds_addr(L.gl + pr[s] * 8 * S + r);
+                tslot[s] = lds_addr(L.tv + w * 32 + jj[s] * 8);
+            }
+        }
+        GatherW<K> rg[RS];
+        double y[RS], Z[RS], dy[RS], rv[RS], rvi[RS];
+        int ri[RS];
+        const double r_hi = RHO_EQ_OVER_RHO_INEQ * rho;
+#pragma unroll
+        for (int s = 0; s < RS; ++s) {
+            const int i = min(tid + s * T2, mp - 1);  // lanes past the padded rows repeat the inert last row
+            ri[s] = i;
+            dy[s] = 0.0;
+            if (i < m) rg[s].load(p.grow + (long)i * kGS, abase, xbase);
+            else rg[s].clear(abase + 8u * nnzA, xbase);
+            y[s] = L.ys[i];
+            Z[s] = C.Z[i];
+            const signed char cl = L.ct[i];  // OSQP rho_vec / rho_inv_vec of the row
+            rv[s] = cl < 0 ? RHO_MIN : (cl > 0 ? r_hi : rho);
+            rvi[s] = cl < 0 ? 1.0 / RHO_MIN : (cl > 0 ? 1.0 / r_hi : 1.0 / rho);
+        }
+        __syncthreads();  // every ys / Z read before w is written
+#pragma unroll
+        for (int s = 0; s < RS; ++s) L.w[ri[s]] = rv[s] * Z[s] - y[s];  // w = rho z_prev - y (rho may be new)
+        int stop_at = p.max_iter;
+        if (p.check_term) stop_at = min(stop_at, (iter / p.check_term + 1) * p.check_term);
+        if (p.adaptive_rho && p.rho_interval) stop_at = min(stop_at, (iter / p.rho_interval + 1) * p.rho_interval);
+        __syncthreads();
+        PH(5)
+        double* const cw = L.cor + w * 32;  // this wave's c_k rows < 8
+        double* const tw = L.tv + w * 32;   // this wave's t_j rows < 8
+        while (iter < stop_at) {
+            ++iter;
+            // rhs = sigma x_prev - q + A' (rho z_prev - y), own column
+            {
+                double av[K], wv[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    av[k] = lds_at(cg.e[k] & 0xFFFFu);
+                    wv[k] = lds_at(cg.e[k] >> 16);
+                }
+                double v = sigma * X - Q;
+#pragma unroll
+                for (int k = 0; k < K; ++k) v += av[k] * wv[k];
+                L.rb[pc] = cv ? v : 0.0;
+            }
+            __syncthreads();
+            PH(1)
+            // A (both waves): c_k = sum_{j<k} G_kj b_j, rows < 8
+            {
+                const double* gq = L.gl + rr * S + 4 * ch;
+                double bj[NB - 1][4], ga[NP][4];
+#pragma unroll
+                for (int j = 0; j < NB - 1; ++j)
+#pragma unroll
+                    for (int e = 0; e < 4; e += 2) ld2(L.rb + j * S + 4 * ch + e, bj[j][e], bj[j][e + 1]);
+#pragma unroll
+                for (int q = 0; q < NP; ++q)
+#pragma unroll
+                    for (int e = 0; e < 4; e += 2) ld2(gq + q * 8 * S + e, ga[q][e], ga[q][e + 1]);
+#pragma unroll
+                for (int k = 1; k < NB; ++k) {
+                    double acc = 0.0;
+#pragma unroll
+                    for (int j = 0; j < k; ++j)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) acc += ga[k * (k - 1) / 2 + j][e] * bj[j][e];
+                    cw[k * 8 + rr] = reduce8(acc);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            PH(12)
+            // B: own row t_kb[r] = S_kb^{-1}[r] (b_kb + c_kb); recomputed rows < 8 of t_jr
+            double t;
+            {
+                double v[S], cc[8];
+#pragma unroll
+                for (int c = 0; c < S; c += 2) ld2(L.rb + kb * S + c, v[c], v[c + 1]);
+#pragma unroll
+                for (int c = 0; c < 8; c += 2) ld2(cw + kb * 8 + c, cc[c], cc[c + 1]);
+                double u[8], uc[8];
+#pragma unroll
+                for (int i = 0; i < 8; i += 2) {
+                    ld2(L.rb + jr * S + 8 * cq + i, u[i], u[i + 1]);
+                    ld2(cw + jr * 8 + i, uc[i], uc[i + 1]);
+                }
+#pragma unroll
+                for (int c = 0; c < 8; ++c) v[c] += cc[c];
+                double a[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int c = 0; c < S; ++c) a[c & 3] += SB[c] * v[c];
+                t = (a[0] + a[1]) + (a[2] + a[3]);
+                double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+                for (int i = 0; i < 8; i += 2) {
+                    a0 += SR[i] * (cq == 0 ? u[i] + uc[i] : u[i]);
+                    a1 += SR[i + 1] * (cq == 0 ? u[i + 1] + uc[i + 1] : u[i + 1]);
+                }
+                double tr = a0 + a1;
+                tr += dpp<0xB1>(tr);
+                tr += dpp<0x4E>(tr);  // sum over the quad (the four column chunks)
+                tw[jr * 8 + rq] = tr;
+                if (r < 8) tw[kb * 8 + r] = t;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            PH(13)
+            // C: x~_kb[r] = t + sum_s G_{pair_s}[q][r] t_{j_s}[q]
+            {
+                double gv[3][8], tq[3][8];
+#pragma unroll
+                for (int s = 0; s < 3; ++s) {
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) gv[s][q] = lds_at(gslot[s] + q * S * 8);
+#pragma unroll
+                    for (int q = 0; q < 8; q += 2) {
+                        lds_at2(tslot[s] + q * 8, tq[s][q], tq[s][q + 1]);
+                    }
+                }
+                double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+                for (int s = 0; s < 3; ++s)
+#pragma unroll
+                    for (int q = 0; q < 8; q += 2) {
+                        a0 += gv[s][q] * tq[s][q];
+                        a1 += gv[s][q + 1] * tq[s][q + 1];
+                    }
+                const double xn = t + (a0 + a1);
+                L.xt[pc] = xn;
+                const double xnew = alpha * xn + (1.0 - alpha) * X;
+                DX = xnew - X;
+                X = xnew;
+            }
+            __syncthreads();
+            PH(14)
+            // z~ = A x~ ; relaxed + projected z ; y ; next w
+            {
+                double av[RS][K], xv[RS][K], lo[RS], up[RS];
+#pragma unroll
+                for (int s = 0; s < RS; ++s) {
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        av[s][k] = lds_at(rg[s].e[k] & 0xFFFFu);
+                        xv[s][k] = lds_at(rg[s].e[k] >> 16);
+                    }
+                    lo[s] = L.lo[ri[s]];
+                    up[s] = L.up[ri[s]];
+                }
+#pragma unroll
+                for (int s = 0; s < RS; ++s) {
+                    double zt = av[s][0] * xv[s][0];
+#pragma unroll
+                    for (int k = 1; k < K; ++k) zt += av[s][k] * xv[s][k];
+                    const double zr = alpha * zt + (1.0 - alpha) * Z[s];
+                    const double zn = __builtin_fmin(__builtin_fmax(zr + rvi[s] * y[s], lo[s]), up[s]);
+                    const double dd = rv[s] * (zr - zn);
+                    Z[s] = zn;
+                    dy[s] = dd;
+                    y[s] += dd;
+                    L.w[ri[s]] = rv[s] * zn - y[s];
+                }
+            }
+            __syncthreads();
+            PH(3)
+        }
+        // run state back to LDS for the out-of-line phases
+        C.X[pc] = X;
+        L.dx[pc] = DX;
+#pragma unroll
+        for (int s = 0; s < RS; ++s) { L.ys[ri[s]] = y[s]; C.Z[ri[s]] = Z[s]; C.dY[ri[s]] = dy[s]; }
+        __syncthreads();
+        // ---- out-of-line phases (only scalars live across these calls) ----
+        can_check = p.check_term && (iter % p.check_term == 0);
+        const bool do_rho = p.adaptive_rho && p.rho_interval && (iter % p.rho_interval == 0);
+        if (!can_check && !do_rho) break;  // max_iter reached
+        update_info_nl<T2>(p.self, b, cinv);
+        info_iter = iter;
+        bool stop = false;
+        if (can_check) {
+            status = check_termination_nl<T2>(p.self, b, cval, cinv, 0);
+            stop = status != MPCQP_UNSOLVED_;
+        }
+        if (!stop && do_rho) {
+            Res R;
+            R.restore(L.res);
+            const double pr = R.rpri / (cmax(R.rz, R.rax) + DIVISION_TOL);
+            const double du = R.rdua / (cmax(cmax(R.rq, R.raty), R.rpx) + DIVISION_TOL);
+            double rn = rho * sqrt(pr / (du + DIVISION_TOL));
+            rn = cmin(cmax(rn, RHO_MIN), RHO_MAX);
+            if (rn > rho * p.rho_tol || rn < rho / p.rho_tol) {
+                rho = cmin(cmax(rn, RHO_MIN), RHO_MAX);
+                rho_updates++;
+                need_factor = true;
+            }
+        }
+        __syncthreads();
+        PH(4)
+        if (stop || iter >= p.max_iter) break;
+    }
+    if (!can_check && status == MPCQP_UNSOLVED_) {
+        update_info_nl<T2>(p.self, b, cinv);
+        info_iter = iter;
+        status = check_termination_nl<T2>(p.self, b, cval, cinv, 0);
+    }
+    const bool has_sol = !(status == MPCQP_PRIMAL_INFEASIBLE_ || status == MPCQP_PRIMAL_INFEASIBLE_INACCURATE_ ||
+                           status == MPCQP_DUAL_INFEASIBLE_ || status == MPCQP_DUAL_INFEASIBLE_INACCURATE_ ||
+                           status == MPCQP_NON_CVX_);
+    if (has_sol) objective_nl<T2>(p.self, cinv);
+    if (status == MPCQP_UNSOLVED_) {
+        status = check_termination_nl<T2>(p.self, b, cval, cinv, 1);
+        if (status == MPCQP_UNSOLVED_) status = MPCQP_MAX_ITER_REACHED_;
+    }
+    finalize_nl<T2>(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates);
+#ifdef MPCQP_PHASE_PROF
+    if (prof) {
+        __syncthreads();
+        PH(5)
+        if (tid == 0) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) p.prof[b * kProfSlots + k] = L.pacc[k];
+#pragma unroll
+            for (int k = 8; k < 15; ++k) p.prof[b * kProfSlots + k] = L.pacc[k];
+            p.prof[b * kProfSlots + 2] = L.pacc[12] + L.pacc[13] + L.pacc[14];
+            p.prof[b * kProfSlots + 6] = clock64() - t0c;
+            p.prof[b * kProfSlots + 7] = wall_clock64() - t0w;
+        }
+    }
+#endif
+#undef PH
+}
+
+template <int K, int RS>
+static hipError_t go_w2(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st, size_t lds) {
+    auto k = k_solve_w2<K, RS>;
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(T2), lds, st, p, xo, yo, fo);
+    return hipGetLastError();
+}
+
+template <int K, int RS>
+static hipError_t go_w(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st, size_t lds) {
+    auto k = k_solve_w<K, RS>;
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(TW), lds, st, p, xo, yo, fo);
+    return hipGetLastError();
+}
+
+// Wave-kernel instantiations (solve.hip::variant_fits gives their preconditions).
+hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st) {
+    const size_t lds = lds_solve_bytes(p);
+    switch (p.variant) {
+        case 8: return go_w<6, 3>(p, B, xo, yo, factor_only, st, lds);
+        case 9: return go_w<8, 4>(p, B, xo, yo, factor_only, st, lds);
+        case 10: return go_w2<6, 2>(p, B, xo, yo, factor_only, st, lds);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace mpcqp

@@ -60,6 +60,9 @@ def main():
             print(f"   {nm:9s} {row[k]:12.0f} cyc {100 * row[k] / tot:5.1f}%  {row[k] / max(its, 1):8.0f} /iter")
         for k, nm in zip(range(8, 12), ["f.asm", "f.F/S", "f.GJ", "f.epi"]):
             print(f"     {nm:7s} {row[k]:12.0f} cyc")
+        if row[12:15].any():
+            for k, nm in zip(range(12, 15), ["s.A", "s.B", "s.C"]):
+                print(f"     {nm:7s} {row[k]:12.0f} cyc  {row[k] / max(its, 1):8.0f} /iter")
 
 
 if __name__ == "__main__":
