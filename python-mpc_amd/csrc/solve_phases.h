@@ -34,6 +34,59 @@ __device__ __forceinline__ double rho_of(signed char t, double rho) {
     return t < 0 ? RHO_MIN : (t > 0 ? RHO_EQ_OVER_RHO_INEQ * rho : rho);
 }
 
+// Gauss-Jordan inverse of the SPD tile T (32 x 32 in LDS) by ONE wave, in place, with a
+// copy to Sgk.  Lane (i, h) = (lane % 32, lane / 32) keeps row i, columns [16 h, 16 h + 16)
+// in registers.  The in-place Gauss-Jordan matrix of a symmetric input stays symmetric up
+// to sign -- M_ij = -M_ji exactly when one of i, j is already pivoted -- so row p is
+// published by the lanes that hold column p (one ds_write_b64 per lane and pivot) and the
+// 32 pivots need no workgroup barrier.  buf: 2 S doubles.  False on a non-positive pivot.
+__device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restrict__ buf, double* __restrict__ Sgk) {
+    const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
+    double v[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; jj += 2) {
+        const double2 t2 = *(const double2*)(T + i * S + 16 * h + jj);
+        v[jj] = t2.x;
+        v[jj + 1] = t2.y;
+    }
+    bool ok = true;
+#pragma unroll
+    for (int p = 0; p < S; ++p) {
+        double* rb = buf + (p & 1) * S;
+        if (h == (p >> 4)) rb[i] = i < p ? -v[p & 15] : v[p & 15];  // row p = +-column p
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double rowv[16];
+#pragma unroll
+        for (int jj = 0; jj < 16; jj += 2) {
+            const double2 t2 = *(const double2*)(rb + 16 * h + jj);
+            rowv[jj] = t2.x;
+            rowv[jj + 1] = t2.y;
+        }
+        const double piv = rb[p];
+        const double mi = rb[i];
+        const double colv = i < p ? -mi : mi;  // M_ip
+        ok = ok && piv > 0.0;
+        const double d = 1.0 / piv;
+        if (i == p) {
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) v[jj] = rowv[jj] * d;
+        } else {
+            const double cd = colv * d;
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) v[jj] = __builtin_fma(-cd, rowv[jj], v[jj]);
+        }
+        if (h == (p >> 4)) v[p & 15] = i == p ? d : -colv * d;
+    }
+#pragma unroll
+    for (int jj = 0; jj < 16; jj += 2) {
+        *(double2*)(T + i * S + 16 * h + jj) = make_double2(v[jj], v[jj + 1]);
+        *(double2*)(Sgk + i * S + 16 * h + jj) = make_double2(v[jj], v[jj + 1]);
+    }
+    return ok;
+}
+
 // Assemble K's tiles for the current rho and factor them (block LDL'):
 //   S_0 = D_0,  F_k = E_k S_{k-1}^{-1},  S_k = D_k - F_k E_k',  H_{k-1} = F_k'
 // E_k is nonzero only in its first amax rows (block k's first BFS level), so F_k
@@ -135,60 +188,72 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
             __syncthreads();
         }
         FPH(9)
-        // Gauss-Jordan inverse with the tile in registers: thread (i0 + TT/8 * ii, jg)
-        // keeps elements [i][jg + 8c]; per pivot only its row and column go through
-        // LDS (double-buffered in EK, free by now), so each pivot costs one barrier.
-        double v[NI][4];
-#pragma unroll
-        for (int ii = 0; ii < NI; ++ii)
-#pragma unroll
-            for (int cc = 0; cc < 4; ++cc) v[ii][cc] = DK[(i0 + TT / 8 * ii) * S + jg + 8 * cc];
-        double* rowbuf = EK;
-        double* colbuf = EK + 2 * S;
-#pragma unroll 1
-        for (int pv = 0; pv < S; ++pv) {
-            const int buf = (pv & 1) * S;
-            const int cp = pv >> 3;
-#pragma unroll
-            for (int ii = 0; ii < NI; ++ii) {
-                const int i = i0 + TT / 8 * ii;
-                if (i == pv) {
-#pragma unroll
-                    for (int cc = 0; cc < 4; ++cc) rowbuf[buf + jg + 8 * cc] = v[ii][cc];
-                }
-                if (jg == (pv & 7))
-                    colbuf[buf + i] = cp == 0 ? v[ii][0] : cp == 1 ? v[ii][1] : cp == 2 ? v[ii][2] : v[ii][3];
+        if constexpr (TT <= 128) {
+            // one wave inverts the tile (no barrier per pivot); the verdict goes through LDS
+            double* okslot = EK + 2 * S;
+            if (tid < 64) {
+                const bool okw = gj_wave(DK, EK, Sg + (long)k * SS);
+                if (tid == 0) okslot[0] = okw ? 1.0 : 0.0;
             }
             __syncthreads();
-            const double piv = rowbuf[buf + pv];
-            if (!(piv > 0.0)) ok = false;
-            const double d = 1.0 / piv;
-            double rowv[4];
+            if (!(okslot[0] > 0.5)) ok = false;
+            FPH(10)
+        } else {
+            // Gauss-Jordan inverse with the tile in registers: thread (i0 + TT/8 * ii, jg)
+            // keeps elements [i][jg + 8c]; per pivot only its row and column go through
+            // LDS (double-buffered in EK, free by now), so each pivot costs one barrier.
+            double v[NI][4];
 #pragma unroll
-            for (int cc = 0; cc < 4; ++cc) rowv[cc] = rowbuf[buf + jg + 8 * cc];
+            for (int ii = 0; ii < NI; ++ii)
 #pragma unroll
-            for (int ii = 0; ii < NI; ++ii) {
-                const int i = i0 + TT / 8 * ii;
-                const double colv = colbuf[buf + i];
+                for (int cc = 0; cc < 4; ++cc) v[ii][cc] = DK[(i0 + TT / 8 * ii) * S + jg + 8 * cc];
+            double* rowbuf = EK;
+            double* colbuf = EK + 2 * S;
+#pragma unroll 1
+            for (int pv = 0; pv < S; ++pv) {
+                const int buf = (pv & 1) * S;
+                const int cp = pv >> 3;
 #pragma unroll
-                for (int cc = 0; cc < 4; ++cc) {
-                    const int j = jg + 8 * cc;
-                    if (i == pv) v[ii][cc] = (j == pv) ? d : rowv[cc] * d;
-                    else if (j == pv) v[ii][cc] = -colv * d;
-                    else v[ii][cc] = v[ii][cc] - colv * (rowv[cc] * d);
+                for (int ii = 0; ii < NI; ++ii) {
+                    const int i = i0 + TT / 8 * ii;
+                    if (i == pv) {
+#pragma unroll
+                        for (int cc = 0; cc < 4; ++cc) rowbuf[buf + jg + 8 * cc] = v[ii][cc];
+                    }
+                    if (jg == (pv & 7))
+                        colbuf[buf + i] = cp == 0 ? v[ii][0] : cp == 1 ? v[ii][1] : cp == 2 ? v[ii][2] : v[ii][3];
+                }
+                __syncthreads();
+                const double piv = rowbuf[buf + pv];
+                if (!(piv > 0.0)) ok = false;
+                const double d = 1.0 / piv;
+                double rowv[4];
+#pragma unroll
+                for (int cc = 0; cc < 4; ++cc) rowv[cc] = rowbuf[buf + jg + 8 * cc];
+#pragma unroll
+                for (int ii = 0; ii < NI; ++ii) {
+                    const int i = i0 + TT / 8 * ii;
+                    const double colv = colbuf[buf + i];
+#pragma unroll
+                    for (int cc = 0; cc < 4; ++cc) {
+                        const int j = jg + 8 * cc;
+                        if (i == pv) v[ii][cc] = (j == pv) ? d : rowv[cc] * d;
+                        else if (j == pv) v[ii][cc] = -colv * d;
+                        else v[ii][cc] = v[ii][cc] - colv * (rowv[cc] * d);
+                    }
                 }
             }
+#pragma unroll
+            for (int ii = 0; ii < NI; ++ii)
+#pragma unroll
+                for (int cc = 0; cc < 4; ++cc) DK[(i0 + TT / 8 * ii) * S + jg + 8 * cc] = v[ii][cc];
+            FPH(10)
+#pragma unroll
+            for (int ii = 0; ii < NI; ++ii)
+#pragma unroll
+                for (int cc = 0; cc < 4; ++cc)
+                    Sg[(long)k * SS + (i0 + TT / 8 * ii) * S + jg + 8 * cc] = v[ii][cc];
         }
-#pragma unroll
-        for (int ii = 0; ii < NI; ++ii)
-#pragma unroll
-            for (int cc = 0; cc < 4; ++cc) DK[(i0 + TT / 8 * ii) * S + jg + 8 * cc] = v[ii][cc];
-        FPH(10)
-#pragma unroll
-        for (int ii = 0; ii < NI; ++ii)
-#pragma unroll
-            for (int cc = 0; cc < 4; ++cc)
-                Sg[(long)k * SS + (i0 + TT / 8 * ii) * S + jg + 8 * cc] = v[ii][cc];
         double* t = SP; SP = DK; DK = t;  // S_k^{-1} becomes "previous"
         __syncthreads();
         FPH(11)
@@ -348,7 +413,7 @@ __device__ __noinline__ void update_info_nl(const KParams* gp, long b, double ci
     double v[14];
 #pragma unroll
     for (int k = 0; k < 14; ++k) v[k] = 0.0;
-    #pragma unroll 1
+#pragma unroll 1
     for (int i = tid; i < m; i += TT) {
         const double ax = row_dot(p, c.L.Acsc, c.X, i);
         const double zi = c.Z[i];
@@ -361,7 +426,7 @@ __device__ __noinline__ void update_info_nl(const KParams* gp, long b, double ci
         v[9] = cmax(v[9], fabs(zi));
         v[10] = cmax(v[10], fabs(ax));
     }
-    #pragma unroll 1
+#pragma unroll 1
     for (int pc = tid; pc < npad; pc += TT) {
         if (p.pad_var[pc] < 0) continue;
         const double px = psym_dot(p, c.L.Pv, c.X, pc);
@@ -404,7 +469,7 @@ __device__ bool primal_infeasible(const KP& p, SL2& c, long b, double eps) {
     const double* Eg = p.E + b * m;
     const double* Dg = p.D + b * npad;
     double nd[1] = {0.0};
-    #pragma unroll 1
+#pragma unroll 1
     for (int i = tid; i < m; i += TT) {
         double d = c.dY[i];
         if (c.L.up[i] > OSQP_INFTY * MIN_SCALING) d = (c.L.lo[i] < -OSQP_INFTY * MIN_SCALING) ? 0.0 : cmin(d, 0.0);
@@ -416,12 +481,12 @@ __device__ bool primal_infeasible(const KP& p, SL2& c, long b, double eps) {
     const double norm_dy = nd[0];
     if (!(norm_dy > eps)) return false;
     double sum[1] = {0.0};
-    #pragma unroll 1
+#pragma unroll 1
     for (int i = tid; i < m; i += TT) sum[0] += c.L.up[i] * cmax(c.dY[i], 0.0) + c.L.lo[i] * cmin(c.dY[i], 0.0);
     block_sum<TT>(sum, c.L.red);
     if (!(sum[0] < eps * norm_dy)) return false;
     double na[1] = {0.0};
-    #pragma unroll 1
+#pragma unroll 1
     for (int pc = tid; pc < npad; pc += TT) {
         if (p.pad_var[pc] < 0) continue;
         double a = col_dot(p, c.L.Acsc, c.dY, pc);
@@ -441,7 +506,7 @@ __device__ bool dual_infeasible(const KP& p, SL2& c, long b, double cs_, double 
     const double* Dg = p.D + b * npad;
     const double cs = unscale ? cs_ : 1.0;
     double v[1] = {0.0}, sum[1] = {0.0};
-    #pragma unroll 1
+#pragma unroll 1
     for (int pc = tid; pc < npad; pc += TT) {
         if (p.pad_var[pc] < 0) continue;
         const double dx = c.L.dx[pc];
@@ -454,7 +519,7 @@ __device__ bool dual_infeasible(const KP& p, SL2& c, long b, double cs_, double 
     block_sum<TT>(sum, c.L.red);
     if (!(sum[0] < cs * eps * norm_dx)) return false;
     double np[1] = {0.0};
-    #pragma unroll 1
+#pragma unroll 1
     for (int pc = tid; pc < npad; pc += TT) {
         if (p.pad_var[pc] < 0) continue;
         double a = psym_dot(p, c.L.Pv, c.L.dx, pc);
@@ -464,7 +529,7 @@ __device__ bool dual_infeasible(const KP& p, SL2& c, long b, double cs_, double 
     block_max<TT>(np, c.L.red);
     if (!(np[0] < cs * eps * norm_dx)) return false;
     bool viol = false;
-    #pragma unroll 1
+#pragma unroll 1
     for (int i = tid; i < m; i += TT) {
         double a = row_dot(p, c.L.Acsc, c.L.dx, i);
         if (unscale) a *= 1.0 / Eg[i];
@@ -533,12 +598,12 @@ __device__ __noinline__ void objective_nl(const KParams* gp, double cinv) {
     SL2 c = carve(p);
     const int tid = threadIdx.x;
     double sacc[1] = {0.0};
-    #pragma unroll 1
+#pragma unroll 1
     for (int v = tid; v < p.nnzP; v += TT) {
         const int r = p.p_r[v], cc = p.p_c[v];
         sacc[0] += (r == cc) ? 0.5 * c.L.Pv[v] * c.X[r] * c.X[r] : c.L.Pv[v] * c.X[r] * c.X[cc];
     }
-    #pragma unroll 1
+#pragma unroll 1
     for (int pc = tid; pc < p.npad; pc += TT) sacc[0] += c.L.qv[pc] * c.X[pc];
     block_sum<TT>(sacc, c.L.red);
     if (tid == 0) c.L.res[14] = p.scaling ? sacc[0] * cinv : sacc[0];
@@ -571,14 +636,14 @@ __device__ __noinline__ void finalize_nl(const KParams* gp, long b, double* __re
     const bool dinf = status == MPCQP_DUAL_INFEASIBLE_ || status == MPCQP_DUAL_INFEASIBLE_INACCURATE_;
     const bool dx_scaled = c.L.flag[2] != 0, dy_scaled = c.L.flag[3] != 0;
     double nrm[2] = {0.0, 0.0};
-    #pragma unroll 1
+#pragma unroll 1
     for (int pc = tid; pc < npad; pc += TT) {
         double dx = c.L.dx[pc];
         if (dx_scaled) dx *= Dg[pc];
         c.L.dx[pc] = dx;
         nrm[1] = cmax(nrm[1], fabs(dx));
     }
-    #pragma unroll 1
+#pragma unroll 1
     for (int i = tid; i < m; i += TT) {
         double dy = c.dY[i];
         if (dy_scaled) dy *= Eg[i];
@@ -586,7 +651,7 @@ __device__ __noinline__ void finalize_nl(const KParams* gp, long b, double* __re
         nrm[0] = cmax(nrm[0], fabs(dy));
     }
     block_max<TT>(nrm, c.L.red);
-    #pragma unroll 1
+#pragma unroll 1
     for (int pc = tid; pc < npad; pc += TT) {
         const int j = p.pad_var[pc];
         const double xv = c.X[pc];
@@ -596,7 +661,7 @@ __device__ __noinline__ void finalize_nl(const KParams* gp, long b, double* __re
         }
         p.x[b * npad + pc] = has_sol ? xv : 0.0;
     }
-    #pragma unroll 1
+#pragma unroll 1
     for (int i = tid; i < m; i += TT) {
         const double yv = c.L.ys[i];
         if (yo) yo[b * m + i] = has_sol ? (p.scaling ? (Eg[i] * yv) * cinv : yv) : __builtin_nan("");
