@@ -201,11 +201,13 @@ def main():
                        "parallelism": f"batch-shard x{world}",
                        "iters_mean": float(iters.mean()), "iters_max": int(iters.max()),
                        "solved_frac": float(np.mean(status == 1)),
-                       "plan": {"nb": info["nb"], "block": S, "lds_bytes": info["lds_bytes_solve"]}},
+                       "plan": {"nb": info["nb"], "block": S, "amax": info["amax"], "lds_bytes": info["lds_bytes_solve"],
+                                "kernel_variant": info["variant"], "threads_per_qp": info["threads_per_qp"]}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic.get("bytes_per_launch"),
                          "traffic_source": traffic.get("source"),
-                         "kernel": "mpcqp::k_solve", "kernel_ms": solve_ms, "setup_kernel_ms": setup_ms,
+                         "kernel": {64: "mpcqp::k_solve_w", 128: "mpcqp::k_solve_w2"}.get(info["threads_per_qp"], "mpcqp::k_solve"),
+                         "kernel_ms": solve_ms, "setup_kernel_ms": setup_ms,
                          "bytes_per_solve": bytes_per_solve, "launch_instances": B,
                          "fp64_tflops_model": fp64_tflops, "fp64_peak_tflops": FP64_PEAK_TFLOPS},
             "cpu_baseline": cpu,

@@ -80,6 +80,10 @@ typedef struct {
     int32_t n_devices;
     int64_t lds_bytes_solve;    /* dynamic LDS per workgroup of the ADMM kernel */
     int64_t bytes_per_instance; /* device workspace per instance */
+    int32_t amax;               /* coupling rows of the off-diagonal blocks */
+    int32_t gather_k;           /* max nonzeros per row / column of A */
+    int32_t variant;            /* solve-kernel instantiation in use */
+    int32_t threads_per_qp;     /* workgroup size of that kernel */
 } mpcqp_plan_info;
 
 typedef struct mpcqp_handle mpcqp_handle;

@@ -551,6 +551,10 @@ int mpcqp_get_plan_info(const mpcqp_handle* h, mpcqp_plan_info* info) {
     info->batch = h->B; info->n_devices = (int)h->shards.size();
     info->lds_bytes_solve = h->shards.empty() ? 0 : (int64_t)lds_solve_bytes(h->shards[0].kp);
     info->bytes_per_instance = (int64_t)(workspace_bytes(h->plan, 1, false));
+    info->amax = h->plan.amax;
+    info->gather_k = h->plan.gather_k;
+    info->variant = h->shards.empty() ? -1 : h->shards[0].kp.variant;
+    info->threads_per_qp = h->shards.empty() ? 0 : solve_threads(h->shards[0].kp.variant);
     return 0;
 }
 

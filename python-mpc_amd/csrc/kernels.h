@@ -55,6 +55,7 @@ hipError_t launch_update(const KParams& p, long B, const double* q, const double
 hipError_t launch_warm(const KParams& p, long B, const double* x, const double* y, hipStream_t st);
 int solve_variant(const KParams& p);  // -1: no instantiation fits the plan
 int solve_mode(int variant);
+int solve_threads(int variant);  // workgroup size of the variant's kernel
 bool variant_fits(const KParams& p, int variant);
 hipError_t launch_solve(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st);
 // one-wave-per-QP kernel (solve_wave.hip), variants 8 and 9

@@ -535,6 +535,14 @@ int solve_variant(const KParams& p) {
     return -1;
 }
 
+int solve_threads(int variant) {
+    switch (variant) {
+        case 8: case 9: return 64;
+        case 10: return 128;
+        default: return T;
+    }
+}
+
 int solve_mode(int variant) {  // what factorize stores for the variant (KParams::mode)
     switch (variant) {
         case 0: case 8: case 9: case 10: return 2;

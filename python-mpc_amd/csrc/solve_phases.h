@@ -68,7 +68,10 @@ __device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restri
         const double mi = rb[i];
         const double colv = i < p ? -mi : mi;  // M_ip
         ok = ok && piv > 0.0;
-        const double d = 1.0 / piv;
+        // 1 / piv: hardware reciprocal and two Newton steps (full double precision)
+        double d = __builtin_amdgcn_rcp(piv);
+        d = __builtin_fma(d, __builtin_fma(-piv, d, 1.0), d);
+        d = __builtin_fma(d, __builtin_fma(-piv, d, 1.0), d);
         if (i == p) {
 #pragma unroll
             for (int jj = 0; jj < 16; ++jj) v[jj] = rowv[jj] * d;
@@ -124,19 +127,39 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
         __syncthreads();
         if (tid < S) DK[tid * S + tid] = p.pad_var[k * S + tid] >= 0 ? p.sigma : 1.0;
         __syncthreads();
-        // every target has one owner: its terms are summed in plan order
+        // every target has one owner: its terms are summed in plan order.  Four targets
+        // per thread and pass, so that their term loads (the ELL plan in global memory,
+        // L2-resident) are in flight together.
+        {
+            const int t_beg = p.asm_blk_ptr[k], t_end = p.asm_blk_ptr[k + 1];
+            const int2 zt = make_int2(p.nnzA | (p.nnzA << 16), 0);
 #pragma unroll 1
-        for (int t = p.asm_blk_ptr[k] + tid; t < p.asm_blk_ptr[k + 1]; t += TT) {
-            double acc = 0.0;
-#pragma unroll 4
-            for (int j = 0; j < tmax; ++j) {
-                const int2 w = tt[(long)j * ntgt + t];
-                const int a = w.x & 0xFFFF, bb = (int)((unsigned)w.x >> 16), r = w.y;
-                acc += r < 0 ? L.Pv[a] : rho_of(L.ct[r], rho) * L.Acsc[a] * L.Acsc[bb];
+            for (int t0 = t_beg + tid; t0 < t_end; t0 += 4 * TT) {
+                double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 2
+                for (int j = 0; j < tmax; ++j) {
+                    int2 w[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int t = t0 + u * TT;
+                        w[u] = t < t_end ? tt[(long)j * ntgt + t] : zt;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int a = w[u].x & 0xFFFF, bb = (int)((unsigned)w[u].x >> 16), r = w[u].y;
+                        acc[u] += r < 0 ? L.Pv[a] : rho_of(L.ct[r], rho) * L.Acsc[a] * L.Acsc[bb];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int t = t0 + u * TT;
+                    if (t < t_end) {
+                        const int tg = p.asm_tgt[t];
+                        if (tg < SS) DK[tg] += acc[u];
+                        else EK[tg - SS] += acc[u];
+                    }
+                }
             }
-            const int tg = p.asm_tgt[t];
-            if (tg < SS) DK[tg] += acc;
-            else EK[tg - SS] += acc;
         }
         __syncthreads();
         FPH(8)
@@ -188,7 +211,7 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
             __syncthreads();
         }
         FPH(9)
-        if constexpr (TT <= 128) {
+        if constexpr (TT <= 256) {
             // one wave inverts the tile (no barrier per pivot); the verdict goes through LDS
             double* okslot = EK + 2 * S;
             if (tid < 64) {

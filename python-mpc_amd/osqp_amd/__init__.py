@@ -79,6 +79,7 @@ class _PlanInfo(C.Structure):
         ("n", C.c_int32), ("m", C.c_int32), ("nb", C.c_int32), ("block", C.c_int32),
         ("npad", C.c_int32), ("max_level", C.c_int32), ("batch", C.c_int64),
         ("n_devices", C.c_int32), ("lds_bytes_solve", C.c_int64), ("bytes_per_instance", C.c_int64),
+        ("amax", C.c_int32), ("gather_k", C.c_int32), ("variant", C.c_int32), ("threads_per_qp", C.c_int32),
     ]
 
 
