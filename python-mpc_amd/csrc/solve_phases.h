@@ -427,7 +427,7 @@ __device__ __forceinline__ double psym_dot(const KP& p, const double* Pv, const 
 // update_info: residuals and the norms of their tolerances (OSQP compute_pri_res /
 // compute_dua_res / compute_pri_tol / compute_dua_tol, scaled and unscaled)
 template <int TT>
-__device__ __noinline__ void update_info_nl(const KParams* gp, long b, double cinv) {
+__device__ __forceinline__ void update_info_ph(const KParams* gp, long b, double cinv) {
     KPc& p = kconst(gp);
     SL2 c = carve(p);
     const int tid = threadIdx.x, m = p.m, npad = p.npad;
@@ -482,6 +482,10 @@ __device__ __noinline__ void update_info_nl(const KParams* gp, long b, double ci
         R.save(c.L.res);
     }
     __syncthreads();
+}
+template <int TT>
+__device__ __noinline__ void update_info_nl(const KParams* gp, long b, double cinv) {
+    update_info_ph<TT>(gp, b, cinv);
 }
 
 // is_primal_infeasible (delta_y in dY, projected in place as OSQP does)
@@ -565,7 +569,7 @@ __device__ bool dual_infeasible(const KP& p, SL2& c, long b, double cs_, double 
 
 // check_termination on the Res in LDS; status / obj / certificate flags in LDS.
 template <int TT>
-__device__ __noinline__ int check_termination_nl(const KParams* gp, long b, double cval, double cinv,
+__device__ __forceinline__ int check_termination_ph(const KParams* gp, long b, double cval, double cinv,
                                                  int approximate) {
     KPc& p = kconst(gp);
     SL2 c = carve(p);
@@ -613,10 +617,15 @@ __device__ __noinline__ int check_termination_nl(const KParams* gp, long b, doub
     __syncthreads();
     return done ? st : MPCQP_UNSOLVED_;
 }
+template <int TT>
+__device__ __noinline__ int check_termination_nl(const KParams* gp, long b, double cval, double cinv,
+                                                 int approximate) {
+    return check_termination_ph<TT>(gp, b, cval, cinv, approximate);
+}
 
 // compute_obj_val (needs X)
 template <int TT>
-__device__ __noinline__ void objective_nl(const KParams* gp, double cinv) {
+__device__ __forceinline__ void objective_ph(const KParams* gp, double cinv) {
     KPc& p = kconst(gp);
     SL2 c = carve(p);
     const int tid = threadIdx.x;
@@ -632,10 +641,14 @@ __device__ __noinline__ void objective_nl(const KParams* gp, double cinv) {
     if (tid == 0) c.L.res[14] = p.scaling ? sacc[0] * cinv : sacc[0];
     __syncthreads();
 }
+template <int TT>
+__device__ __noinline__ void objective_nl(const KParams* gp, double cinv) {
+    objective_ph<TT>(gp, cinv);
+}
 
 // store_solution + info (y is in ys)
 template <int TT>
-__device__ __noinline__ void finalize_nl(const KParams* gp, long b, double* __restrict__ xo,
+__device__ __forceinline__ void finalize_ph(const KParams* gp, long b, double* __restrict__ xo,
                                          double* __restrict__ yo, double cinv, double rho, int status,
                                          int info_iter, int rho_updates) {
     KPc& p = kconst(gp);
@@ -703,13 +716,23 @@ __device__ __noinline__ void finalize_nl(const KParams* gp, long b, double* __re
         p.scal[b * 4 + 2] = rho;
     }
 }
+template <int TT>
+__device__ __noinline__ void finalize_nl(const KParams* gp, long b, double* __restrict__ xo,
+                                         double* __restrict__ yo, double cinv, double rho, int status,
+                                         int info_iter, int rho_updates) {
+    finalize_ph<TT>(gp, b, xo, yo, cinv, rho, status, info_iter, rho_updates);
+}
 
 template <int TT>
-__device__ __noinline__ bool factorize_nl(const KParams* gp, long b, double rho) {
+__device__ __forceinline__ bool factorize_ph(const KParams* gp, long b, double rho) {
     KPc& p = kconst(gp);
     SL2 c = carve(p);
     return factorize<TT>(p, c.L, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
                      p.Si + b * (long)p.nb * SS);
+}
+template <int TT>
+__device__ __noinline__ bool factorize_nl(const KParams* gp, long b, double rho) {
+    return factorize_ph<TT>(gp, b, rho);
 }
 
 
