@@ -158,6 +158,64 @@ int mpcqp_analyze(int32_t n, int32_t m, const int32_t *Pp, const int32_t *Pi,
                   const int32_t *Ap, const int32_t *Ai, int32_t *nb, int32_t *block,
                   int32_t *var_pad, int32_t *bsize);
 
+/* ======================================================================
+ * The MPC data path around the solver, on the device.
+ * Replaces the Python work of Control/MPC/mpc_dynamics.py:main between two
+ * osqp solves, batched over B vehicles.  Device pointers, enqueued on `stream`.
+ * ====================================================================== */
+
+/* Vehicle_Dynamics(...) constructor arguments (Vehicle_Dynamics/vehicle_models.py:27-50) */
+typedef struct {
+    double m, l_f, l_r, width, length, C_d, A_f, C_roll, dt;
+} mpcqp_vehicle;
+
+/* F2 -- Vehicle_Dynamics.get_dynamics_model (vehicle_models.py:52-340), batched.
+ * For b < B, k < N: x = dx[b*x_sb + k*x_sk + 0..6) = (X, Y, yaw, vx, vy, r),
+ * u = du[b*u_sb + k*u_sk + 0..2) = (steer, accel)  ->  Ad[(b*N + k)*36] (6x6),
+ * Bd[(b*N + k)*12] (6x2), gd[(b*N + k)*6], row-major.  The low-speed guard
+ * (:143-159) acts on copies: unlike the reference, inputs are never written. */
+int mpcqp_linearise_device(const mpcqp_vehicle *veh, int64_t B, int32_t N, const double *dx, int64_t x_sb,
+                           int64_t x_sk, const double *du, int64_t u_sb, int64_t u_sk, double *dAd, double *dBd,
+                           double *dgd, int32_t device, void *stream);
+
+/* F1 -- the QP of mpc_increment (Control/MPC/mpc_dynamics.py:281-389) for a batch
+ * sharing N, nx, nu, weights, bounds and the structural nonzeros of Ad / Bd
+ * (maskA[nx*nx], maskB[nx*nu], 1 = entry may be nonzero).  Q, QN (nx x nx) and
+ * R (nu x nu) are dense row-major; xmin_t / xmax_t have nx+nu entries, dumin /
+ * dumax nu (+-inf allowed; clipped to +-1e30 as the osqp wrapper does).
+ * Variables (x~_0..x~_N, du_0..du_{N-1}), x~ = (x, u_prev); rows [A_eq; I]. */
+typedef struct mpcqp_incr_layout mpcqp_incr_layout;
+int mpcqp_incr_layout_create(int32_t N, int32_t nx, int32_t nu, const double *Q, const double *QN, const double *R,
+                             const double *xmin_t, const double *xmax_t, const double *dumin, const double *dumax,
+                             const uint8_t *maskA, const uint8_t *maskB, int32_t device, mpcqp_incr_layout **out);
+int mpcqp_incr_layout_dims(const mpcqp_incr_layout *L, int32_t *n, int32_t *m, int32_t *nnzP, int32_t *nnzA);
+/* The shared pattern (P upper-triangular CSC with its constant values; A CSC) and the
+ * constant parts of the per-instance arrays; any pointer may be NULL. */
+int mpcqp_incr_layout_pattern(const mpcqp_incr_layout *L, int32_t *Pp, int32_t *Pi, double *Px, int32_t *Ap,
+                              int32_t *Ai, double *Ax_template, double *l_template, double *u_template);
+/* Per instance b: Ad/Bd/gd as produced by mpcqp_linearise_device for stages 0..N-1,
+ * xt0[b*(nx+nu)] = x~(0), Xr[b*nx*(N+1)] = reference (nx rows, N+1 columns)
+ * -> Ax[b*nnzA], q[b*n], l[b*m], u[b*m] for mpcqp_setup_device. */
+int mpcqp_incr_assemble_device(const mpcqp_incr_layout *L, int64_t B, const double *dAd, const double *dBd,
+                               const double *dgd, const double *dxt0, const double *dXr, double *dAx, double *dq,
+                               double *dl, double *du, void *stream);
+void mpcqp_incr_layout_free(mpcqp_incr_layout *L);
+
+/* F3 -- reference_search (mpc_dynamics.py:44-90, nearest_point :30-41) for every
+ * vehicle: pred[b*(N+1)*nxa + k*nxa + 0..nxa) predicted augmented states
+ * -> Xr[b*6*(N+1)] (6 rows: path x, path y, yaw 0, vx 10, vy 0, r 0).  Near the
+ * path's end the index stops at the last point (the reference indexes past it). */
+int mpcqp_reference_search_device(int64_t B, int32_t N, int32_t nxa, int32_t npath, const double *dpath_x,
+                                  const double *dpath_y, const double *dpred, double dt, double *dXr, int32_t device,
+                                  void *stream);
+/* F3 -- plant step and horizon shift of mpc_dynamics.main (:578-617), dynamic bicycle
+ * (nx 6, nu 2): from the unscaled solutions sol[b*n] and the step's stage-0 model
+ * (Ad/Bd/gd of mpcqp_linearise_device), advance x~ (xt[b*8], in/out) and write the
+ * shifted predictions pred[b*(N+1)*8] and pred_du[b*(N+1)*2]. */
+int mpcqp_incr_shift_device(const mpcqp_incr_layout *L, const mpcqp_vehicle *veh, int64_t B, const double *dsol,
+                            const double *dAd, const double *dBd, const double *dgd, double *dxt, double *dpred,
+                            double *dpdu, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

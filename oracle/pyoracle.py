@@ -194,7 +194,7 @@ class OSQP:
         return lib().orc_kkt_nnz_L(self._w)
 
     def __del__(self):
-        if getattr(self, "_w", None) and self._w.value:
+        if getattr(self, "_w", None) and self._w.value and lib is not None:  # module torn down at exit
             lib().orc_cleanup(self._w)
             self._w = C.c_void_p()
 

@@ -39,6 +39,21 @@ int fail(int code, const char* fmt, ...) {
     return code;
 }
 
+}  // namespace
+
+// shared with the other translation units of the library (mpc_device.hip)
+int mpcqp::set_error(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+namespace {
+
 #define HIPCHK(expr)                                                                        \
     do {                                                                                    \
         hipError_t e_ = (expr);                                                             \

@@ -48,6 +48,9 @@ struct KParams {
 
 size_t lds_setup_bytes(const KParams& p);
 size_t lds_solve_bytes(const KParams& p);
+// error text for mpcqp_last_error() (api.hip); returns code
+int set_error(int code, const char* fmt, ...);
+
 hipError_t launch_setup(const KParams& p, long B, const double* Px, const double* Ax, const double* q,
                         const double* l, const double* u, hipStream_t st);
 hipError_t launch_update(const KParams& p, long B, const double* q, const double* l, const double* u,

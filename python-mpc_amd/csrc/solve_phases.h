@@ -34,12 +34,37 @@ __device__ __forceinline__ double rho_of(signed char t, double rho) {
     return t < 0 ? RHO_MIN : (t > 0 ? RHO_EQ_OVER_RHO_INEQ * rho : rho);
 }
 
+// v[j] for a uniform j in [0, 16) without demoting v to scratch (a register array
+// indexed by a runtime value would be): a scalar switch
+__device__ __forceinline__ double pick16(const double (&v)[16], int j) {
+    switch (j) {
+#define C(k) case k: return v[k];
+        C(0) C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8) C(9) C(10) C(11) C(12) C(13) C(14)
+#undef C
+        default: return v[15];
+    }
+}
+__device__ __forceinline__ void put16(double (&v)[16], int j, double x) {
+    switch (j) {
+#define C(k) case k: v[k] = x; break;
+        C(0) C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8) C(9) C(10) C(11) C(12) C(13) C(14)
+#undef C
+        default: v[15] = x;
+    }
+}
+
 // Gauss-Jordan inverse of the SPD tile T (32 x 32 in LDS) by ONE wave, in place, with a
 // copy to Sgk.  Lane (i, h) = (lane % 32, lane / 32) keeps row i, columns [16 h, 16 h + 16)
 // in registers.  The in-place Gauss-Jordan matrix of a symmetric input stays symmetric up
 // to sign -- M_ij = -M_ji exactly when one of i, j is already pivoted -- so row p is
 // published by the lanes that hold column p (one ds_write_b64 per lane and pivot) and the
 // 32 pivots need no workgroup barrier.  buf: 2 S doubles.  False on a non-positive pivot.
+//
+// Compact = false: the pivot loop is unrolled (static register indices, fastest; the
+// wave kernels can afford its ~200 VGPRs).  Compact = true: a rolled loop whose pivot
+// slot is picked with scalar switches (~90 VGPRs), for the 256-thread kernels, where
+// the unrolled form costs occupancy in every other phase.
+template <bool Compact>
 __device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restrict__ buf, double* __restrict__ Sgk) {
     const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
     double v[16];
@@ -49,29 +74,34 @@ __device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restri
         v[jj] = t2.x;
         v[jj + 1] = t2.y;
     }
-    bool ok = true;
-#pragma unroll
-    for (int p = 0; p < S; ++p) {
-        double* rb = buf + (p & 1) * S;
-        if (h == (p >> 4)) rb[i] = i < p ? -v[p & 15] : v[p & 15];  // row p = +-column p
+    double minpiv = 1.0;  // -1 once a pivot is not positive (NaN-safe running flag)
+    auto pivot = [&](const int p, const int pj) __attribute__((always_inline)) {
+        const int ph = p >> 4;
+        double* rb = buf + (pj & 1) * S;
+        if (h == ph) {
+            const double vp = Compact ? pick16(v, pj) : v[pj];
+            rb[i] = i < p ? -vp : vp;  // row p = +-column p
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         double rowv[16];
 #pragma unroll
         for (int jj = 0; jj < 16; jj += 2) {
-            const double2 t2 = *(const double2*)(rb + 16 * h + jj);
-            rowv[jj] = t2.x;
-            rowv[jj + 1] = t2.y;
+            const double2 r2 = *(const double2*)(rb + 16 * h + jj);
+            rowv[jj] = r2.x;
+            rowv[jj + 1] = r2.y;
         }
         const double piv = rb[p];
         const double mi = rb[i];
         const double colv = i < p ? -mi : mi;  // M_ip
-        ok = ok && piv > 0.0;
+        minpiv = piv > 0.0 ? minpiv : -1.0;
         // 1 / piv: hardware reciprocal and two Newton steps (full double precision)
         double d = __builtin_amdgcn_rcp(piv);
         d = __builtin_fma(d, __builtin_fma(-piv, d, 1.0), d);
         d = __builtin_fma(d, __builtin_fma(-piv, d, 1.0), d);
+        // row update: the pivot row becomes row_p / piv, every other row loses M_ip / piv
+        // times row_p (measured: this form beats a branch-free keep * v - cd * row_p)
         if (i == p) {
 #pragma unroll
             for (int jj = 0; jj < 16; ++jj) v[jj] = rowv[jj] * d;
@@ -80,14 +110,24 @@ __device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restri
 #pragma unroll
             for (int jj = 0; jj < 16; ++jj) v[jj] = __builtin_fma(-cd, rowv[jj], v[jj]);
         }
-        if (h == (p >> 4)) v[p & 15] = i == p ? d : -colv * d;
+        if (h == ph) {
+            if (Compact) put16(v, pj, i == p ? d : -colv * d);
+            else v[pj] = i == p ? d : -colv * d;
+        }
+    };
+    if constexpr (Compact) {
+#pragma unroll 1
+        for (int p = 0; p < S; ++p) pivot(p, __builtin_amdgcn_readfirstlane(p & 15));
+    } else {
+#pragma unroll
+        for (int p = 0; p < S; ++p) pivot(p, p & 15);
     }
 #pragma unroll
     for (int jj = 0; jj < 16; jj += 2) {
         *(double2*)(T + i * S + 16 * h + jj) = make_double2(v[jj], v[jj + 1]);
         *(double2*)(Sgk + i * S + 16 * h + jj) = make_double2(v[jj], v[jj + 1]);
     }
-    return ok;
+    return minpiv > 0.0;
 }
 
 // Assemble K's tiles for the current rho and factor them (block LDL'):
@@ -127,39 +167,19 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
         __syncthreads();
         if (tid < S) DK[tid * S + tid] = p.pad_var[k * S + tid] >= 0 ? p.sigma : 1.0;
         __syncthreads();
-        // every target has one owner: its terms are summed in plan order.  Four targets
-        // per thread and pass, so that their term loads (the ELL plan in global memory,
-        // L2-resident) are in flight together.
-        {
-            const int t_beg = p.asm_blk_ptr[k], t_end = p.asm_blk_ptr[k + 1];
-            const int2 zt = make_int2(p.nnzA | (p.nnzA << 16), 0);
+        // every target has one owner: its terms are summed in plan order
 #pragma unroll 1
-            for (int t0 = t_beg + tid; t0 < t_end; t0 += 4 * TT) {
-                double acc[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 2
-                for (int j = 0; j < tmax; ++j) {
-                    int2 w[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int t = t0 + u * TT;
-                        w[u] = t < t_end ? tt[(long)j * ntgt + t] : zt;
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int a = w[u].x & 0xFFFF, bb = (int)((unsigned)w[u].x >> 16), r = w[u].y;
-                        acc[u] += r < 0 ? L.Pv[a] : rho_of(L.ct[r], rho) * L.Acsc[a] * L.Acsc[bb];
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int t = t0 + u * TT;
-                    if (t < t_end) {
-                        const int tg = p.asm_tgt[t];
-                        if (tg < SS) DK[tg] += acc[u];
-                        else EK[tg - SS] += acc[u];
-                    }
-                }
+        for (int t = p.asm_blk_ptr[k] + tid; t < p.asm_blk_ptr[k + 1]; t += TT) {
+            double acc = 0.0;
+#pragma unroll 4
+            for (int j = 0; j < tmax; ++j) {
+                const int2 w = tt[(long)j * ntgt + t];
+                const int a = w.x & 0xFFFF, bb = (int)((unsigned)w.x >> 16), r = w.y;
+                acc += r < 0 ? L.Pv[a] : rho_of(L.ct[r], rho) * L.Acsc[a] * L.Acsc[bb];
             }
+            const int tg = p.asm_tgt[t];
+            if (tg < SS) DK[tg] += acc;
+            else EK[tg - SS] += acc;
         }
         __syncthreads();
         FPH(8)
@@ -215,7 +235,7 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
             // one wave inverts the tile (no barrier per pivot); the verdict goes through LDS
             double* okslot = EK + 2 * S;
             if (tid < 64) {
-                const bool okw = gj_wave(DK, EK, Sg + (long)k * SS);
+                const bool okw = gj_wave<(TT > 128)>(DK, EK, Sg + (long)k * SS);
                 if (tid == 0) okslot[0] = okw ? 1.0 : 0.0;
             }
             __syncthreads();

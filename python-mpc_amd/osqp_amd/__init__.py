@@ -96,6 +96,15 @@ def lib():
         raise ImportError(
             f"{LIB_PATH} not found: build the HIP extension first "
             "(python -c 'import __graft_entry__ as g; g.build()')")
+    # One HIP runtime per process: torch wheels ship their own libamdhip64 (same soname
+    # as /opt/rocm's).  Loaded first, torch's copy also satisfies libmpcqp.so's
+    # dependency; loaded the other way round the process ends up with two runtimes and
+    # torch.cuda sees no device.  Device tensors are handed to the C ABI (DeviceBatch,
+    # mpc_device), so torch goes first whenever it is installed.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     i32p, dp, vp = _P(C.c_int32), _P(C.c_double), C.c_void_p
     hp = _P(C.c_void_p)
@@ -389,6 +398,10 @@ class DeviceBatch:
     ``data_ptr()`` to contiguous float64 / int32 device memory on `device`
     (e.g. torch tensors); this module never touches their contents.
     P, A give the shared pattern (canonicalised like osqp-python; values ignored).
+    ``stream``: a hipStream_t (int or c_void_p); None = the handle's own stream, which
+    is NOT ordered with torch's legacy default stream -- callers mixing torch kernels
+    and these calls pass a non-default torch stream's ``cuda_stream`` (see
+    mpc_device.DynamicMPC) or synchronise in between.
     """
 
     def __init__(self, P, A, B, device=0, **settings):

@@ -1,0 +1,269 @@
+"""Device-resident MPC data path around the solver.
+
+The reference's incremental dynamic-bicycle MPC (Control/MPC/mpc_dynamics.py:main)
+does, per control step and in Python:
+
+  Xr = reference_search(path_x, path_y, pred_x~, dt, N)            :44-90   (F3)
+  Ad_k, Bd_k, gd_k = vehicle.get_dynamics_model(pred_x~[:, k])      vehicle_models.py:52-340 (F2)
+  pred_x~, pred_du = mpc_increment(Ad, Bd, gd, x~, Xr, ...)         :281-432 (F1 + the solve)
+  plant step + horizon shift                                        :578-617 (F3)
+
+This module runs the same steps for B vehicles at once on the MI355X through the
+C ABI of include/mpcqp.h (mpcqp_linearise_device, mpcqp_incr_*,
+mpcqp_reference_search_device) and the batched solver (DeviceBatch).  Arrays are
+torch tensors on the device; nothing is copied to the host inside a step.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import scipy.sparse as sparse
+
+from . import DeviceBatch, _check, lib
+
+_P = C.POINTER
+vp = C.c_void_p
+
+
+class Vehicle(C.Structure):
+    """Vehicle_Dynamics.__init__ arguments (vehicle_models.py:27-50); dt as in mpc_dynamics.main (0.05)."""
+    _fields_ = [(k, C.c_double) for k in ("m", "l_f", "l_r", "width", "length", "C_d", "A_f", "C_roll", "dt")]
+
+    def __init__(self, m=1300, l_f=1.25, l_r=1.40, width=1.78, length=4.25, C_d=0.34, A_f=2.0, C_roll=0.015,
+                 dt=0.05):
+        super().__init__(m, l_f, l_r, width, length, C_d, A_f, C_roll, dt)
+
+
+# structural nonzeros of get_dynamics_model's Ad = I + dt Ac and Bd = dt Bc (vehicle_models.py:273-292)
+DYN_MASK_A = np.eye(6, dtype=np.uint8)
+for _i, _j in [(0, 2), (0, 3), (0, 4), (1, 2), (1, 3), (1, 4), (2, 5), (3, 3), (3, 4), (3, 5), (4, 3), (4, 4),
+               (4, 5), (5, 3), (5, 4), (5, 5)]:
+    DYN_MASK_A[_i, _j] = 1
+DYN_MASK_B = np.zeros((6, 2), np.uint8)
+DYN_MASK_B[3:, :] = 1
+
+
+def _bind():
+    L = lib()
+    if getattr(L, "_mpc_bound", False):
+        return L
+    i64, i32, d = C.c_int64, C.c_int32, C.c_double
+    L.mpcqp_linearise_device.argtypes = [_P(Vehicle), i64, i32, vp, i64, i64, vp, i64, i64, vp, vp, vp, i32, vp]
+    L.mpcqp_incr_layout_create.argtypes = [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, _P(vp)]
+    L.mpcqp_incr_layout_dims.argtypes = [vp, _P(i32), _P(i32), _P(i32), _P(i32)]
+    L.mpcqp_incr_layout_pattern.argtypes = [vp] * 9
+    L.mpcqp_incr_assemble_device.argtypes = [vp, i64] + [vp] * 10
+    L.mpcqp_incr_layout_free.argtypes = [vp]
+    L.mpcqp_incr_layout_free.restype = None
+    L.mpcqp_reference_search_device.argtypes = [i64, i32, i32, i32, vp, vp, vp, d, vp, i32, vp]
+    L.mpcqp_incr_shift_device.argtypes = [vp, _P(Vehicle), i64, vp, vp, vp, vp, vp, vp, vp, vp]
+    L._mpc_bound = True
+    return L
+
+
+def _p(t):
+    return C.c_void_p(t.data_ptr())
+
+
+def _np_ptr(a):
+    return C.c_void_p(a.ctypes.data)
+
+
+def _stream(torch, device):
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def linearise(veh: Vehicle, x, u, device=0):
+    """Batched Vehicle_Dynamics.get_dynamics_model (F2).
+
+    x: (B, N, 6) or (B, 6) float64 device tensor, u: (B, N, 2) or (B, 2) (any strides
+    with a contiguous last dimension) -> Ad (B, N, 6, 6), Bd (B, N, 6, 2), gd (B, N, 6)
+    (N axis dropped for 2-D inputs).  Inputs are not modified (the reference's
+    low-speed guard writes into the caller's view; here it acts on copies)."""
+    import torch
+    L = _bind()
+    squeeze = x.dim() == 2
+    if squeeze:
+        x, u = x[:, None, :], u[:, None, :]
+    B, N = x.shape[0], x.shape[1]
+    if x.shape[2] != 6 or u.shape[2] != 2 or u.shape[:2] != x.shape[:2]:
+        raise ValueError("x must be (B, N, 6) and u (B, N, 2)")
+    if x.stride(2) != 1 or u.stride(2) != 1:
+        raise ValueError("the state / input axis must be contiguous")
+    kw = dict(dtype=torch.float64, device=x.device)
+    Ad = torch.empty((B, N, 6, 6), **kw); Bd = torch.empty((B, N, 6, 2), **kw); gd = torch.empty((B, N, 6), **kw)
+    _check(L.mpcqp_linearise_device(C.byref(veh), B, N, _p(x), x.stride(0), x.stride(1), _p(u), u.stride(0),
+                                    u.stride(1), _p(Ad), _p(Bd), _p(gd), x.device.index or 0,
+                                    _stream(torch, x.device)), "linearise")
+    if squeeze:
+        return Ad[:, 0], Bd[:, 0], gd[:, 0]
+    return Ad, Bd, gd
+
+
+class IncrementalLayout:
+    """The QP of mpc_increment (mpc_dynamics.py:281-389) for a batch sharing N, weights,
+    bounds and the structural nonzeros of Ad / Bd (F1).  ``pattern()`` gives the CSC
+    templates (P with its values, A), ``assemble()`` the per-instance values on the device."""
+
+    def __init__(self, N, Q, QN, R, xmin_t, xmax_t, dumin, dumax, maskA=DYN_MASK_A, maskB=DYN_MASK_B, device=0):
+        L = _bind()
+        Q = np.ascontiguousarray(np.asarray(sparse.csr_matrix(Q).todense(), np.float64))
+        QN = np.ascontiguousarray(np.asarray(sparse.csr_matrix(QN).todense(), np.float64))
+        R = np.ascontiguousarray(np.asarray(sparse.csr_matrix(R).todense(), np.float64))
+        self.N, self.nx, self.nu = int(N), Q.shape[0], R.shape[0]
+        self.nxa = self.nx + self.nu
+        arrs = [np.ascontiguousarray(np.asarray(a, np.float64).ravel()) for a in (xmin_t, xmax_t, dumin, dumax)]
+        mA = np.ascontiguousarray(np.asarray(maskA, np.uint8))
+        mB = np.ascontiguousarray(np.asarray(maskB, np.uint8))
+        h = C.c_void_p()
+        _check(L.mpcqp_incr_layout_create(self.N, self.nx, self.nu, _np_ptr(Q), _np_ptr(QN), _np_ptr(R),
+                                          *(_np_ptr(a) for a in arrs), _np_ptr(mA), _np_ptr(mB), int(device),
+                                          C.byref(h)), "incr_layout_create")
+        self._h = h.value
+        self._free = L.mpcqp_incr_layout_free  # held: module globals may be gone at interpreter exit
+        self._keep = (Q, QN, R, arrs, mA, mB)
+        n, m, nP, nA = (C.c_int32() for _ in range(4))
+        _check(L.mpcqp_incr_layout_dims(self._h, C.byref(n), C.byref(m), C.byref(nP), C.byref(nA)), "dims")
+        self.n, self.m, self.nnzP, self.nnzA = n.value, m.value, nP.value, nA.value
+        self.device = int(device)
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            self._free(h)
+
+    def pattern(self):
+        """(P, A, l_template, u_template): scipy CSC templates (P upper triangle with its
+        constant values; A with the constant entries and zeros at the stage entries) and
+        the inequality-row bounds (clipped to +-1e30; equality rows 0)."""
+        n, m = self.n, self.m
+        Pp = np.zeros(n + 1, np.int32); Pi = np.zeros(self.nnzP, np.int32); Px = np.zeros(self.nnzP)
+        Ap = np.zeros(n + 1, np.int32); Ai = np.zeros(self.nnzA, np.int32); At = np.zeros(self.nnzA)
+        lt = np.zeros(m); ut = np.zeros(m)
+        _check(lib().mpcqp_incr_layout_pattern(self._h, *(_np_ptr(a) for a in (Pp, Pi, Px, Ap, Ai, At, lt, ut))),
+               "pattern")
+        P = sparse.csc_matrix((Px, Pi, Pp), shape=(n, n))
+        A = sparse.csc_matrix((At, Ai, Ap), shape=(m, n))
+        return P, A, lt, ut
+
+    def assemble(self, Ad, Bd, gd, xt0, Xr, out=None):
+        """Ad (B,N,nx,nx), Bd (B,N,nx,nu), gd (B,N,nx), xt0 (B,nx+nu), Xr (B,nx,N+1), all
+        contiguous float64 device tensors -> (Ax, q, l, u) in the layout's pattern order."""
+        import torch
+        B = Ad.shape[0]
+        if out is None:
+            kw = dict(dtype=torch.float64, device=Ad.device)
+            out = (torch.empty((B, self.nnzA), **kw), torch.empty((B, self.n), **kw),
+                   torch.empty((B, self.m), **kw), torch.empty((B, self.m), **kw))
+        for t in (Ad, Bd, gd, xt0, Xr):
+            if not t.is_contiguous() or t.dtype != torch.float64:
+                raise ValueError("assemble inputs must be contiguous float64 tensors")
+        Ax, q, l, u = out
+        _check(lib().mpcqp_incr_assemble_device(self._h, B, _p(Ad), _p(Bd), _p(gd), _p(xt0), _p(Xr), _p(Ax), _p(q),
+                                                _p(l), _p(u), _stream(torch, Ad.device)), "incr_assemble")
+        return out
+
+
+def reference_search(path_x, path_y, pred, dt):
+    """reference_search (mpc_dynamics.py:44-90) per vehicle: pred (B, N+1, nxa) device tensor
+    of predicted augmented states -> Xr (B, 6, N+1)."""
+    import torch
+    L = _bind()
+    B, N1, nxa = pred.shape
+    Xr = torch.empty((B, 6, N1), dtype=torch.float64, device=pred.device)
+    _check(L.mpcqp_reference_search_device(B, N1 - 1, nxa, path_x.numel(), _p(path_x), _p(path_y), _p(pred),
+                                           float(dt), _p(Xr), pred.device.index or 0, _stream(torch, pred.device)),
+           "reference_search")
+    return Xr
+
+
+class DynamicMPC:
+    """B copies of mpc_dynamics.main's closed loop (:437-617), every step on the device.
+
+    State per vehicle: x~ = (X, Y, yaw, vx, vy, r, steer, accel), the predicted
+    horizon pred_x~ (N+1 stages) and pred_du.  ``step()`` = reference search ->
+    linearisation of every predicted stage -> mpc_increment's QP -> batched OSQP
+    solve (settings of :393: polish off, warm_start off) -> plant step and shift."""
+
+    Q = np.diag([100.0, 100.0, 100.0, 50.0, 50.0, 50.0])          # :456-458
+    QN = np.diag([1000.0, 1000.0, 1000.0, 500.0, 500.0, 500.0])
+    R = np.diag([50.0, 50.0])
+    DUMIN = np.array([-np.deg2rad(2.0), -0.5])                      # :461-464
+    XMIN_T = np.array([-np.inf, -np.inf, -2 * np.pi, -100., -30., -0.5 * np.pi, -np.deg2rad(15), -3.])
+    XMAX_T = np.array([np.inf, np.inf, 2 * np.pi, 100., 30., 0.5 * np.pi, np.deg2rad(15), 1.])
+
+    def __init__(self, x0, u0, path_x, path_y, N=30, veh: Vehicle | None = None, device=0, **solver_settings):
+        import torch
+        self.torch = torch
+        self.dev = torch.device("cuda", device)
+        self.veh = veh or Vehicle()
+        self.N = int(N)
+        x0 = np.atleast_2d(np.asarray(x0, np.float64)); u0 = np.atleast_2d(np.asarray(u0, np.float64))
+        self.B = x0.shape[0]
+        self.layout = IncrementalLayout(self.N, self.Q, self.QN, self.R, self.XMIN_T, self.XMAX_T, self.DUMIN,
+                                        -self.DUMIN, device=device)
+        P, A, _, _ = self.layout.pattern()
+        settings = dict(verbose=False, polish=False, warm_start=False)   # mpc_dynamics.py:393
+        settings.update(solver_settings)
+        settings.pop("verbose", None)
+        self.solver = DeviceBatch(P, A, self.B, device=device, **settings)
+        kw = dict(dtype=torch.float64, device=self.dev)
+        self.Px = torch.from_numpy(np.tile(P.data, (self.B, 1))).to(**kw).contiguous()
+        self.path_x = torch.as_tensor(np.asarray(path_x, np.float64), **kw).contiguous()
+        self.path_y = torch.as_tensor(np.asarray(path_y, np.float64), **kw).contiguous()
+        self.xt = torch.from_numpy(np.concatenate([x0, u0], axis=1)).to(**kw).contiguous()
+        n, m = self.layout.n, self.layout.m
+        self.sol = torch.empty((self.B, n), **kw)
+        self.y = torch.empty((self.B, m), **kw)
+        self.status = torch.empty(self.B, dtype=torch.int32, device=self.dev)
+        self.iters = torch.empty(self.B, dtype=torch.int32, device=self.dev)
+        self.pdu = torch.zeros((self.B, self.N + 1, 2), **kw)
+        # every kernel of a step runs on this stream, in order; a null (legacy default)
+        # torch stream would be passed as NULL, which the solver's C ABI reads as "the
+        # handle's own stream" -- unordered with torch's kernels
+        self.stream = torch.cuda.Stream(self.dev)
+        self.stream.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(self.stream):
+            self.pred = self._initial_rollout()
+        torch.cuda.current_stream(self.dev).wait_stream(self.stream)
+
+    def _initial_rollout(self):
+        """Initial guess (:513-522): roll the linearised model forward with zero increments."""
+        torch = self.torch
+        pred = torch.empty((self.B, self.N + 1, 8), dtype=torch.float64, device=self.dev)
+        pred[:, 0] = self.xt
+        xk = self.xt.clone()
+        for i in range(self.N):
+            Ad, Bd, gd = linearise(self.veh, xk[:, :6].contiguous(), xk[:, 6:].contiguous(), self.dev.index or 0)
+            x1 = torch.einsum("bij,bj->bi", Ad, xk[:, :6]) + torch.einsum("bij,bj->bi", Bd, xk[:, 6:]) + gd
+            xk = torch.cat([x1, xk[:, 6:] + self.pdu[:, i]], dim=1)
+            pred[:, i + 1] = xk
+        return pred
+
+    def step(self):
+        """One receding-horizon step for every vehicle; returns (status, iters) device tensors.
+        Asynchronous: ordered after the caller's current stream, and the caller's stream
+        is ordered after the step."""
+        torch = self.torch
+        caller = torch.cuda.current_stream(self.dev)
+        self.stream.wait_stream(caller)
+        with torch.cuda.stream(self.stream):
+            out = self._step()
+        caller.wait_stream(self.stream)
+        return out
+
+    def _step(self):
+        L = _bind()
+        torch = self.torch
+        Xr = reference_search(self.path_x, self.path_y, self.pred, self.veh.dt)
+        Ad, Bd, gd = linearise(self.veh, self.pred[:, :self.N, :6], self.pred[:, :self.N, 6:], self.dev.index or 0)
+        Ax, q, l, u = self.layout.assemble(Ad, Bd, gd, self.xt, Xr)
+        st = _stream(torch, self.dev)  # self.stream
+        self.solver.setup(self.Px, Ax, q, l, u, stream=st)
+        self.solver.solve(self.sol, self.y, self.status, self.iters, stream=st)
+        _check(L.mpcqp_incr_shift_device(self.layout._h, C.byref(self.veh), self.B, _p(self.sol), _p(Ad), _p(Bd),
+                                         _p(gd), _p(self.xt), _p(self.pred), _p(self.pdu),
+                                         _stream(torch, self.dev)), "incr_shift")
+        self.last = dict(Ad=Ad, Bd=Bd, gd=gd, Xr=Xr, Ax=Ax, q=q, l=l, u=u)
+        return self.status, self.iters

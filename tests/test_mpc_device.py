@@ -1,0 +1,250 @@
+"""Device MPC data path (csrc/mpc_device.hip) against host
+restatements of the reference's steps and the reference's own fixtures.
+
+  F2  linearise        vs tests/golden/linearise.npz (Vehicle_Dynamics.get_dynamics_model)
+  F1  incr assembly    vs tests/golden/dyn_incr_n50.npz (mpc_increment's P, q, A, l, u)
+  F3  reference search vs the restatement below of mpc_dynamics.py:30-90
+      closed loop      each step decomposed: device Xr / Ad / QP / solution / shifted
+                       horizon vs the host restatement of mpc_dynamics.main (:506-617)
+                       fed the device's own state, with the solve checked against the
+                       CPU oracle on the host-built QP.
+
+The pattern test runs on CPU (layout creation is host-only); the rest needs the GPU.
+"""
+import numpy as np
+import pytest
+
+from osqp_amd import canonical_data, mpc
+from osqp_amd.mpc_device import DYN_MASK_A, DYN_MASK_B, IncrementalLayout
+
+INF = 1e30  # OSQP_INFTY: bounds are clipped to it (osqp 0.6 osqp_setup / update_bounds)
+
+
+def dense(M):
+    return np.asarray(M.todense())
+
+
+def _layout(N, **kw):
+    return IncrementalLayout(N, mpc.DYN_Q, mpc.DYN_QN, mpc.DYN_R, mpc.DYN_XMIN_T, mpc.DYN_XMAX_T, mpc.DYN_DUMIN,
+                             -mpc.DYN_DUMIN, **kw)
+
+
+@pytest.mark.parametrize("N", [2, 3, 30, 50])
+def test_layout_pattern_matches_host_builder(N):
+    """The C layout's CSC templates equal mpc_increment's matrices (host builder, same
+    structural nonzeros) after the osqp-python canonicalisation."""
+    L = _layout(N)
+    P, A, lt, ut = L.pattern()
+    assert (L.n, L.m) == ((N + 1) * 8 + N * 2, (N + 1) * 8 + (N + 1) * 8 + N * 2)
+    P2, _, A2, l2, u2 = mpc.incremental_qp([np.where(DYN_MASK_A, 7.0, 0.0)] * N, [np.where(DYN_MASK_B, 7.0, 0.0)] * N,
+                                           [np.zeros(6)] * N, np.zeros(8), np.zeros((6, N + 1)), mpc.DYN_Q,
+                                           mpc.DYN_QN, mpc.DYN_R, N, mpc.DYN_XMIN_T, mpc.DYN_XMAX_T, mpc.DYN_DUMIN,
+                                           -mpc.DYN_DUMIN)
+    P2, A2 = canonical_data(P2, A2)
+    assert np.array_equal(P.indptr, P2.indptr) and np.array_equal(P.indices, P2.indices)
+    assert np.array_equal(P.data, P2.data)
+    assert np.array_equal(A.indptr, A2.indptr) and np.array_equal(A.indices, A2.indices)
+    const = A2.data != 7.0
+    assert np.array_equal(A.data[const], A2.data[const]) and not A.data[~const].any()
+    ineq = slice((N + 1) * 8, None)
+    assert np.array_equal(lt[ineq], np.clip(l2[ineq], -INF, INF))
+    assert np.array_equal(ut[ineq], np.clip(u2[ineq], -INF, INF))
+
+
+def test_layout_rejects_bad_arguments():
+    for N in (0, 1):
+        with pytest.raises(Exception):
+            _layout(N)
+    with pytest.raises(Exception):
+        IncrementalLayout(10, mpc.DYN_Q, mpc.DYN_QN, mpc.DYN_R, mpc.DYN_XMIN_T, mpc.DYN_XMAX_T, mpc.DYN_DUMIN,
+                          mpc.DYN_DUMIN - 1.0)  # dumin > dumax
+
+
+# ------------------------------------------------------------------ host restatements --
+def nearest_point(path_x, path_y, x, y, look_ind=0):
+    """mpc_dynamics.py:30-41 (reversed scan, strict <)."""
+    min_d, min_ind = np.inf, -1
+    for i in reversed(range(len(path_x))):
+        d = np.sqrt((path_x[i] - x) ** 2 + (path_y[i] - y) ** 2)
+        if d < min_d:
+            min_d, min_ind = d, i
+    return min_ind + look_ind
+
+
+def reference_search(path_x, path_y, pred_state, dt, N):
+    """mpc_dynamics.py:44-90: pred_state (6, N+1) -> Xr (6, N+1)."""
+    x_ref = np.zeros((6, N + 1))
+    cumul_d = 0.0
+    ind = nearest_point(path_x, path_y, pred_state[0, 0], pred_state[1, 0], look_ind=1)
+    path_d = np.sqrt((path_x[ind + 1] - path_x[ind]) ** 2 + (path_y[ind + 1] - path_y[ind]) ** 2)
+    for i in range(N + 1):
+        cumul_d = cumul_d + abs(pred_state[3, i]) * dt
+        while cumul_d >= path_d:
+            ind = ind + 1
+            path_d = path_d + np.sqrt((path_x[ind + 1] - path_x[ind]) ** 2 + (path_y[ind + 1] - path_y[ind]) ** 2)
+        x_ref[0, i], x_ref[1, i], x_ref[3, i] = path_x[ind], path_y[ind], 10.0
+    return x_ref
+
+
+def path():
+    """mpc_dynamics.main's path (:468-469): 200 points on y = 0.5 x + 5."""
+    px = np.linspace(-10, 100, 200)
+    return px, px * 0.5 + 5
+
+
+def shift(sol, Ad0, Bd0, gd0, xt, veh, N):
+    """Plant step + horizon shift of mpc_dynamics.main (:578-617) with the solution
+    unpacked as in mpc_increment (:405-432).  The terminal Euler step
+    (update_dynamics_model) is x + dt f(x, u), written here as Ad x + Bd u + gd of the
+    linearisation at the same point (equal up to rounding)."""
+    nx, nu, nxa = 6, 2, 8
+    S = sol[:(N + 1) * nxa].reshape(N + 1, nxa)          # pred_x~ (stage-major)
+    D = sol[(N + 1) * nxa:].reshape(N, nu)                # del_u
+    u = xt[nx:] + D[0]
+    x = Ad0 @ xt[:nx] + Bd0 @ u + gd0
+    xt_new = np.concatenate([x, u])
+    pred = np.empty((N + 1, nxa)); pdu = np.empty((N + 1, nu))
+    pred[0] = xt_new
+    pred[1:N] = S[2:N + 1]
+    pdu[0:N - 1] = D[1:N]
+    pdu[N - 1] = D[N - 1]
+    Ae, Be, ge = mpc.linearise_dynamics(veh, S[N, :nx][None], S[N - 1, nx:][None])
+    pred[N, :nx] = Ae[0] @ S[N, :nx] + Be[0] @ S[N - 1, nx:] + ge[0]
+    pred[N, nx:] = pred[N - 1, nx:]
+    pdu[N] = pdu[N - 1]
+    return xt_new, pred, pdu
+
+
+# ------------------------------------------------------------------------- GPU tests --
+@pytest.mark.gpu
+def test_linearise_matches_reference_fixture(golden):
+    import torch
+    from osqp_amd.mpc_device import Vehicle, linearise
+    g = golden("linearise.npz")
+    x = torch.tensor(g["x"], device="cuda"); u = torch.tensor(g["u"], device="cuda")
+    x0, u0 = x.clone(), u.clone()
+    Ad, Bd, gd = linearise(Vehicle(dt=float(g["dt"])), x, u)
+    assert torch.equal(x, x0) and torch.equal(u, u0)  # the guard acts on copies
+    assert np.allclose(Ad.cpu().numpy(), g["Ad"], rtol=1e-13, atol=1e-15)
+    assert np.allclose(Bd.cpu().numpy(), g["Bd"], rtol=1e-13, atol=1e-15)
+    assert np.allclose(gd.cpu().numpy(), g["gd"], rtol=1e-12, atol=1e-13)
+    # horizon-shaped input with a strided view: (B, N, 6) taken from (B, N, 8)
+    xt = torch.cat([x, u], dim=1).reshape(6, 8, 8)
+    Ad3, Bd3, gd3 = linearise(Vehicle(dt=float(g["dt"])), xt[..., :6], xt[..., 6:])
+    assert torch.equal(Ad3.reshape(48, 6, 6), Ad) and torch.equal(gd3.reshape(48, 6), gd)
+
+
+@pytest.mark.gpu
+def test_incremental_assembly_matches_reference_fixture(golden):
+    import torch
+    g = golden("dyn_incr_n50.npz")
+    L = IncrementalLayout(50, g["Q"], g["QN"], g["R"], g["xmin_t"], g["xmax_t"], g["del_umin"], g["del_umax"])
+    P, A, _, _ = L.pattern()
+    T = g["q"].shape[0]
+    dev = lambda a: torch.tensor(np.ascontiguousarray(a), dtype=torch.float64, device="cuda")
+    Ax, q, l, u = L.assemble(dev(g["Ad"]), dev(g["Bd"]), dev(g["gd"][..., 0]), dev(g["xt0"]), dev(g["Xr"]))
+    Ax, q, l, u = (t.cpu().numpy() for t in (Ax, q, l, u))
+    for t in range(T):
+        Pr = g["P"].copy(); Pr.data = g["Px"][t]
+        Ar = g["A"].copy(); Ar.data = g["Ax"][t]
+        A.data = Ax[t]
+        assert np.array_equal(dense(P), dense(Pr))
+        assert np.allclose(dense(A), dense(Ar), rtol=1e-15, atol=0)
+        assert np.allclose(q[t], g["q"][t], rtol=1e-15, atol=0)
+        assert np.array_equal(l[t], np.clip(g["l"][t], -INF, INF))
+        assert np.array_equal(u[t], np.clip(g["u"][t], -INF, INF))
+
+
+@pytest.mark.gpu
+def test_reference_search_matches_restatement():
+    import torch
+    from osqp_amd.mpc_device import reference_search as dev_search
+    px, py = path()
+    rng = np.random.default_rng(3)
+    B, N, dt = 64, 30, 0.05
+    pred = np.zeros((B, N + 1, 8))
+    s0 = rng.uniform(-5, 60, B)
+    pred[:, :, 0] = s0[:, None] + rng.normal(0, 1, (B, 1))
+    pred[:, :, 1] = 0.5 * s0[:, None] + 5 + rng.normal(0, 3, (B, 1))
+    pred[:, :, 3] = rng.uniform(0, 30, (B, N + 1))
+    pred[:B // 4, :, 3] *= -1  # reversing: |vx| is used
+    Xr = dev_search(torch.tensor(px, device="cuda"), torch.tensor(py, device="cuda"),
+                    torch.tensor(pred, device="cuda"), dt).cpu().numpy()
+    for b in range(B):
+        assert np.array_equal(Xr[b], reference_search(px, py, pred[b].T[:6], dt, N)), b
+
+
+@pytest.mark.gpu
+def test_reference_search_clamps_at_path_end():
+    """Where the reference raises IndexError (its index reaches the last path point), the
+    kernel holds the start of the last segment."""
+    import torch
+    from osqp_amd.mpc_device import reference_search as dev_search
+    px, py = path()
+    pred = np.zeros((1, 11, 8)); pred[0, :, 0] = 99.0; pred[0, :, 1] = 54.5; pred[0, :, 3] = 40.0
+    Xr = dev_search(torch.tensor(px, device="cuda"), torch.tensor(py, device="cuda"),
+                    torch.tensor(pred, device="cuda"), 0.05).cpu().numpy()
+    assert np.all(Xr[0, 0] == px[-2]) and np.all(Xr[0, 1] == py[-2])
+
+
+@pytest.mark.gpu
+def test_closed_loop_matches_host_restatement():
+    import pyoracle
+    import torch
+    from osqp_amd.mpc_device import DynamicMPC
+    B, N, steps = 4, 30, 6
+    x0 = np.zeros((B, 6)); x0[:, 3] = 15.0
+    x0[:, 1] = [0.0, 1.0, -1.5, 0.5]; x0[:, 2] = np.deg2rad([0.0, 5.0, -3.0, 10.0])
+    u0 = np.zeros((B, 2))
+    px, py = path()
+    ctl = DynamicMPC(x0, u0, px, py, N=N)
+    veh = mpc.VehicleParams(dt=0.05)
+    # initial guess (:513-522)
+    xk = np.concatenate([x0, u0], 1)
+    pred0 = [xk]
+    for i in range(N):
+        Ad, Bd, gd = mpc.linearise_dynamics(veh, xk[:, :6], xk[:, 6:])
+        xk = np.concatenate([np.einsum("bij,bj->bi", Ad, xk[:, :6]) + np.einsum("bij,bj->bi", Bd, xk[:, 6:]) + gd,
+                             xk[:, 6:]], 1)
+        pred0.append(xk)
+    assert np.allclose(ctl.pred.cpu().numpy(), np.stack(pred0, 1), rtol=1e-12, atol=1e-12)
+    Apat = ctl.layout.pattern()[1]
+    n_iter_match = 0
+    for step in range(steps):
+        xt, pred = ctl.xt.cpu().numpy(), ctl.pred.cpu().numpy()
+        status, iters = ctl.step()
+        status, iters = status.cpu().numpy(), iters.cpu().numpy()
+        last = {k: v.cpu().numpy() for k, v in ctl.last.items()}
+        sol = ctl.sol.cpu().numpy()
+        for b in range(B):
+            Xr = reference_search(px, py, pred[b].T[:6], 0.05, N)
+            assert np.array_equal(last["Xr"][b], Xr)
+            Ad, Bd, gd = mpc.linearise_dynamics(veh, pred[b, :N, :6], pred[b, :N, 6:])
+            assert np.allclose(last["Ad"][b], Ad, rtol=1e-13, atol=1e-15)
+            assert np.allclose(last["gd"][b], gd, rtol=1e-12, atol=1e-13)
+            P, q, A, l, u = mpc.incremental_qp(list(Ad), list(Bd), list(gd), xt[b], Xr, mpc.DYN_Q, mpc.DYN_QN,
+                                               mpc.DYN_R, N, mpc.DYN_XMIN_T, mpc.DYN_XMAX_T, mpc.DYN_DUMIN,
+                                               -mpc.DYN_DUMIN)
+            A_dev = Apat.copy(); A_dev.data = last["Ax"][b]
+            assert np.allclose(dense(A_dev), dense(A), rtol=1e-12, atol=1e-15)
+            assert np.allclose(last["q"][b], q, rtol=1e-12, atol=1e-12)
+            assert np.allclose(last["l"][b], np.clip(l, -INF, INF), rtol=1e-12, atol=1e-14)
+            o = pyoracle.OSQP()
+            o.setup(P, q, A, l, u, polish=False, warm_start=False)
+            ro = o.solve()
+            assert status[b] == 1 and ro.info.status == "solved"
+            n_iter_match += int(iters[b] == ro.info.iter)
+            scale = max(1.0, np.abs(ro.x).max())
+            assert np.abs(sol[b] - ro.x).max() < 1e-5 * scale, (step, b)
+            du = slice((N + 1) * 8, None)
+            assert np.abs(sol[b, du] - ro.x[du]).max() < 1e-4
+            # plant step + shift from the device's own solution
+            xt_new, pred_new, pdu_new = shift(sol[b], last["Ad"][b, 0], last["Bd"][b, 0], last["gd"][b, 0], xt[b],
+                                              veh, N)
+            assert np.allclose(ctl.xt[b].cpu().numpy(), xt_new, rtol=1e-13, atol=1e-13)
+            assert np.allclose(ctl.pred[b].cpu().numpy(), pred_new, rtol=1e-10, atol=1e-10)
+            assert np.allclose(ctl.pdu[b].cpu().numpy(), pdu_new, rtol=0, atol=0)
+    assert n_iter_match >= 0.9 * B * steps
+    # the vehicles converge toward the path (lateral error shrinks)
+    xt = ctl.xt.cpu().numpy()
+    assert np.all(np.isfinite(xt))
