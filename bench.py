@@ -13,7 +13,8 @@ inputs already resident in HBM when the timed region starts.
 Multi-GPU: one process per GPU (torch.distributed.run); every rank solves its
 own batch (weak scaling, no data-path collective); timing = barrier +
 synchronize on both sides, max over ranks.  --config 3/5 select the slack /
-incremental-dynamic workloads (not the headline line).
+incremental-dynamic workloads (not the headline line); cfg 5 is warm-started as
+SURVEY.md §8d D2 prescribes (cold solve, one-stage shift, timed warm re-solve).
 
 rank 0 prints ONE JSON line with "roofline" (k_solve, HBM-bound by the
 algorithmic-bytes model of SURVEY.md §8d D3, HIP-event kernel times from the
@@ -112,9 +113,23 @@ def main():
     dit = torch.empty(B, dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
     solver = DeviceBatch(P, A, B, device=local, **settings)
+    warm = args.config == 5
+    xs = ys = None
+    if warm:
+        # SURVEY.md §8d D2, cfg 5 ("warm-started ADMM"): solve once cold, shift the solution
+        # one stage as the reference shifts its horizon (mpc_dynamics.py:589-610), and time
+        # setup + warm start from the shifted (x, y) + solve
+        from osqp_amd.mpc_device import warm_shift
+        solver.setup(dPx, dAx, dq, dl, du)
+        solver.solve(dx, dy, dst, dit)
+        solver.synchronize()
+        xs, ys = warm_shift(b["N"], 8, 2, dx, dy)
+        torch.cuda.synchronize()
 
     def step():
         solver.setup(dPx, dAx, dq, dl, du)
+        if warm:
+            solver.warm_start(xs, ys)
         solver.solve(dx, dy, dst, dit)
 
     for _ in range(args.warmup):
@@ -144,7 +159,7 @@ def main():
 
     value = world * B * args.steps / dt
     nnzP, nnzA = P.nnz, A.nnz
-    bytes_per_solve = 8 * (nnzP + nnzA + n + 2 * m) + 8 * (n + m)
+    bytes_per_solve = 8 * (nnzP + nnzA + n + 2 * m) + 8 * (n + m) + (8 * (n + m) if warm else 0)
     solve_ms = kt["solve_ms"] / max(1, kt["n_solve"])
     setup_ms = kt["setup_ms"] / max(1, kt["n_setup"])
     achieved = bytes_per_solve * B / (solve_ms * 1e-3) / 1e9
@@ -164,16 +179,20 @@ def main():
         # bounded sample: passes over the same instances until ~cpu_seconds of wall time
         nc = min(B, max(threads * 8, 64))
         done, tc, passes = 0, 0.0, 0
+        ws = {}
+        if warm:
+            ws = dict(x0=xs[:nc].cpu().numpy(), y0=ys[:nc].cpu().numpy())
         while tc < args.cpu_seconds and passes < 10000:
             t = time.perf_counter()
             rc = pyoracle.solve_batch(P, A, Px[:nc], b["q"][:nc], Ax[:nc], b["l"][:nc], b["u"][:nc],
-                                      nthreads=threads, **settings)
+                                      nthreads=threads, **ws, **settings)
             tc += time.perf_counter() - t
             done += nc
             passes += 1
         cpu = {"value": done / tc, "unit": "QP solves/s", "cores": threads, "kind": "port",
                "sample": f"{passes} passes over the first {nc} of the {B} instances ({done} solves), "
-                         f"fresh setup()+solve() each, {threads} POSIX threads, oracle/osqp_oracle.c "
+                         f"fresh setup(){'+warm_start(shifted x, y)' if warm else ''}+solve() each, "
+                         f"{threads} POSIX threads, oracle/osqp_oracle.c "
                          f"(OSQP 0.6 restatement; osqp itself is not installed on the box)",
                "seconds": round(tc, 3),
                "status_match_gpu": float(np.mean(rc.status_val == status[:nc])),
@@ -197,7 +216,8 @@ def main():
             "config": {"workload": spec["name"], "config_index": args.config, "batch_per_gpu": B,
                        "global_batch": world * B, "horizon_N": b["N"], "n": n, "m": m,
                        "nnz_triuP": nnzP, "nnz_A": nnzA, "eps_abs": 1e-3, "eps_rel": 1e-3,
-                       "step": "setup()+solve() per instance, inputs resident in HBM",
+                       "step": ("setup()+warm_start(previous solution shifted one stage)+solve()" if warm else
+                                "setup()+solve()") + " per instance, inputs resident in HBM",
                        "parallelism": f"batch-shard x{world}",
                        "iters_mean": float(iters.mean()), "iters_max": int(iters.max()),
                        "solved_frac": float(np.mean(status == 1)),

@@ -204,7 +204,8 @@ void mpcqp_incr_layout_free(mpcqp_incr_layout *L);
 /* F3 -- reference_search (mpc_dynamics.py:44-90, nearest_point :30-41) for every
  * vehicle: pred[b*(N+1)*nxa + k*nxa + 0..nxa) predicted augmented states
  * -> Xr[b*6*(N+1)] (6 rows: path x, path y, yaw 0, vx 10, vy 0, r 0).  Near the
- * path's end the index stops at the last point (the reference indexes past it). */
+ * path's end the index holds the start of the last segment (where the reference
+ * raises IndexError). */
 int mpcqp_reference_search_device(int64_t B, int32_t N, int32_t nxa, int32_t npath, const double *dpath_x,
                                   const double *dpath_y, const double *dpred, double dt, double *dXr, int32_t device,
                                   void *stream);
@@ -215,6 +216,14 @@ int mpcqp_reference_search_device(int64_t B, int32_t N, int32_t nxa, int32_t npa
 int mpcqp_incr_shift_device(const mpcqp_incr_layout *L, const mpcqp_vehicle *veh, int64_t B, const double *dsol,
                             const double *dAd, const double *dBd, const double *dgd, double *dxt, double *dpred,
                             double *dpdu, void *stream);
+/* F3 -- warm start for the next step (cfg 5): shift a solution of
+ * the incremental layout one stage forward, x[b*n], y[b*m] -> xs[b*n], ys[b*m].
+ * Variable blocks x~_0..x~_N | du_0..du_{N-1} and row blocks eq_0..eq_N |
+ * box_0..box_N | du-box_0..du-box_{N-1} each move k+1 -> k, the last one repeated
+ * (the reference's own shift of pred_x~ / pred_du, mpc_dynamics.py:589-610, applied
+ * to the primal and dual iterates).  y / ys may be NULL.  In-place is not allowed. */
+int mpcqp_incr_warm_shift_device(int64_t B, int32_t N, int32_t nxa, int32_t nu, const double *dx, const double *dy,
+                                 double *dxs, double *dys, int32_t device, void *stream);
 
 #ifdef __cplusplus
 }

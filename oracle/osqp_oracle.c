@@ -958,6 +958,7 @@ typedef struct {
     int b0, b1, n, m;
     const int *Pp, *Pi, *Ap, *Ai;
     const double *Px_b, *q_b, *Ax_b, *l_b, *u_b;
+    const double *x0_b, *y0_b;
     const orc_settings *s;
     double *x_out, *y_out;
     int *status, *iters;
@@ -977,6 +978,7 @@ static void *batch_worker(void *arg) {
             if (j->status) j->status[b] = ORC_NON_CVX;
             continue;
         }
+        if (j->x0_b && j->y0_b) orc_warm_start(w, j->x0_b + (size_t)b * j->n, j->y0_b + (size_t)b * j->m);
         orc_solve(w);
         orc_get_solution(w, j->x_out ? j->x_out + (size_t)b * j->n : NULL,
                          j->y_out ? j->y_out + (size_t)b * j->m : NULL, NULL, NULL);
@@ -991,6 +993,15 @@ int orc_solve_batch(int B, int n, int m, const int *Pp, const int *Pi, const dou
                     const double *q_b, const int *Ap, const int *Ai, const double *Ax_b,
                     const double *l_b, const double *u_b, const orc_settings *s,
                     double *x_out, double *y_out, int *status, int *iters, int nthreads) {
+    return orc_solve_batch_warm(B, n, m, Pp, Pi, Px_b, q_b, Ap, Ai, Ax_b, l_b, u_b, NULL, NULL, s, x_out, y_out,
+                                status, iters, nthreads);
+}
+
+int orc_solve_batch_warm(int B, int n, int m, const int *Pp, const int *Pi, const double *Px_b,
+                         const double *q_b, const int *Ap, const int *Ai, const double *Ax_b,
+                         const double *l_b, const double *u_b, const double *x0_b, const double *y0_b,
+                         const orc_settings *s, double *x_out, double *y_out, int *status, int *iters,
+                         int nthreads) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > B) nthreads = B > 0 ? B : 1;
     batch_job *jobs = (batch_job *)calloc(nthreads, sizeof(batch_job));
@@ -1001,6 +1012,7 @@ int orc_solve_batch(int B, int n, int m, const int *Pp, const int *Pi, const dou
         j->b1 = (int)((long long)B * (t + 1) / nthreads);
         j->n = n; j->m = m; j->Pp = Pp; j->Pi = Pi; j->Ap = Ap; j->Ai = Ai;
         j->Px_b = Px_b; j->q_b = q_b; j->Ax_b = Ax_b; j->l_b = l_b; j->u_b = u_b; j->s = s;
+        j->x0_b = x0_b; j->y0_b = y0_b;
         j->x_out = x_out; j->y_out = y_out; j->status = status; j->iters = iters;
     }
     if (nthreads == 1) {

@@ -101,6 +101,14 @@ int orc_solve_batch(int B, int n, int m,
                     const double *l_b, const double *u_b, const orc_settings *s,
                     double *x_out, double *y_out, int *status, int *iters,
                     int nthreads);
+/* Same, each instance warm-started from x0_b[b*n], y0_b[b*m] (osqp_warm_start) after
+ * its setup; NULL x0_b / y0_b = cold. */
+int orc_solve_batch_warm(int B, int n, int m,
+                         const int *Pp, const int *Pi, const double *Px_b, const double *q_b,
+                         const int *Ap, const int *Ai, const double *Ax_b,
+                         const double *l_b, const double *u_b, const double *x0_b, const double *y0_b,
+                         const orc_settings *s, double *x_out, double *y_out, int *status, int *iters,
+                         int nthreads);
 
 #ifdef __cplusplus
 }

@@ -92,12 +92,18 @@ def lib():
                                       P(C.c_double), P(C.c_double), P(_Settings),
                                       P(C.c_double), P(C.c_double), P(C.c_int), P(C.c_int),
                                       C.c_int]
+        L.orc_solve_batch_warm.argtypes = [C.c_int, C.c_int, C.c_int,
+                                           P(C.c_int), P(C.c_int), P(C.c_double), P(C.c_double),
+                                           P(C.c_int), P(C.c_int), P(C.c_double),
+                                           P(C.c_double), P(C.c_double), P(C.c_double), P(C.c_double),
+                                           P(_Settings), P(C.c_double), P(C.c_double), P(C.c_int), P(C.c_int),
+                                           C.c_int]
         _lib = L
     return _lib
 
 
 def _dp(a):
-    return a.ctypes.data_as(C.POINTER(C.c_double))
+    return None if a is None else a.ctypes.data_as(C.POINTER(C.c_double))
 
 
 def _ip(a):
@@ -199,8 +205,9 @@ class OSQP:
             self._w = C.c_void_p()
 
 
-def solve_batch(P, A, Px_b, q_b, Ax_b, l_b, u_b, nthreads=1, **settings):
-    """B fresh setup()+solve() runs with a shared pattern (values per instance)."""
+def solve_batch(P, A, Px_b, q_b, Ax_b, l_b, u_b, nthreads=1, x0=None, y0=None, **settings):
+    """B fresh setup()+solve() runs with a shared pattern (values per instance);
+    with x0 (B, n) and y0 (B, m) each instance is warm-started after its setup."""
     P, A = canon(P, A)
     n, m = P.shape[0], A.shape[0]
     B = q_b.shape[0]
@@ -212,7 +219,11 @@ def solve_batch(P, A, Px_b, q_b, Ax_b, l_b, u_b, nthreads=1, **settings):
     l_b = np.ascontiguousarray(l_b, np.float64); u_b = np.ascontiguousarray(u_b, np.float64)
     x = np.empty((B, n)); y = np.empty((B, m))
     st = np.empty(B, np.int32); it = np.empty(B, np.int32)
-    e = lib().orc_solve_batch(B, n, m, _ip(Pp), _ip(Pi), _dp(Px_b), _dp(q_b), _ip(Ap), _ip(Ai),
-                              _dp(Ax_b), _dp(l_b), _dp(u_b), C.byref(s), _dp(x), _dp(y),
-                              _ip(st), _ip(it), int(nthreads))
+    if (x0 is None) != (y0 is None):
+        raise ValueError("x0 and y0 go together")
+    if x0 is not None:
+        x0 = np.ascontiguousarray(x0, np.float64); y0 = np.ascontiguousarray(y0, np.float64)
+    e = lib().orc_solve_batch_warm(B, n, m, _ip(Pp), _ip(Pi), _dp(Px_b), _dp(q_b), _ip(Ap), _ip(Ai),
+                                   _dp(Ax_b), _dp(l_b), _dp(u_b), _dp(x0), _dp(y0), C.byref(s), _dp(x),
+                                   _dp(y), _ip(st), _ip(it), int(nthreads))
     return SimpleNamespace(x=x, y=y, status_val=st, iter=it, err=e)

@@ -304,6 +304,26 @@ __global__ __launch_bounds__(128) void k_reference(long B, int N, int nxa, int n
     }
 }
 
+// One-stage shift of a vector made of `groups` blocks of N+1 stages of width nxa followed
+// by one block of N stages of width nu (x: groups 1, y: groups 2); element-parallel.
+__global__ __launch_bounds__(256) void k_stage_shift(long total, int len, int N, int nxa, int nu, int groups,
+                                                     const double* __restrict__ src, double* __restrict__ dst) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= total) return;
+    const long b = e / len;
+    const int i = (int)(e - b * len);
+    const int stage_blk = (N + 1) * nxa, head = groups * stage_blk;
+    int j;
+    if (i < head) {
+        const int g = i / stage_blk, r = i - g * stage_blk, k = r / nxa, c = r - k * nxa;
+        j = g * stage_blk + min(k + 1, N) * nxa + c;
+    } else {
+        const int r = i - head, k = r / nu, c = r - k * nu;
+        j = head + min(k + 1, N - 1) * nu + c;
+    }
+    dst[e] = src[b * len + j];
+}
+
 // plant step and horizon shift of mpc_dynamics.main (:578-617), per vehicle:
 //   pred_x~[:, k] = sol[k nxa ..],  du[:, k] = sol[(N+1) nxa + k nu ..]  (mpc_increment :398-432)
 //   u = u_past + du_0;  x_next = Ad_0 x + Bd_0 u + gd_0;  x~ = (x_next, u)
@@ -571,6 +591,25 @@ int mpcqp_incr_shift_device(const mpcqp_incr_layout* L, const mpcqp_vehicle* veh
     const VehicleK vk = vehicle_constants(*veh);
     hipLaunchKernelGGL(k_incr_shift, dim3(grid_of(B, 128)), dim3(128), 0, (hipStream_t)stream, vk, incr_k(*L),
                        (long)B, dsol, dAd, dBd, dgd, dxt, dpred, dpdu);
+    MHIPCHK(hipGetLastError());
+    return 0;
+}
+
+int mpcqp_incr_warm_shift_device(int64_t B, int32_t N, int32_t nxa, int32_t nu, const double* dx, const double* dy,
+                                 double* dxs, double* dys, int32_t device, void* stream) {
+    if (!dx || !dxs || B < 0 || N < 1 || nxa < 1 || nu < 1 || (!dy) != (!dys) || dx == dxs || (dy && dy == dys))
+        return set_error(MPCQP_EINVAL, "incr_warm_shift: bad arguments");
+    if (B == 0) return 0;
+    MHIPCHK(hipSetDevice(device));
+    const int n = (N + 1) * nxa + N * nu, m = 2 * (N + 1) * nxa + N * nu;
+    const long tx = B * (long)n;
+    hipLaunchKernelGGL(k_stage_shift, dim3(grid_of(tx, 256)), dim3(256), 0, (hipStream_t)stream, tx, n, N, nxa, nu, 1,
+                       dx, dxs);
+    if (dy) {
+        const long ty = B * (long)m;
+        hipLaunchKernelGGL(k_stage_shift, dim3(grid_of(ty, 256)), dim3(256), 0, (hipStream_t)stream, ty, m, N, nxa,
+                           nu, 2, dy, dys);
+    }
     MHIPCHK(hipGetLastError());
     return 0;
 }

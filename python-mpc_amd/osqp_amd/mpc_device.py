@@ -58,6 +58,7 @@ def _bind():
     L.mpcqp_incr_layout_free.restype = None
     L.mpcqp_reference_search_device.argtypes = [i64, i32, i32, i32, vp, vp, vp, d, vp, i32, vp]
     L.mpcqp_incr_shift_device.argtypes = [vp, _P(Vehicle), i64, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.mpcqp_incr_warm_shift_device.argtypes = [i64, i32, i32, i32, vp, vp, vp, vp, i32, vp]
     L._mpc_bound = True
     return L
 
@@ -178,13 +179,29 @@ def reference_search(path_x, path_y, pred, dt):
     return Xr
 
 
+def warm_shift(N, nxa, nu, x, y=None):
+    """Shift an incremental-layout solution (x (B, n), y (B, m) device tensors) one stage
+    forward for warm-starting the next step (mpcqp_incr_warm_shift_device)."""
+    import torch
+    L = _bind()
+    xs = torch.empty_like(x)
+    ys = None if y is None else torch.empty_like(y)
+    _check(L.mpcqp_incr_warm_shift_device(x.shape[0], int(N), int(nxa), int(nu), _p(x),
+                                          None if y is None else _p(y), _p(xs), None if y is None else _p(ys),
+                                          x.device.index or 0, _stream(torch, x.device)), "incr_warm_shift")
+    return xs, ys
+
+
 class DynamicMPC:
     """B copies of mpc_dynamics.main's closed loop (:437-617), every step on the device.
 
     State per vehicle: x~ = (X, Y, yaw, vx, vy, r, steer, accel), the predicted
     horizon pred_x~ (N+1 stages) and pred_du.  ``step()`` = reference search ->
     linearisation of every predicted stage -> mpc_increment's QP -> batched OSQP
-    solve (settings of :393: polish off, warm_start off) -> plant step and shift."""
+    solve (settings of :393: polish off, warm_start off) -> plant step and shift.
+
+    ``warm_start=True`` (an extension; the reference solves every step cold) starts
+    each solve from the previous step's solution shifted one stage (warm_shift)."""
 
     Q = np.diag([100.0, 100.0, 100.0, 50.0, 50.0, 50.0])          # :456-458
     QN = np.diag([1000.0, 1000.0, 1000.0, 500.0, 500.0, 500.0])
@@ -207,6 +224,8 @@ class DynamicMPC:
         settings = dict(verbose=False, polish=False, warm_start=False)   # mpc_dynamics.py:393
         settings.update(solver_settings)
         settings.pop("verbose", None)
+        self.warm = bool(settings.pop("warm_start"))
+        self.have_sol = False
         self.solver = DeviceBatch(P, A, self.B, device=device, **settings)
         kw = dict(dtype=torch.float64, device=self.dev)
         self.Px = torch.from_numpy(np.tile(P.data, (self.B, 1))).to(**kw).contiguous()
@@ -261,7 +280,11 @@ class DynamicMPC:
         Ax, q, l, u = self.layout.assemble(Ad, Bd, gd, self.xt, Xr)
         st = _stream(torch, self.dev)  # self.stream
         self.solver.setup(self.Px, Ax, q, l, u, stream=st)
+        if self.warm and self.have_sol:
+            xs, ys = warm_shift(self.N, 8, 2, self.sol, self.y)
+            self.solver.warm_start(xs, ys, stream=st)
         self.solver.solve(self.sol, self.y, self.status, self.iters, stream=st)
+        self.have_sol = True
         _check(L.mpcqp_incr_shift_device(self.layout._h, C.byref(self.veh), self.B, _p(self.sol), _p(Ad), _p(Bd),
                                          _p(gd), _p(self.xt), _p(self.pred), _p(self.pdu),
                                          _stream(torch, self.dev)), "incr_shift")

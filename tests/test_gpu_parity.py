@@ -176,3 +176,35 @@ def test_shim_closed_loop_matches_oracle():
     o = _slack_closed_loop(pyoracle)
     assert np.all(g[:, 1] == o[:, 1])
     assert np.abs(g[:, 0] - o[:, 0]).max() < U_TOL
+
+
+def _stage_shift(v, N, nxa, nu, groups):
+    """One-stage shift of incremental-layout iterates (mpcqp_incr_warm_shift_device)."""
+    B = v.shape[0]
+    out = []
+    for g in range(groups):
+        blk = v[:, g * (N + 1) * nxa:(g + 1) * (N + 1) * nxa].reshape(B, N + 1, nxa)
+        out.append(np.concatenate([blk[:, 1:], blk[:, -1:]], 1).reshape(B, -1))
+    du = v[:, groups * (N + 1) * nxa:].reshape(B, N, nu)
+    out.append(np.concatenate([du[:, 1:], du[:, -1:]], 1).reshape(B, -1))
+    return np.concatenate(out, 1)
+
+
+def test_cfg5_warm_started_batch():
+    """cfg 5 as bench.py times it: warm start from the cold solution
+    shifted one stage; device and oracle start from the same (x, y)."""
+    b = mpc.make_batch(5, B=64)
+    s = {k: v for k, v in b["settings"].items() if k != "verbose"}
+    r0 = pyoracle.solve_batch(b["P"], b["A"], b["Px"], b["q"], b["Ax"], b["l"], b["u"], nthreads=16, **s)
+    xs, ys = _stage_shift(r0.x, b["N"], 8, 2, 1), _stage_shift(r0.y, b["N"], 8, 2, 2)
+    bo = pyoracle.solve_batch(b["P"], b["A"], b["Px"], b["q"], b["Ax"], b["l"], b["u"], nthreads=16, x0=xs, y0=ys,
+                              **s)
+    bg = OSQPBatch()
+    bg.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
+    bg.warm_start(x=xs, y=ys)
+    rg = bg.solve()
+    same_iter = rg.iter == bo.iter
+    assert (rg.status_val == bo.status_val).mean() >= 0.99 and same_iter.mean() >= 0.95
+    du = np.abs(rg.x[:, b["u_block"]] - bo.x[:, b["u_block"]]).max(axis=1)
+    assert np.all(du[same_iter] < U_TOL), du.max()
+    assert bo.iter.mean() < r0.iter.mean()

@@ -248,3 +248,74 @@ def test_closed_loop_matches_host_restatement():
     # the vehicles converge toward the path (lateral error shrinks)
     xt = ctl.xt.cpu().numpy()
     assert np.all(np.isfinite(xt))
+
+
+@pytest.mark.gpu
+def test_warm_shift_moves_every_block_one_stage():
+    import torch
+    from osqp_amd.mpc_device import warm_shift
+    N, nxa, nu, B = 7, 8, 2, 5
+    n, m = (N + 1) * nxa + N * nu, 2 * (N + 1) * nxa + N * nu
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((B, n)); y = rng.standard_normal((B, m))
+    xs, ys = warm_shift(N, nxa, nu, torch.tensor(x, device="cuda"), torch.tensor(y, device="cuda"))
+
+    def shift(v, groups):
+        out = []
+        for g in range(groups):
+            blk = v[:, g * (N + 1) * nxa:(g + 1) * (N + 1) * nxa].reshape(B, N + 1, nxa)
+            out.append(np.concatenate([blk[:, 1:], blk[:, -1:]], 1).reshape(B, -1))
+        du = v[:, groups * (N + 1) * nxa:].reshape(B, N, nu)
+        out.append(np.concatenate([du[:, 1:], du[:, -1:]], 1).reshape(B, -1))
+        return np.concatenate(out, 1)
+
+    assert np.array_equal(xs.cpu().numpy(), shift(x, 1))
+    assert np.array_equal(ys.cpu().numpy(), shift(y, 2))
+
+
+@pytest.mark.gpu
+def test_closed_loop_warm_start_matches_oracle():
+    """warm_start=True (an extension): every step's solve starts from the previous
+    solution shifted one stage; the oracle, warm-started from the same shifted iterates
+    on the step's QP, gives the same controls.  Fewer iterations than the cold loop."""
+    import pyoracle
+    from osqp_amd.mpc_device import DynamicMPC
+    B, N, steps = 64, 30, 6
+    rng = np.random.default_rng(11)
+    x0 = np.zeros((B, 6)); x0[:, 3] = rng.uniform(10, 20, B); x0[:, 1] = rng.uniform(-2, 2, B)
+    x0[:, 2] = np.deg2rad(rng.uniform(-8, 8, B))
+    px, py = path()
+    cold = DynamicMPC(x0, np.zeros((B, 2)), px, py, N=N)
+    warm = DynamicMPC(x0, np.zeros((B, 2)), px, py, N=N, warm_start=True)
+    P, A, _, _ = warm.layout.pattern()
+    Px = np.tile(P.data, (B, 1))
+    du = slice((N + 1) * 8, None)
+    ic = iw = match = 0
+    prev = None
+    for step in range(steps):
+        sc, itc = cold.step()
+        sw, itw = warm.step()
+        ic += int(itc.sum()); iw += int(itw.sum())
+        assert (sc.cpu().numpy() == 1).all() and (sw.cpu().numpy() == 1).all()
+        last = {k: v.cpu().numpy() for k, v in warm.last.items()}
+        ws = {} if prev is None else dict(x0=_stage_shift(prev[0], N, 8, 2, 1), y0=_stage_shift(prev[1], N, 8, 2, 2))
+        ro = pyoracle.solve_batch(P, A, Px, last["q"], last["Ax"], last["l"], last["u"], nthreads=16, polish=False,
+                                  **ws)
+        x = warm.sol.cpu().numpy()
+        same = ro.iter == itw.cpu().numpy()
+        match += int(same.sum())
+        assert np.abs(x[same][:, du] - ro.x[same][:, du]).max() < 1e-4
+        prev = (x, warm.y.cpu().numpy())
+    assert match >= 0.9 * B * steps
+    assert iw < ic
+
+
+def _stage_shift(v, N, nxa, nu, groups):
+    B = v.shape[0]
+    out = []
+    for g in range(groups):
+        blk = v[:, g * (N + 1) * nxa:(g + 1) * (N + 1) * nxa].reshape(B, N + 1, nxa)
+        out.append(np.concatenate([blk[:, 1:], blk[:, -1:]], 1).reshape(B, -1))
+    d = v[:, groups * (N + 1) * nxa:].reshape(B, N, nu)
+    out.append(np.concatenate([d[:, 1:], d[:, -1:]], 1).reshape(B, -1))
+    return np.concatenate(out, 1)

@@ -130,3 +130,20 @@ def test_oracle_batch_helper_threads(golden):
     r4 = pyoracle.solve_batch(b["P"], b["A"], b["Px"], b["q"], b["Ax"], b["l"], b["u"], nthreads=4)
     assert (r1.status_val == 1).all()
     assert np.array_equal(r1.x, r4.x) and np.array_equal(r1.iter, r4.iter)
+
+
+def test_oracle_batch_warm_start_matches_single():
+    """solve_batch(x0=, y0=) equals setup + warm_start + solve per instance."""
+    from osqp_amd import mpc
+    b = mpc.make_batch(5, B=4, N=10)
+    s = {k: v for k, v in b["settings"].items() if k != "verbose"}
+    r0 = pyoracle.solve_batch(b["P"], b["A"], b["Px"], b["q"], b["Ax"], b["l"], b["u"], nthreads=2, **s)
+    x0, y0 = r0.x * 0.9, r0.y * 0.9
+    rw = pyoracle.solve_batch(b["P"], b["A"], b["Px"], b["q"], b["Ax"], b["l"], b["u"], nthreads=2, x0=x0, y0=y0, **s)
+    for t in range(4):
+        P = b["P"].copy(); P.data = b["Px"][t].copy()
+        A = b["A"].copy(); A.data = b["Ax"][t].copy()
+        o = pyoracle.OSQP(); o.setup(P, b["q"][t], A, b["l"][t], b["u"][t], **s)
+        o.warm_start(x=x0[t], y=y0[t])
+        r = o.solve()
+        assert r.info.iter == rw.iter[t] and np.array_equal(r.x, rw.x[t])
