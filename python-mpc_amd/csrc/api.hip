@@ -221,7 +221,7 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
     k.mode = solve_mode(k.variant);
     k.self = (const KParams*)(base + carve<KParams>(off, 1));
     HIPCHK(hipMemcpy((void*)k.self, &k, sizeof(KParams), hipMemcpyHostToDevice));
-    if (size_t lds = lds_solve_bytes(k); lds > 160 * 1024)
+    if (size_t lds = lds_kernel_bytes(k); lds > 160 * 1024)
         return fail(MPCQP_EUNSUPPORTED, "problem needs %zu bytes of LDS per instance (> 160 KiB)", lds);
     return 0;
 }
@@ -564,7 +564,7 @@ int mpcqp_get_plan_info(const mpcqp_handle* h, mpcqp_plan_info* info) {
     info->n = h->n; info->m = h->m; info->nb = h->plan.nb; info->block = kS;
     info->npad = h->plan.npad; info->max_level = h->plan.max_level;
     info->batch = h->B; info->n_devices = (int)h->shards.size();
-    info->lds_bytes_solve = h->shards.empty() ? 0 : (int64_t)lds_solve_bytes(h->shards[0].kp);
+    info->lds_bytes_solve = h->shards.empty() ? 0 : (int64_t)lds_kernel_bytes(h->shards[0].kp);
     info->bytes_per_instance = (int64_t)(workspace_bytes(h->plan, 1, false));
     info->amax = h->plan.amax;
     info->gather_k = h->plan.gather_k;

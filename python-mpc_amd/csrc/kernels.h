@@ -7,6 +7,7 @@
 namespace mpcqp {
 
 constexpr int kThreads = 256;
+constexpr int kThreadsBig = 512;  // solve_big.hip (long horizons)
 constexpr int kProfSlots = 16;  // factor, rhs, bt_solve, update, checks, tail, total cycles, total 100 MHz ticks,
                                 // factor split: assembly, F/S products, Gauss-Jordan, block epilogue,
                                 // solve split (wave kernels): phase A, phase B, phase C, spare
@@ -48,6 +49,8 @@ struct KParams {
 
 size_t lds_setup_bytes(const KParams& p);
 size_t lds_solve_bytes(const KParams& p);
+size_t lds_solve_bytes_big(const KParams& p);  // + the F rows of solve_big.hip
+size_t lds_kernel_bytes(const KParams& p);     // what the chosen variant's kernel allocates
 // error text for mpcqp_last_error() (api.hip); returns code
 int set_error(int code, const char* fmt, ...);
 
@@ -63,5 +66,7 @@ bool variant_fits(const KParams& p, int variant);
 hipError_t launch_solve(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st);
 // one-wave-per-QP kernel (solve_wave.hip), variants 8 and 9
 hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st);
+// 512-thread long-horizon kernel (solve_big.hip), variants 11-13
+hipError_t launch_solve_big(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st);
 
 }  // namespace mpcqp

@@ -498,6 +498,10 @@ size_t lds_solve_bytes(const KParams& p) {
            mp + 64;
 }
 
+size_t lds_kernel_bytes(const KParams& p) {
+    return p.variant >= 11 && p.variant <= 13 ? lds_solve_bytes_big(p) : lds_solve_bytes(p);
+}
+
 template <int NB, int A, int K, int CS, int RS, int W, bool TRI = false>
 static hipError_t go(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st, size_t lds) {
     auto k = k_solve<NB, A, K, CS, RS, W, TRI>;
@@ -524,12 +528,18 @@ bool variant_fits(const KParams& p, int v) {
         case 8: return p.nb == 4 && p.amax <= 8 && p.gk <= 6 && p.m <= 3 * 64 && lds_solve_bytes(p) < 65536;
         case 9: return p.nb == 4 && p.amax <= 8 && p.gk <= 8 && p.m <= 4 * 64 && lds_solve_bytes(p) < 65536;
         case 10: return p.nb == 4 && p.amax <= 8 && p.gk <= 6 && p.m <= 2 * 128 && lds_solve_bytes(p) < 65536;
+        case 11: case 12: case 13: {
+            const int nbm = v == 11 ? 12 : v == 12 ? 18 : 24, csm = v == 11 ? 1 : 2, rsm = v == 13 ? 3 : 2;
+            const int csb = (p.npad + kThreadsBig - 1) / kThreadsBig, rsb = (p.m + kThreadsBig - 1) / kThreadsBig;
+            return p.nb > 4 && p.nb <= nbm && p.amax <= 16 && p.gk <= 8 && csb <= csm && rsb <= rsm &&
+                   lds_solve_bytes_big(p) <= 160 * 1024;
+        }
         default: return false;
     }
 }
 
 int solve_variant(const KParams& p) {
-    static const int order[] = {10, 8, 9, 0, 1, 2, 3, 4, 5, 6};
+    static const int order[] = {10, 8, 9, 0, 1, 2, 3, 11, 12, 13, 4, 5, 6};
     for (int v : order)
         if (variant_fits(p, v)) return v;
     return -1;
@@ -539,6 +549,7 @@ int solve_threads(int variant) {
     switch (variant) {
         case 8: case 9: return 64;
         case 10: return 128;
+        case 11: case 12: case 13: return kThreadsBig;
         default: return T;
     }
 }
@@ -546,7 +557,7 @@ int solve_threads(int variant) {
 int solve_mode(int variant) {  // what factorize stores for the variant (KParams::mode)
     switch (variant) {
         case 0: case 8: case 9: case 10: return 2;
-        case 1: case 2: case 3: case 7: return 1;
+        case 1: case 2: case 3: case 7: case 11: case 12: case 13: return 1;
         default: return 0;
     }
 }
@@ -563,6 +574,7 @@ hipError_t launch_solve(const KParams& p, long B, double* xo, double* yo, int fa
         case 6: return go<0, 32, 16, 8, 8, 1>(p, B, xo, yo, factor_only, st, lds);
         case 7: return go<4, 8, 6, 1, 1, 4, false>(p, B, xo, yo, factor_only, st, lds);
         case 8: case 9: case 10: return launch_solve_wave(p, B, xo, yo, factor_only, st);
+        case 11: case 12: case 13: return launch_solve_big(p, B, xo, yo, factor_only, st);
         default: return hipErrorInvalidValue;
     }
 }

@@ -146,8 +146,7 @@ __device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restri
 template <int TT, class KP>
 __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, double* __restrict__ Fg,
                                           double* __restrict__ Hg, double* __restrict__ Sg) {
-    constexpr int NI = 256 / TT;  // Gauss-Jordan tile rows per thread
-    const int tid = threadIdx.x, i0 = tid >> 3, jg = tid & 7;
+    const int tid = threadIdx.x;
     const int nb = p.nb, amax = p.amax, ntgt = p.ntgt, tmax = p.term_max, mode = p.mode;
     const long gstride = (long)amax * S;
     const int2* __restrict__ tt = (const int2*)p.tterm;
@@ -231,7 +230,7 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
             __syncthreads();
         }
         FPH(9)
-        if constexpr (TT <= 256) {
+        {
             // one wave inverts the tile (no barrier per pivot); the verdict goes through LDS
             double* okslot = EK + 2 * S;
             if (tid < 64) {
@@ -241,61 +240,6 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
             __syncthreads();
             if (!(okslot[0] > 0.5)) ok = false;
             FPH(10)
-        } else {
-            // Gauss-Jordan inverse with the tile in registers: thread (i0 + TT/8 * ii, jg)
-            // keeps elements [i][jg + 8c]; per pivot only its row and column go through
-            // LDS (double-buffered in EK, free by now), so each pivot costs one barrier.
-            double v[NI][4];
-#pragma unroll
-            for (int ii = 0; ii < NI; ++ii)
-#pragma unroll
-                for (int cc = 0; cc < 4; ++cc) v[ii][cc] = DK[(i0 + TT / 8 * ii) * S + jg + 8 * cc];
-            double* rowbuf = EK;
-            double* colbuf = EK + 2 * S;
-#pragma unroll 1
-            for (int pv = 0; pv < S; ++pv) {
-                const int buf = (pv & 1) * S;
-                const int cp = pv >> 3;
-#pragma unroll
-                for (int ii = 0; ii < NI; ++ii) {
-                    const int i = i0 + TT / 8 * ii;
-                    if (i == pv) {
-#pragma unroll
-                        for (int cc = 0; cc < 4; ++cc) rowbuf[buf + jg + 8 * cc] = v[ii][cc];
-                    }
-                    if (jg == (pv & 7))
-                        colbuf[buf + i] = cp == 0 ? v[ii][0] : cp == 1 ? v[ii][1] : cp == 2 ? v[ii][2] : v[ii][3];
-                }
-                __syncthreads();
-                const double piv = rowbuf[buf + pv];
-                if (!(piv > 0.0)) ok = false;
-                const double d = 1.0 / piv;
-                double rowv[4];
-#pragma unroll
-                for (int cc = 0; cc < 4; ++cc) rowv[cc] = rowbuf[buf + jg + 8 * cc];
-#pragma unroll
-                for (int ii = 0; ii < NI; ++ii) {
-                    const int i = i0 + TT / 8 * ii;
-                    const double colv = colbuf[buf + i];
-#pragma unroll
-                    for (int cc = 0; cc < 4; ++cc) {
-                        const int j = jg + 8 * cc;
-                        if (i == pv) v[ii][cc] = (j == pv) ? d : rowv[cc] * d;
-                        else if (j == pv) v[ii][cc] = -colv * d;
-                        else v[ii][cc] = v[ii][cc] - colv * (rowv[cc] * d);
-                    }
-                }
-            }
-#pragma unroll
-            for (int ii = 0; ii < NI; ++ii)
-#pragma unroll
-                for (int cc = 0; cc < 4; ++cc) DK[(i0 + TT / 8 * ii) * S + jg + 8 * cc] = v[ii][cc];
-            FPH(10)
-#pragma unroll
-            for (int ii = 0; ii < NI; ++ii)
-#pragma unroll
-                for (int cc = 0; cc < 4; ++cc)
-                    Sg[(long)k * SS + (i0 + TT / 8 * ii) * S + jg + 8 * cc] = v[ii][cc];
         }
         double* t = SP; SP = DK; DK = t;  // S_k^{-1} becomes "previous"
         __syncthreads();
