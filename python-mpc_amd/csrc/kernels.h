@@ -29,12 +29,13 @@ enum : int {
 // workspace (instance-major arrays) + settings.  Passed by value.
 struct KParams {
     int n, m, nb, npad, nnzP, nnzA, amax, gk, pk, ntgt, term_max;
+    int bmax, pmeet;  // two-sided factorisation (solve_big.hip): tail width, meeting block
     int variant;  // solve-kernel instantiation (solve.hip: launch_solve)
     int mode;     // factor storage of that variant (solve.hip: factorize)
     // plan
     const int *pad_var, *acsc_ptr, *acsc_row, *acsc_v, *acsr_ptr, *acsr_col, *acsr_v;
     const int *psym_ptr, *psym_col, *psym_v, *p_r, *p_c, *a_r, *a_c;
-    const int *asm_blk_ptr, *asm_tgt, *tterm, *acsr_pos, *gcol, *grow, *gpsym;
+    const int *asm_blk_ptr, *asm_tgt, *tterm, *acsr_pos, *gcol, *grow, *gpsym, *toff;
     // workspace
     double *Px, *Ax, *q, *D, *l, *u, *E, *x, *z, *y, *scal, *F, *H, *Si, *dyc, *dxc;
     double *obj, *pri, *dua, *rho_est;

@@ -249,6 +249,21 @@ std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const
         }
     for (size_t t = 0; t < pl.asm_tgt.size(); ++t)
         if (pl.asm_tgt[t] >= SS) pl.amax = std::max(pl.amax, (int)((pl.asm_tgt[t] - SS) / kS) + 1);
+    {
+        std::vector<int> cmin(pl.nb, kS), cmax(pl.nb, -1);
+        for (int k = 1; k < pl.nb; ++k)
+            for (int t = pl.asm_blk_ptr[k]; t < pl.asm_blk_ptr[k + 1]; ++t)
+                if (pl.asm_tgt[t] >= SS) {
+                    const int c = (pl.asm_tgt[t] - (int)SS) % kS;
+                    cmin[k - 1] = std::min(cmin[k - 1], c);
+                    cmax[k - 1] = std::max(cmax[k - 1], c);
+                }
+        pl.bmax = 1;
+        for (int k = 0; k < pl.nb; ++k)
+            if (cmax[k] >= 0) pl.bmax = std::max(pl.bmax, cmax[k] - cmin[k] + 1);
+        pl.toff.assign(pl.nb, 0);
+        for (int k = 0; k < pl.nb; ++k) pl.toff[k] = cmax[k] >= 0 ? std::min(cmin[k], kS - pl.bmax) : 0;
+    }
     pl.acsr_pos.resize(pl.nnzA);
     for (int e = 0; e < pl.nnzA; ++e) pl.acsr_pos[e] = csc_pos[pl.acsr_v[e]];
     pl.csc_pos = csc_pos;

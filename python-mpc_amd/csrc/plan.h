@@ -57,6 +57,10 @@ struct Plan {
     int p_k = 0;                  // max nonzeros per column of the symmetric P
     std::vector<int> gpsym;       // [npad*kGS] P by padded column: (Pv index) | (padded column << 16)
     int amax = 0;                 // max over k of (last nonzero local row of E_k) + 1: F_k rows / H_{k-1} cols
+    // the other side of the coupling: the columns of E_{k+1} (variables of block k that
+    // couple to block k+1, its last BFS level) lie in [toff[k], toff[k] + bmax)
+    std::vector<int> toff;        // [nb]
+    int bmax = 0;
 };
 
 // Returns "" on success, otherwise an error message.

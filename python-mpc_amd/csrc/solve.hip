@@ -531,7 +531,7 @@ bool variant_fits(const KParams& p, int v) {
         case 11: case 12: case 13: {
             const int nbm = v == 11 ? 12 : v == 12 ? 18 : 24, csm = v == 11 ? 1 : 2, rsm = v == 13 ? 3 : 2;
             const int csb = (p.npad + kThreadsBig - 1) / kThreadsBig, rsb = (p.m + kThreadsBig - 1) / kThreadsBig;
-            return p.nb > 4 && p.nb <= nbm && p.amax <= 16 && p.gk <= 8 && csb <= csm && rsb <= rsm &&
+            return p.nb > 4 && p.nb <= nbm && p.amax <= 16 && p.bmax <= 16 && p.gk <= 8 && csb <= csm && rsb <= rsm &&
                    lds_solve_bytes_big(p) <= 160 * 1024;
         }
         default: return false;
@@ -557,7 +557,8 @@ int solve_threads(int variant) {
 int solve_mode(int variant) {  // what factorize stores for the variant (KParams::mode)
     switch (variant) {
         case 0: case 8: case 9: case 10: return 2;
-        case 1: case 2: case 3: case 7: case 11: case 12: case 13: return 1;
+        case 1: case 2: case 3: case 7: return 1;
+        case 11: case 12: case 13: return 3;  // two-sided factor (solve_big.hip)
         default: return 0;
     }
 }

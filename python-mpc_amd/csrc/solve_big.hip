@@ -32,78 +32,363 @@
 namespace mpcqp {
 
 constexpr int TB = kThreadsBig;
+// row stride of the F / G rows in LDS: 40 doubles, so the 8 rows a wave reads at once
+// (and the 8 columns it reads transposed) fall on different banks (stride 32: 8-way
+// conflicts)
+constexpr int FGS = 40;
 
-template <int NBM>
-struct BigFactor {
-    double Si[NBM][2], H[NBM > 1 ? NBM - 1 : 1];
-    // Sg: S_k^{-1} tiles, Fg: F_k tiles (rows < amax valid); F rows go to Fc (LDS)
-    __device__ __forceinline__ void load(int nb, int amax, const double* __restrict__ Fg,
-                                         const double* __restrict__ Sg, double* __restrict__ Fc) {
-        const int tid = threadIdx.x, i = tid >> 4, jl = tid & 15;
-#pragma unroll
-        for (int k = 0; k < NBM; ++k) {
-            if (k < nb) {
-                Si[k][0] = Sg[(long)k * SS + i * S + jl];
-                Si[k][1] = Sg[(long)k * SS + i * S + jl + 16];
-            }
-            if (k < NBM - 1) H[k] = (k + 1 < nb && jl < amax) ? Fg[(long)(k + 1) * SS + jl * S + i] : 0.0;
+// ---------------------------------------------------------------------------
+// Two-sided ("twisted") block factorisation of K = tridiag(E_k, D_k, E_{k+1}'),
+// meeting at block p = pmeet:
+//   top     k = 0 .. p-1 :  S_k = D_k - F_k E_k'        F_k = E_k S_{k-1}^{-1}     (rows < amax)
+//   bottom  k = nb-1 .. p+1: T_k = D_k - G_k E_{k+1}    G_k = E_{k+1}' T_{k+1}^{-1} (rows toff_k + [0, bmax))
+//   middle  M = D_p - F_p E_p' - G_p E_{p+1}
+// E_k has nonzero rows < amax (block k's first BFS level) and nonzero columns in
+// toff_{k-1} + [0, bmax) (block k-1's last level), so F_k and G_k are thin and the
+// Schur corrections touch an amax x amax / bmax x bmax corner only.  The two chains
+// run in lock-step -- threads 0-255 the top, 256-511 the bottom, wave 0 and wave 4
+// invert their tiles at the same time -- so the factorisation takes max(p, nb-1-p)+1
+// steps instead of nb.  Stored: Sg[k] = S_k^{-1} / M^{-1} / T_k^{-1};  Fg[k] rows
+// < amax = F_k (k = 1..p);  Hg[k] rows < bmax = G_k's tail rows (k = p..nb-2).
+// X2: four scratch tiles besides SLds' three.  False on a non-positive pivot.
+template <class KP>
+__device__ __forceinline__ bool factorize2(const KP& p, SLds& L, double* __restrict__ X2, double rho,
+                                           double* __restrict__ Fg, double* __restrict__ Hg,
+                                           double* __restrict__ Sg) {
+    const int tid = threadIdx.x, half = tid >> 8, u = tid & 255;
+    const int nb = p.nb, amax = p.amax, bmax = p.bmax, pm = p.pmeet, ntgt = p.ntgt, tmax = p.term_max;
+    const int nst = max(pm, nb - 1 - pm);
+    const int2* __restrict__ tt = (const int2*)p.tterm;
+    double *SP = L.SP, *DK = L.DK, *EK = L.EK;                                   // top chain
+    double *SP2 = X2, *DK2 = X2 + SS, *EK2 = X2 + 2 * SS, *EKp = X2 + 3 * SS;   // bottom chain
+    bool ok = true;
+#ifdef MPCQP_PHASE_PROF
+    long long tf = clock64();
+#define FPH(k) if (tid == 0) { const long long t_ = clock64(); L.pacc[k] += t_ - tf; tf = t_; }
+#else
+#define FPH(k)
+#endif
+    auto init = [&](int k, double* D, double* E, int t0, int stride) {
+        for (int e = t0; e < SS; e += stride) {
+            const int r = e >> 5;
+            D[e] = e == r * (S + 1) ? (p.pad_var[k * S + r] >= 0 ? p.sigma : 1.0) : 0.0;
+            E[e] = 0.0;
         }
-        for (int o = tid; o < (nb - 1) * amax * S; o += TB) {
-            const int k = o / (amax * S), r = o - k * amax * S;
-            Fc[o] = Fg[(long)(k + 1) * SS + r];
+    };
+    // every target of block k has one owner: its terms are summed in plan order
+    auto assemble = [&](int k, double* D, double* E, int t0, int stride) {
+#pragma unroll 1
+        for (int t = p.asm_blk_ptr[k] + t0; t < p.asm_blk_ptr[k + 1]; t += stride) {
+            double acc = 0.0;
+#pragma unroll 4
+            for (int j = 0; j < tmax; ++j) {
+                const int2 w = tt[(long)j * ntgt + t];
+                const int a = w.x & 0xFFFF, bb = (int)((unsigned)w.x >> 16), r = w.y;
+                acc += r < 0 ? L.Pv[a] : rho_of(L.ct[r], rho) * L.Acsc[a] * L.Acsc[bb];
+            }
+            const int tg = p.asm_tgt[t];
+            if (tg < SS) D[tg] += acc;
+            else E[tg - SS] += acc;
+        }
+    };
+    // F_k = E_k S_{k-1}^{-1} (rows < amax) -> f, Fg[k]
+    auto top_f = [&](int k, double (&f)[2]) {
+        int nf = 0;
+#pragma unroll 1
+        for (int o = u; o < amax * S; o += 256, ++nf) {
+            const int r = o >> 5, j = o & (S - 1);
+            double sacc = 0.0;
+#pragma unroll 8
+            for (int l = 0; l < S; ++l) sacc += EK[r * S + l] * SP[l * S + j];
+            f[nf & 1] = sacc;
+            Fg[(long)k * SS + o] = sacc;
+        }
+    };
+    // G_k = E_{k+1}' T_{k+1}^{-1} on block k's tail rows (E_{k+1} in EKp, T^{-1} in SP2) -> g, Hg[k]
+    auto bot_g = [&](int k, int toff, double (&g)[2], int t0, int stride) {
+        int ng = 0;
+#pragma unroll 1
+        for (int o = t0; o < bmax * S; o += stride, ++ng) {
+            const int a = o >> 5, j = o & (S - 1);
+            double sacc = 0.0;
+#pragma unroll 1
+            for (int r = 0; r < amax; ++r) sacc += EKp[r * S + toff + a] * SP2[r * S + j];
+            g[ng & 1] = sacc;
+            Hg[(long)k * SS + o] = sacc;
+        }
+    };
+    // D -= F E' on the amax x amax corner (F rows in SP, E in EK)
+    auto top_corr = [&](double* D, int t0, int stride) {
+#pragma unroll 1
+        for (int o = t0; o < amax * amax; o += stride) {
+            const int r = o / amax, c = o - r * amax;
+            double sacc = 0.0;
+#pragma unroll 8
+            for (int l = 0; l < S; ++l) sacc += SP[r * S + l] * EK[c * S + l];
+            D[r * S + c] -= sacc;
+        }
+    };
+    // D -= G E_{k+1} on the bmax x bmax tail corner (G rows in SP2, E_{k+1} in EKp)
+    auto bot_corr = [&](double* D, int toff, int t0, int stride) {
+#pragma unroll 1
+        for (int o = t0; o < bmax * bmax; o += stride) {
+            const int a = o / bmax, c = o - a * bmax;
+            double sacc = 0.0;
+#pragma unroll 1
+            for (int r = 0; r < amax; ++r) sacc += SP2[a * S + r] * EKp[r * S + toff + c];
+            D[(toff + a) * S + toff + c] -= sacc;
+        }
+    };
+
+#pragma unroll 1
+    for (int s = 0; s < nst; ++s) {
+        const int kt = s, kb = nb - 1 - s;
+        const bool top = half == 0 && s < pm, bot = half == 1 && s < nb - 1 - pm;
+        const int toffb = kb < nb - 1 ? p.toff[kb] : 0;
+        if (top) init(kt, DK, EK, u, 256);
+        if (bot) init(kb, DK2, EK2, u, 256);
+        __syncthreads();
+        if (top) assemble(kt, DK, EK, u, 256);
+        if (bot) assemble(kb, DK2, EK2, u, 256);
+        __syncthreads();
+        FPH(8)
+        double f[2] = {0.0, 0.0};
+        if (top && kt > 0) top_f(kt, f);
+        if (bot && kb < nb - 1) bot_g(kb, toffb, f, u, 256);
+        __syncthreads();  // every read of S_{k-1}^{-1} / T_{k+1}^{-1} done
+        {
+            int nf = 0;
+            if (top && kt > 0)
+                for (int o = u; o < amax * S; o += 256, ++nf) SP[o] = f[nf & 1];
+            if (bot && kb < nb - 1)
+                for (int o = u; o < bmax * S; o += 256, ++nf) SP2[o] = f[nf & 1];
+        }
+        __syncthreads();
+        if (top && kt > 0) top_corr(DK, u, 256);
+        if (bot && kb < nb - 1) bot_corr(DK2, toffb, u, 256);
+        __syncthreads();
+        FPH(9)
+        // wave 0 inverts the top tile, wave 4 the bottom one, at the same time
+        double* okslot = EK + 2 * S;
+        double* okslot2 = EKp + 2 * S;
+        const bool topw = s < pm, botw = s < nb - 1 - pm;
+        if (tid < 64 && topw) {
+            const bool okw = gj_wave<true>(DK, EK, Sg + (long)kt * SS);
+            if (tid == 0) okslot[0] = okw ? 1.0 : 0.0;
+        }
+        if (tid >= 256 && tid < 320 && botw) {
+            const bool okw = gj_wave<true>(DK2, EKp, Sg + (long)kb * SS);
+            if (tid == 256) okslot2[0] = okw ? 1.0 : 0.0;
+        }
+        __syncthreads();
+        if (topw && !(okslot[0] > 0.5)) ok = false;
+        if (botw && !(okslot2[0] > 0.5)) ok = false;
+        FPH(10)
+        if (topw) { double* t = SP; SP = DK; DK = t; }
+        if (botw) {
+            double* t = SP2; SP2 = DK2; DK2 = t;
+            t = EKp; EKp = EK2; EK2 = t;  // E_kb is the next bottom step's E_{k+1}
+        }
+        __syncthreads();  // the okslots are rewritten by the next step's init
+    }
+    // middle block: both corrections, then its inverse
+    {
+        const int toffp = pm < nb - 1 ? p.toff[pm] : 0;
+        init(pm, DK, EK, tid, TB);
+        __syncthreads();
+        assemble(pm, DK, EK, tid, TB);
+        __syncthreads();
+        FPH(8)
+        double f[2] = {0.0, 0.0};
+        if (half == 0 && pm > 0) top_f(pm, f);
+        if (half == 1 && pm < nb - 1) bot_g(pm, toffp, f, u, 256);
+        __syncthreads();
+        {
+            int nf = 0;
+            if (half == 0 && pm > 0)
+                for (int o = u; o < amax * S; o += 256, ++nf) SP[o] = f[nf & 1];
+            if (half == 1 && pm < nb - 1)
+                for (int o = u; o < bmax * S; o += 256, ++nf) SP2[o] = f[nf & 1];
+        }
+        __syncthreads();
+        if (pm > 0) top_corr(DK, tid, TB);
+        __syncthreads();
+        if (pm < nb - 1) bot_corr(DK, toffp, tid, TB);
+        __syncthreads();
+        FPH(9)
+        double* okslot = EK + 2 * S;
+        if (tid < 64) {
+            const bool okw = gj_wave<true>(DK, EK, Sg + (long)pm * SS);
+            if (tid == 0) okslot[0] = okw ? 1.0 : 0.0;
+        }
+        __syncthreads();
+        if (!(okslot[0] > 0.5)) ok = false;
+        FPH(10)
+    }
+#undef FPH
+    return ok;
+}
+
+template <class KP>
+__device__ __noinline__ bool factorize2_nl(const KP* gp, long b, double rho, double* X2) {
+    const KPc& p = kconst(gp);
+    SL2 C = carve(p);
+    return factorize2(p, C.L, X2, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
+                      p.Si + b * (long)p.nb * SS);
+}
+
+// The factor on chip for the two-sided sweep.  Thread t: half h = t / 256 (0 top,
+// 1 bottom), (i, jg) = (t % 256 / 8, t % 8): row i of a tile is summed by one 8-lane
+// DPP half-row, lane jg holding columns jg + 8c.
+//   top    Inv[s] = S_s^{-1} (s < p), M^{-1} (s = p)      (registers)
+//   bottom Inv[s] = T_{nb-1-s}^{-1}                       (registers)
+//   F_k rows (k = 1..p) and G_k tail rows (k = p..nb-2)  (LDS; the backward sweep
+//   reads them transposed: H_k = F_{k+1}', T_k^{-1} E_k = G_{k-1}')
+template <int SL>
+struct TwoSided {
+    double Inv[SL][4];
+    __device__ __forceinline__ void load(int nb, int pm, int amax, int bmax, const double* __restrict__ Fg,
+                                         const double* __restrict__ Hg, const double* __restrict__ Sg,
+                                         double* __restrict__ Fc, double* __restrict__ Gc) {
+        const int tid = threadIdx.x, half = __builtin_amdgcn_readfirstlane(tid >> 8), u = tid & 255, i = u >> 3,
+                  jg = u & 7;
+        const int nbot = nb - 1 - pm;
+#pragma unroll
+        for (int s = 0; s < SL; ++s) {
+            const bool have = half == 0 ? s <= pm : s < nbot;
+            const int k = half == 0 ? s : nb - 1 - s;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) Inv[s][c] = have ? Sg[(long)k * SS + i * S + jg + 8 * c] : 0.0;
+        }
+        for (int o = tid; o < pm * amax * S; o += TB) {  // row q = k amax + r of F_{k+1}
+            const int q = o >> 5, j = o & (S - 1), k = q / amax, r = q - k * amax;
+            Fc[q * FGS + j] = Fg[(long)(k + 1) * SS + r * S + j];
+        }
+        for (int o = tid; o < nbot * bmax * S; o += TB) {
+            const int q = o >> 5, j = o & (S - 1), k = q / bmax, r = q - k * bmax;
+            Gc[q * FGS + j] = Hg[(long)(pm + k) * SS + r * S + j];
         }
     }
 };
 
-// xt = K^{-1} rb (rb is overwritten by the forward sweep).  2 nb - 1 barriers.
-template <int NBM>
-__device__ __forceinline__ void big_solve(const BigFactor<NBM>& R, int nb, int amax, const double* Fc, double* rb,
-                                          double* xt) {
+__device__ __forceinline__ double dot4c(const double (&a)[4], const double (&v)[4]) {
+    return (a[0] * v[0] + a[1] * v[1]) + (a[2] * v[2] + a[3] * v[3]);
+}
+
+// xt = K^{-1} rb.  rb is read-only: the forward sweeps' low-rank updates go to
+// two dense correction arrays, corT[k][r] = (F_k w_{k-1})[r] (r < amax) and
+// corB[k][toff_k + a] = (G_k w~_{k+1})[a] (a < bmax), zero everywhere else (they
+// are cleared once per solve and the same entries are rewritten every iteration).
+// A step reads w_k - corT_k - corB_k with independent LDS loads, sums two 8-lane
+// DPP dot products side by side and writes plainly -- no read-modify-write and no
+// branch on its critical path.  Both halves run the same instruction stream with
+// per-half operands.  2 max(p, nb-1-p) + 1 barriers.
+template <int SL>
+__device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KParams& p, const double* Fc,
+                                              const double* Gc, const int* toffL, const double* rb, double* xt,
+                                              double* corT, double* corB, long long* pacc) {
+#ifdef MPCQP_PHASE_PROF
+    long long t0s = clock64();
+#define SPH(k) if (pacc && threadIdx.x == 0) { const long long t_ = clock64(); pacc[k] += t_ - t0s; t0s = t_; }
+#else
+#define SPH(k)
+#endif
     int opq = 0;
     asm volatile("" : "+s"(opq));  // keep per-block LDS addresses out of the register budget
-    const int tid = threadIdx.x, i = tid >> 4, jl = (tid & 15) + opq;
-    const bool frow = i < amax;
+    const int tid = threadIdx.x, half = __builtin_amdgcn_readfirstlane(tid >> 8), u = tid & 255, i = u >> 3,
+              jg = (u & 7) + opq, j0 = u & 7;
+    const int nb = p.nb, pm = p.pmeet, amax = p.amax, bmax = p.bmax, nbot = nb - 1 - pm;
+    const int nst = nbot > pm ? nbot : pm;
+    const int nmine = half ? nbot : pm, lim = half ? bmax : amax;
+    const bool writer = j0 == 0, lowrank = i < lim;
+    const int ir = lowrank ? i : 0;  // F / G row this thread sums (row 0 for the rest: reads stay in range)
+    double* corW = half ? corB : corT;
+    auto load_w = [&](int k, double (&v4)[4]) {
+        const double* w = rb + k * S;
+        const double* ct = corT + k * S;
+        const double* cb = corB + k * S;
 #pragma unroll
-    for (int k = 1; k < NBM; ++k) {
-        if (k < nb) {
-            const double* v = rb + (k - 1) * S;
-            const double v0 = v[jl], v1 = v[jl + 16];
-            const double s2 = reduce16(R.Si[k - 1][0] * v0 + R.Si[k - 1][1] * v1);
-            if (frow) {
-                const double* f = Fc + ((k - 1) * amax + i) * S;
-                const double s1 = reduce16(f[jl] * v0 + f[jl + 16] * v1);
-                if ((tid & 15) == 0) rb[k * S + i] -= s1;
+        for (int c = 0; c < 4; ++c) v4[c] = (w[jg + 8 * c] - ct[jg + 8 * c]) - cb[jg + 8 * c];
+    };
+    // forward: top step s: t_{s-1} = S_{s-1}^{-1} w_{s-1}, corT_s = F_s w_{s-1};
+    //          bottom step s (k = nb-1-s): t~_{k+1} = T_{k+1}^{-1} w~_{k+1}, corB_k = G_k w~_{k+1}
+#pragma unroll
+    for (int s = 1; s < SL; ++s) {
+        if (s <= nst) {
+            if (s <= nmine) {
+                const int ks = half ? nb - s : s - 1, kd = half ? nb - 1 - s : s;
+                const int woff = kd * S + (half ? toffL[kd] : 0);
+                double v4[4];
+                load_w(ks, v4);
+                const double* f = (half ? Gc + (kd - pm) * bmax * FGS : Fc + (s - 1) * amax * FGS) + ir * FGS;
+                const double f4[4] = {f[jg], f[jg + 8], f[jg + 16], f[jg + 24]};
+                const double t = reduce8(dot4c(R.Inv[s - 1], v4));
+                const double c = reduce8(dot4c(f4, v4));
+                if (writer) {
+                    xt[ks * S + i] = t;
+                    if (lowrank) corW[woff + i] = c;
+                }
             }
-            if ((tid & 15) == 0) xt[(k - 1) * S + i] = s2;
             __syncthreads();
         }
     }
+    SPH(12)
+    // middle: x_p = M^{-1} w_p with both chains' corrections, by the top half
+    if (half == 0) {
+        double v4[4];
+        load_w(pm, v4);
 #pragma unroll
-    for (int k = 0; k < NBM; ++k) {
-        if (k == nb - 1) {
-            const double* v = rb + k * S;
-            const double s2 = reduce16(R.Si[k][0] * v[jl] + R.Si[k][1] * v[jl + 16]);
-            if ((tid & 15) == 0) xt[k * S + i] = s2;
+        for (int s = 0; s < SL; ++s) {
+            if (s == pm) {
+                const double t = reduce8(dot4c(R.Inv[s], v4));
+                if (writer) xt[pm * S + i] = t;
+            }
         }
     }
     __syncthreads();
+    SPH(13)
+    // backward: top x_k = t_k - H_k x_{k+1}[0, amax) (k = p-1 .. 0);
+    //           bottom x_k = t~_k - G_{k-1}' x_{k-1}[toff_{k-1} + (0, bmax)] (k = p+1 .. nb-1)
 #pragma unroll
-    for (int k = NBM - 2; k >= 0; --k) {
-        if (k <= nb - 2) {
-            const double s = reduce16(R.H[k] * xt[(k + 1) * S + (jl & 15)]);
-            if ((tid & 15) == 0) xt[k * S + i] -= s;
+    for (int s = 1; s < SL; ++s) {
+        if (s <= nst) {
+            if (s <= nmine) {
+                const int k = half ? pm + s : pm - s;
+                const double* x1 = xt + (half ? (k - 1) * S + toffL[k - 1] : (k + 1) * S);
+                // H_k[i][r] = F_{k+1}[r][i] (top), G_{k-1}[r][i] (bottom); rows >= lim read as 0
+                const double* h = (half ? Gc + (k - 1 - pm) * bmax * FGS : Fc + k * amax * FGS) + i;
+                const double tk = xt[k * S + i];
+                const int r0 = j0 < lim ? j0 : 0, r1 = j0 + 8 < lim ? j0 + 8 : 0;
+                const double h0 = h[r0 * FGS], h1 = h[r1 * FGS], x0 = x1[r0], x8 = x1[r1];
+                const double a0 = j0 < lim ? h0 * x0 : 0.0;
+                const double a1 = j0 + 8 < lim ? h1 * x8 : 0.0;
+                const double c = reduce8(a0 + a1);
+                if (writer) xt[k * S + i] = tk - c;
+            }
             __syncthreads();
         }
     }
+    SPH(14)
+#undef SPH
+}
+
+// doubles of the F / G region: F_k rows (k = 1..p), G_k tail rows (k = p..nb-2), and
+// at least the four scratch tiles factorize2 needs
+__host__ __device__ inline int big_fg_len(const KParams& p) {
+    const int fg = (p.pmeet * p.amax + (p.nb - 1 - p.pmeet) * p.bmax) * FGS;
+    return fg > 4 * SS ? fg : 4 * SS;
 }
 
 // LDS after the common carve (solve.hip::lds_solve_bytes): the F rows
+// (derived from the LDS carve by pointer arithmetic only, so the compiler keeps
+// LDS instructions for it -- an integer round trip would make it a flat pointer)
 __device__ __forceinline__ double* big_fc(const SLds& L) {
-    const unsigned long a = ((unsigned long)(L.flag + 16) + 15ul) & ~15ul;
-    return (double*)a;
+    char* c = (char*)(L.flag + 16);
+    c += (16u - ((unsigned)(unsigned long)c & 15u)) & 15u;
+    return A16((double*)c);
 }
 
-template <int NBM, int K, int CS, int RS>
+template <int SL, int K, int CS, int RS>
 __global__ __launch_bounds__(TB, 1) void k_solve_b(KParams p, double* __restrict__ xo, double* __restrict__ yo,
                                                    int factor_only) {
     const int tid = threadIdx.x;
@@ -115,7 +400,10 @@ __global__ __launch_bounds__(TB, 1) void k_solve_b(KParams p, double* __restrict
     double* Z = C.Z;
     double* dY = C.dY;
     double* Fc = big_fc(L);
+    double* Gc = Fc + p.pmeet * amax * FGS;
+    int* toffL = (int*)(Fc + big_fg_len(p));  // the plan's toff[], after the F/G region
     const double* Fg = p.F + b * (long)nb * SS;
+    const double* Hg = p.H + b * (long)nb * SS;
     const double* Sg = p.Si + b * (long)nb * SS;
 
     if (p.err[b]) {  // invalid data (flagged by setup/update): NaN outputs
@@ -155,6 +443,8 @@ __global__ __launch_bounds__(TB, 1) void k_solve_b(KParams p, double* __restrict
     }
     if (tid < 16) L.res[tid] = 0.0;
     if (tid < 4) L.flag[tid] = 0;
+    for (int k = tid; k < nb; k += TB) toffL[k] = p.toff[k];
+    for (int e = tid; e < 2 * npad; e += TB) L.cor[e] = 0.0;  // corT | corB of the sweep (cor, tv)
 
     int status = MPCQP_UNSOLVED_, rho_updates = 0, iter = 0, info_iter = 0;
     bool can_check = false, need_factor = true;
@@ -170,7 +460,7 @@ __global__ __launch_bounds__(TB, 1) void k_solve_b(KParams p, double* __restrict
         __syncthreads();
         if (need_factor) {  // start, and after a rho change
             need_factor = false;
-            const bool ok = factorize_nl<TB>(p.self, b, rho);
+            const bool ok = factorize2_nl(p.self, b, rho, Fc);  // scratch tiles in the F/G region
             if (!ok) {
                 if (iter == 0) {
                     for (int j = tid; j < n; j += TB) if (xo) xo[b * n + j] = __builtin_nan("");
@@ -186,8 +476,8 @@ __global__ __launch_bounds__(TB, 1) void k_solve_b(KParams p, double* __restrict
             PH(0)
         }
         // ---- run state (re-derived at every run start; nothing but scalars lives across calls) ----
-        BigFactor<NBM> RF;
-        RF.load(nb, amax, Fg, Sg, Fc);
+        TwoSided<SL> RF;
+        RF.load(nb, p.pmeet, amax, p.bmax, Fg, Hg, Sg, Fc, Gc);
         int cvar[CS];
         Gather<K> cg[CS];
 #pragma unroll
@@ -229,7 +519,11 @@ __global__ __launch_bounds__(TB, 1) void k_solve_b(KParams p, double* __restrict
             }
             __syncthreads();
             PH(1)
-            big_solve<NBM>(RF, nb, amax, Fc, L.rb, L.xt);
+#ifdef MPCQP_PHASE_PROF
+            twisted_solve<SL>(RF, p, Fc, Gc, toffL, L.rb, L.xt, L.cor, L.tv, prof ? L.pacc : nullptr);
+#else
+            twisted_solve<SL>(RF, p, Fc, Gc, toffL, L.rb, L.xt, L.cor, L.tv, nullptr);
+#endif
             PH(2)
             // z~ = A x~ ; relaxed + projected z ; y ; next w.   x update; deltas for the checks.
 #pragma unroll
@@ -315,7 +609,7 @@ __global__ __launch_bounds__(TB, 1) void k_solve_b(KParams p, double* __restrict
 #pragma unroll
             for (int k = 0; k < 6; ++k) p.prof[b * kProfSlots + k] = L.pacc[k];
 #pragma unroll
-            for (int k = 8; k < 12; ++k) p.prof[b * kProfSlots + k] = L.pacc[k];
+            for (int k = 8; k < 15; ++k) p.prof[b * kProfSlots + k] = L.pacc[k];
             p.prof[b * kProfSlots + 6] = clock64() - t0c;
             p.prof[b * kProfSlots + 7] = wall_clock64() - t0w;
         }
@@ -325,13 +619,13 @@ __global__ __launch_bounds__(TB, 1) void k_solve_b(KParams p, double* __restrict
 }
 
 size_t lds_solve_bytes_big(const KParams& p) {
-    return lds_solve_bytes(p) + 16 + sizeof(double) * (size_t)(p.nb - 1) * p.amax * S;
+    return lds_solve_bytes(p) + 16 + sizeof(double) * (size_t)big_fg_len(p) + sizeof(int) * (size_t)p.nb;
 }
 
-template <int NBM, int K, int CS, int RS>
+template <int SL, int K, int CS, int RS>
 static hipError_t go_b(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st) {
     const size_t lds = lds_solve_bytes_big(p);
-    auto k = k_solve_b<NBM, K, CS, RS>;
+    auto k = k_solve_b<SL, K, CS, RS>;
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(TB), lds, st, p, xo, yo, fo);
@@ -340,9 +634,9 @@ static hipError_t go_b(const KParams& p, long B, double* xo, double* yo, int fo,
 
 hipError_t launch_solve_big(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st) {
     switch (p.variant) {
-        case 11: return go_b<12, 8, 1, 2>(p, B, xo, yo, factor_only, st);
-        case 12: return go_b<18, 8, 2, 2>(p, B, xo, yo, factor_only, st);
-        case 13: return go_b<24, 8, 2, 3>(p, B, xo, yo, factor_only, st);
+        case 11: return go_b<7, 8, 1, 2>(p, B, xo, yo, factor_only, st);    // nb <= 12
+        case 12: return go_b<10, 8, 2, 2>(p, B, xo, yo, factor_only, st);   // nb <= 18
+        case 13: return go_b<13, 8, 2, 3>(p, B, xo, yo, factor_only, st);   // nb <= 24
         default: return hipErrorInvalidValue;
     }
 }
