@@ -72,6 +72,8 @@ typedef struct {
     double adaptive_rho_tolerance;
     int32_t max_iter, scaling, check_termination, warm_start;
     int32_t adaptive_rho, adaptive_rho_interval, scaled_termination, polish, verbose;
+    double delta;                 /* polish regularisation (OSQP default 1e-6) */
+    int32_t polish_refine_iter;   /* polish iterative-refinement steps (OSQP default 3) */
 } mpcqp_settings;
 
 typedef struct {
@@ -113,6 +115,11 @@ int mpcqp_solve_batch(mpcqp_handle *h, double *x, double *y, int32_t *status, in
 int mpcqp_get_info_batch(mpcqp_handle *h, double *obj_val, double *pri_res, double *dua_res,
                          double *rho_estimate, int32_t *rho_updates);
 /* infeasibility certificates of the last solve (OSQP res.prim_inf_cert / dua_inf_cert) */
+/* res.info.status_polish per instance (osqp polish.c, run after the solve when
+ * settings.polish): 0 not run (status not "solved" or polish off), 1 the polished
+ * solution was taken (x, y, obj_val, pri_res, dua_res are the polished ones), -1
+ * polishing did not improve the residuals (the ADMM solution stands). */
+int mpcqp_get_polish_status(mpcqp_handle *h, int32_t *status_polish);
 int mpcqp_get_certificates(mpcqp_handle *h, double *prim_inf_cert, double *dual_inf_cert);
 
 /* ---- device-resident entry points (single-device handles) ---- */

@@ -316,6 +316,7 @@ struct orc_work {
 };
 
 void orc_default_settings(orc_settings *s) {
+    s->delta = 1e-6; s->polish = 0; s->polish_refine_iter = 3;
     s->rho = 0.1; s->sigma = 1e-6; s->alpha = 1.6;
     s->eps_abs = 1e-3; s->eps_rel = 1e-3; s->eps_prim_inf = 1e-4; s->eps_dual_inf = 1e-4;
     s->adaptive_rho_tolerance = 5.0; s->adaptive_rho_fraction = 0.4;
@@ -898,6 +899,104 @@ static void store_solution(orc_work *w) {
     }
 }
 
+/* ---- polish.c (OSQP 0.6) restated ----
+ * Guess the active constraints from the ADMM iterate (form_Ared), solve the
+ * reduced KKT system [[P + delta I, Ared'], [Ared, -delta I]] [x; y_red] =
+ * [-q; l_low; u_upp] with polish_refine_iter steps of iterative refinement against
+ * the unregularised matrix, map y_red back, project (z, y) onto the normal cone,
+ * and keep the polished point only if it lowers the residuals (or one of them is
+ * already below 1e-10).  All on the scaled data, before store_solution. */
+static void polish(orc_work *w) {
+    int n = w->n, m = w->m;
+    int *A_to_low = (int *)malloc(sizeof(int) * (m ? m : 1)), *A_to_upp = (int *)malloc(sizeof(int) * (m ? m : 1));
+    int *low_to_A = (int *)malloc(sizeof(int) * (m ? m : 1)), *upp_to_A = (int *)malloc(sizeof(int) * (m ? m : 1));
+    int n_low = 0, n_upp = 0;
+    for (int j = 0; j < m; ++j) {
+        if (w->z[j] - w->l[j] < -w->y[j]) { low_to_A[n_low] = j; A_to_low[j] = n_low++; }
+        else A_to_low[j] = -1;
+    }
+    for (int j = 0; j < m; ++j) {
+        if (w->u[j] - w->z[j] < w->y[j]) { upp_to_A[n_upp] = j; A_to_upp[j] = n_upp++; }
+        else A_to_upp[j] = -1;
+    }
+    int mred = n_low + n_upp;
+    /* Ared (CSC, column by column: lower-active copy, then upper-active copy) */
+    int nnz = 0;
+    for (int p = 0; p < w->Ap[n]; ++p) nnz += (A_to_low[w->Ai[p]] >= 0) + (A_to_upp[w->Ai[p]] >= 0);
+    int *Rp = (int *)calloc(n + 1, sizeof(int)), *Ri = (int *)malloc(sizeof(int) * (nnz ? nnz : 1));
+    double *Rx = (double *)malloc(sizeof(double) * (nnz ? nnz : 1));
+    int q_ = 0;
+    for (int j = 0; j < n; ++j) {
+        for (int p = w->Ap[j]; p < w->Ap[j + 1]; ++p) {
+            int i = w->Ai[p];
+            if (A_to_low[i] >= 0) { Ri[q_] = A_to_low[i]; Rx[q_++] = w->Ax[p]; }
+            if (A_to_upp[i] >= 0) { Ri[q_] = A_to_upp[i] + n_low; Rx[q_++] = w->Ax[p]; }
+        }
+        Rp[j + 1] = q_;
+    }
+    double *dinv = dalloc(mred), *rhs = dalloc(n + mred), *sol = dalloc(n + mred), *r2 = dalloc(n + mred);
+    for (int i = 0; i < mred; ++i) dinv[i] = w->set.delta;
+    kkt_t *k = NULL;
+    int e = kkt_init(&k, n, mred, w->Pp, w->Pi, w->Px, Rp, Ri, Rx, w->set.delta, dinv);
+    if (e) {
+        w->info.status_polish = -1;
+    } else {
+        for (int j = 0; j < n; ++j) rhs[j] = -w->q[j];
+        for (int i = 0; i < n_low; ++i) rhs[n + i] = w->l[low_to_A[i]];
+        for (int i = 0; i < n_upp; ++i) rhs[n + n_low + i] = w->u[upp_to_A[i]];
+        memcpy(sol, rhs, sizeof(double) * (n + mred));
+        kkt_solve(k, sol);
+        for (int it = 0; it < w->set.polish_refine_iter; ++it) {
+            /* r2 = rhs - [[P, Ared'], [Ared, 0]] sol */
+            memcpy(r2, rhs, sizeof(double) * (n + mred));
+            sym_mat_vec(w, sol, w->Pxv);
+            for (int j = 0; j < n; ++j) r2[j] -= w->Pxv[j];
+            for (int j = 0; j < n; ++j)
+                for (int p = Rp[j]; p < Rp[j + 1]; ++p) {
+                    r2[j] -= Rx[p] * sol[n + Ri[p]];
+                    r2[n + Ri[p]] -= Rx[p] * sol[j];
+                }
+            kkt_solve(k, r2);
+            for (int j = 0; j < n + mred; ++j) sol[j] += r2[j];
+        }
+        double *px = dalloc(n), *pz = dalloc(m), *py = dalloc(m);
+        memcpy(px, sol, sizeof(double) * n);
+        mat_vec(n, w->Ap, w->Ai, w->Ax, m, px, pz, 0);
+        for (int j = 0; j < m; ++j) {
+            if (mred == 0) py[j] = 0.0;
+            else if (A_to_low[j] >= 0) py[j] = sol[n + A_to_low[j]];
+            else if (A_to_upp[j] >= 0) py[j] = sol[n + n_low + A_to_upp[j]];
+            else py[j] = 0.0;
+        }
+        for (int j = 0; j < m; ++j) {  /* project_normalcone */
+            double t = pz[j] + py[j];
+            pz[j] = dmin(dmax(t, w->l[j]), w->u[j]);
+            py[j] = t - pz[j];
+        }
+        double pobj = compute_obj_val(w, px);
+        double ppri = m == 0 ? 0.0 : compute_pri_res(w, px, pz);
+        double pdua = compute_dua_res(w, px, py);
+        int ok = (ppri < w->info.pri_res && pdua < w->info.dua_res) ||
+                 (ppri < w->info.pri_res && w->info.dua_res < 1e-10) ||
+                 (pdua < w->info.dua_res && w->info.pri_res < 1e-10);
+        if (ok) {
+            w->info.obj_val = pobj;
+            w->info.pri_res = ppri;
+            w->info.dua_res = pdua;
+            w->info.status_polish = 1;
+            memcpy(w->x, px, sizeof(double) * n);
+            memcpy(w->z, pz, sizeof(double) * m);
+            memcpy(w->y, py, sizeof(double) * m);
+        } else {
+            w->info.status_polish = -1;
+        }
+        free(px); free(pz); free(py);
+        kkt_free(k);
+    }
+    free(dinv); free(rhs); free(sol); free(r2); free(Rp); free(Ri); free(Rx);
+    free(A_to_low); free(A_to_upp); free(low_to_A); free(upp_to_A);
+}
+
 int orc_solve(orc_work *w) {
     int iter, can_check = 0;
     int compute_cost = 0; /* verbose off */
@@ -940,6 +1039,8 @@ int orc_solve(orc_work *w) {
         if (!check_termination(w, 1)) w->info.status_val = ORC_MAX_ITER_REACHED;
     }
     w->info.rho_estimate = compute_rho_estimate(w);
+    w->info.status_polish = 0;
+    if (w->set.polish && w->info.status_val == ORC_SOLVED) polish(w);
     store_solution(w);
     return 0;
 }

@@ -14,7 +14,9 @@
  *   algorithm   published OSQP 0.6 (Stellato et al., "OSQP: an operator splitting
  *               solver for quadratic programs", Math. Prog. Comp. 2020), defaults:
  *               rho 0.1, sigma 1e-6, alpha 1.6, eps 1e-3, max_iter 4000, scaling 10,
- *               check_termination 25, adaptive rho (tolerance 5), polish off.
+ *               check_termination 25, adaptive rho (tolerance 5), polish off (when
+ *               enabled: OSQP 0.6 polish.c -- active-set guess, reduced quasi-definite
+ *               KKT with delta regularisation, iterative refinement, acceptance test).
  *
  * Parity status: OSQP outputs are not available in this environment, so iterate
  * parity against OSQP itself is UNPINNED.  The restatement is pinned by
@@ -61,11 +63,14 @@ typedef struct {
     double adaptive_rho_tolerance, adaptive_rho_fraction;
     int max_iter, scaling, check_termination, warm_start;
     int adaptive_rho, adaptive_rho_interval, scaled_termination;
+    double delta;                   /* polish regularisation (OSQP default 1e-6) */
+    int polish, polish_refine_iter; /* polish off / 3 refinement steps by default */
 } orc_settings;
 
 typedef struct {
     int iter, status_val, rho_updates;
     double obj_val, pri_res, dua_res, rho_estimate;
+    int status_polish;              /* 0 not run, 1 polished solution taken, -1 rejected */
 } orc_info;
 
 typedef struct orc_work orc_work;

@@ -43,6 +43,7 @@ class _Settings(C.Structure):
         ("max_iter", C.c_int), ("scaling", C.c_int), ("check_termination", C.c_int),
         ("warm_start", C.c_int), ("adaptive_rho", C.c_int),
         ("adaptive_rho_interval", C.c_int), ("scaled_termination", C.c_int),
+        ("delta", C.c_double), ("polish", C.c_int), ("polish_refine_iter", C.c_int),
     ]
 
 
@@ -50,7 +51,7 @@ class _Info(C.Structure):
     _fields_ = [
         ("iter", C.c_int), ("status_val", C.c_int), ("rho_updates", C.c_int),
         ("obj_val", C.c_double), ("pri_res", C.c_double), ("dua_res", C.c_double),
-        ("rho_estimate", C.c_double),
+        ("rho_estimate", C.c_double), ("status_polish", C.c_int),
     ]
 
 
@@ -117,9 +118,7 @@ def make_settings(**kw) -> _Settings:
     s = _Settings()
     lib().orc_default_settings(C.byref(s))
     for k, v in kw.items():
-        if k in ("verbose", "polish"):
-            if k == "polish" and v:
-                raise ValueError("polish is not restated by the oracle")
+        if k == "verbose":
             continue
         if k not in _SETTING_KEYS:
             raise ValueError(f"unknown setting {k}")
@@ -193,7 +192,8 @@ class OSQP:
         inf = SimpleNamespace(iter=info.iter, status_val=info.status_val,
                               status=STATUS_STR.get(info.status_val, "unknown"),
                               obj_val=info.obj_val, pri_res=info.pri_res, dua_res=info.dua_res,
-                              rho_estimate=info.rho_estimate, rho_updates=info.rho_updates)
+                              rho_estimate=info.rho_estimate, rho_updates=info.rho_updates,
+                              status_polish=info.status_polish)
         return SimpleNamespace(x=x, y=y, info=inf, prim_inf_cert=pc, dual_inf_cert=dc)
 
     def nnz_L(self):

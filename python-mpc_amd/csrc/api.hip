@@ -134,7 +134,7 @@ size_t workspace_bytes(const Plan& pl, long B, bool with_io) {
     carve<double>(off, B * m); carve<double>(off, B * n);              // certificates
     for (int i = 0; i < 4; ++i) carve<double>(off, B);
     carve<signed char>(off, B * m);
-    for (int i = 0; i < 4; ++i) carve<int>(off, B);
+    for (int i = 0; i < 5; ++i) carve<int>(off, B);
     carve<long long>(off, B * kProfSlots);
     carve<KParams>(off, 1);
     if (with_io) {
@@ -186,6 +186,7 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
     k.status = (int*)(base + carve<int>(off, B));
     k.iter = (int*)(base + carve<int>(off, B));
     k.rho_upd = (int*)(base + carve<int>(off, B));
+    k.pstat = (int*)(base + carve<int>(off, B));
     k.err = (int*)(base + carve<int>(off, B));
     k.prof = nullptr;
     if (const char* ev = getenv("MPCQP_PHASE_PROF"); ev && ev[0] == '1')
@@ -208,6 +209,7 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
     k.rho_tol = st.adaptive_rho_tolerance;
     k.max_iter = st.max_iter; k.scaling = st.scaling; k.check_term = st.check_termination;
     k.warm_start = st.warm_start; k.adaptive_rho = st.adaptive_rho; k.scaled_term = st.scaled_termination;
+    k.polish = st.polish; k.refine_iter = st.polish_refine_iter; k.delta = st.delta;
     int interval = st.adaptive_rho_interval;
     if (st.adaptive_rho && interval == 0) interval = st.check_termination ? 4 * st.check_termination : 100;
     k.rho_interval = interval;
@@ -233,7 +235,7 @@ int validate_settings(const mpcqp_settings& s) {
         !(s.alpha > 0 && s.alpha < 2) || s.scaling < 0 || s.check_termination < 0 ||
         s.adaptive_rho_interval < 0 || !(s.adaptive_rho_tolerance >= 1))
         return fail(MPCQP_EINVAL, "invalid settings");
-    if (s.polish) return fail(MPCQP_EUNSUPPORTED, "polish is not supported (the reference never enables it)");
+    if (s.polish && (!(s.delta > 0) || s.polish_refine_iter < 0)) return fail(MPCQP_EINVAL, "invalid polish settings");
     return 0;
 }
 
@@ -315,7 +317,7 @@ void mpcqp_default_settings(mpcqp_settings* s) {
     s->adaptive_rho_tolerance = 5.0;
     s->max_iter = 4000; s->scaling = 10; s->check_termination = 25; s->warm_start = 1;
     s->adaptive_rho = 1; s->adaptive_rho_interval = 0; s->scaled_termination = 0; s->polish = 0;
-    s->verbose = 0;
+    s->verbose = 0; s->delta = 1e-6; s->polish_refine_iter = 3;
 }
 
 const char* mpcqp_last_error(void) { return g_err.c_str(); }
@@ -426,6 +428,18 @@ int mpcqp_get_info_batch(mpcqp_handle* h, double* obj_val, double* pri_res, doub
         if (dua_res) HIPCHK(hipMemcpy(dua_res + s.b0, s.kp.dua, sizeof(double) * s.B, hipMemcpyDeviceToHost));
         if (rho_estimate) HIPCHK(hipMemcpy(rho_estimate + s.b0, s.kp.rho_est, sizeof(double) * s.B, hipMemcpyDeviceToHost));
         if (rho_updates) HIPCHK(hipMemcpy(rho_updates + s.b0, s.kp.rho_upd, sizeof(int) * s.B, hipMemcpyDeviceToHost));
+    }
+    return 0;
+}
+
+int mpcqp_get_polish_status(mpcqp_handle* h, int32_t* status_polish) {
+    if (!h || !status_polish) return fail(MPCQP_EINVAL, "NULL argument");
+    for (auto& s : h->shards) {
+        HIPCHK(hipSetDevice(s.dev));
+        if (h->set.polish)
+            HIPCHK(hipMemcpy(status_polish + s.b0, s.kp.pstat, sizeof(int) * s.B, hipMemcpyDeviceToHost));
+        else
+            std::fill(status_polish + s.b0, status_polish + s.b0 + s.B, 0);
     }
     return 0;
 }

@@ -44,8 +44,10 @@ struct KParams {
     const struct KParams* self;  // device copy of this block (read by the out-of-line device functions)
     long long* prof;  // optional per-instance phase timers (MPCQP_PHASE_PROF=1), kProfSlots each
     // settings
-    double sigma, alpha, eps_abs, eps_rel, eps_pinf, eps_dinf, rho0, rho_tol;
+    double sigma, alpha, eps_abs, eps_rel, eps_pinf, eps_dinf, rho0, rho_tol, delta;
     int max_iter, scaling, check_term, warm_start, adaptive_rho, rho_interval, scaled_term;
+    int polish, refine_iter;
+    int* pstat;  // per instance: 0 polish not run, 1 polished solution taken, -1 rejected
 };
 
 size_t lds_setup_bytes(const KParams& p);
@@ -65,6 +67,8 @@ int solve_mode(int variant);
 int solve_threads(int variant);  // workgroup size of the variant's kernel
 bool variant_fits(const KParams& p, int variant);
 hipError_t launch_solve(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st);
+// solution polishing (OSQP 0.6 polish.c) after the solve; launch_solve runs it when p.polish
+hipError_t launch_polish(const KParams& p, long B, double* xo, double* yo, hipStream_t st);
 // one-wave-per-QP kernel (solve_wave.hip), variants 8 and 9
 hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st);
 // 512-thread long-horizon kernel (solve_big.hip), variants 11-13

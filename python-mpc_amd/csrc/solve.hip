@@ -489,6 +489,183 @@ __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ 
 #undef PH
 }
 
+// ------------------------------------------------------------------ polish --
+// OSQP 0.6 polish.c on the device, after the solve, on the scaled data (osqp_solve
+// calls polish() when settings.polish and the status is "solved"; the reference
+// never enables it -- SURVEY.md §8f F4, API parity).  The reduced KKT system
+//   [[P + delta I, Ared'], [Ared, -delta I]] [x; y_red] = [-q; b_red]
+// (Ared: the rows guessed active at the ADMM point -- lower-active z - l < -y,
+// upper-active u - z < y, a row active at both ends appears twice; b_red their
+// active bounds) is solved in its eliminated form
+//   (P + delta I + Ared' Ared / delta) x = -q + Ared' b_red / delta,
+//   y_red = (Ared x - b_red) / delta,
+// which has the block-tridiagonal structure of the ADMM system (factorize<POL>).
+// Iterative refinement against the unregularised matrix (polish_refine_iter steps)
+// removes the delta error as OSQP's does.  Then y from y_red, the normal-cone
+// projection of (A x, y), the residuals and OSQP's acceptance test; outputs, the
+// warm-start iterates and the info are replaced only when the polished point is
+// accepted.  pstat: 0 not run (status not solved), 1 accepted, -1 rejected.
+
+// x~ = K_pol^{-1} rb (rb overwritten) with the mode-1 factor in the workspace:
+// F_k rows < amax, S_k^{-1}.  Block Thomas, 2 nb - 1 barriers.
+__device__ void pol_solve(const KParams& p, const double* __restrict__ Fg, const double* __restrict__ Sg,
+                          double* rb, double* xt) {
+    const int tid = threadIdx.x, i = tid >> 3, jg = tid & 7, nb = p.nb, amax = p.amax;
+    for (int k = 0; k < nb; ++k) {
+        const double* v = rb + k * S;
+        const double* Sk = Sg + (long)k * SS + i * S;
+        double a = 0.0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) a += Sk[jg + 8 * c] * v[jg + 8 * c];
+        const double t = reduce8(a);
+        if (k + 1 < nb && i < amax) {
+            const double* Fk = Fg + (long)(k + 1) * SS + i * S;
+            double f = 0.0;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) f += Fk[jg + 8 * c] * v[jg + 8 * c];
+            f = reduce8(f);
+            if (jg == 0) rb[(k + 1) * S + i] -= f;
+        }
+        if (jg == 0) xt[k * S + i] = t;
+        __syncthreads();
+    }
+    for (int k = nb - 2; k >= 0; --k) {  // x_k = t_k - F_{k+1}' x_{k+1}[0, amax)
+        const double* F1 = Fg + (long)(k + 1) * SS;
+        double a = 0.0;
+        for (int r = jg; r < amax; r += 8) a += F1[r * S + i] * xt[(k + 1) * S + r];
+        a = reduce8(a);
+        if (jg == 0) xt[k * S + i] -= a;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(T) void k_polish(KParams p, double* __restrict__ xo, double* __restrict__ yo) {
+    const int tid = threadIdx.x;
+    const long b = blockIdx.x;
+    const int n = p.n, m = p.m, npad = p.npad, nnzP = p.nnzP, nnzA = p.nnzA;
+    if (p.status[b] != MPCQP_SOLVED_) {
+        if (tid == 0) p.pstat[b] = 0;
+        return;
+    }
+    SL2 C = carve(p);
+    SLds& L = C.L;
+    double* X = C.X;   // polish x
+    double* YL = C.Z;  // duals of the lower-active copies
+    double* AX = C.dY;
+    const double cinv = p.scal[b * 4 + 1], idelta = 1.0 / p.delta;
+    const double* Fg = p.F + b * (long)p.nb * SS;
+    const double* Sg = p.Si + b * (long)p.nb * SS;
+    for (int e = tid; e < nnzA; e += T) L.Acsc[e] = p.Ax[b * nnzA + p.acsc_v[e]];
+    if (tid == 0) L.Acsc[nnzA] = 0.0;
+    for (int v = tid; v < nnzP; v += T) L.Pv[v] = p.Px[b * nnzP + v];
+    if (tid == 0) L.Pv[nnzP] = 0.0;
+    for (int i = tid; i < m; i += T) {  // form_Ared: the active-set guess
+        const double lo = p.l[b * m + i], up = p.u[b * m + i], z = p.z[b * m + i], y = p.y[b * m + i];
+        L.lo[i] = lo;
+        L.up[i] = up;
+        L.ct[i] = (signed char)((z - lo < -y ? 1 : 0) | (up - z < y ? 2 : 0));
+    }
+    for (int pc = tid; pc < npad; pc += T) L.qv[pc] = p.q[b * npad + pc];
+    __syncthreads();
+    const bool ok = factorize_pol_nl<T>(p.self, b);
+    if (!ok) {  // the reduced KKT matrix is not quasi-definite: polish fails
+        if (tid == 0) p.pstat[b] = -1;
+        return;
+    }
+    double* YU = L.ys;  // duals of the upper-active copies (V is free after the factorisation)
+    for (int pc = tid; pc < npad; pc += T) X[pc] = 0.0;
+    for (int i = tid; i < m; i += T) { YL[i] = 0.0; YU[i] = 0.0; }
+    __syncthreads();
+    for (int it = 0; it <= p.refine_iter; ++it) {
+        // residual of [[P, Ared'], [Ared, 0]] [x; y_red] = [-q; b_red], folded into the
+        // eliminated rhs: r_x + Ared' r_y / delta
+        for (int i = tid; i < m; i += T) {
+            const int fl = L.ct[i];
+            const double ax = row_dot(p, L.Acsc, X, i);
+            AX[i] = ax;
+            const double rl = L.lo[i] - ax, ru = L.up[i] - ax;
+            L.w[i] = ((fl & 1) ? rl * idelta - YL[i] : 0.0) + ((fl & 2) ? ru * idelta - YU[i] : 0.0);
+        }
+        __syncthreads();
+        for (int pc = tid; pc < npad; pc += T)
+            L.rb[pc] = p.pad_var[pc] >= 0 ? (-L.qv[pc] - psym_dot(p, L.Pv, X, pc)) + col_dot(p, L.Acsc, L.w, pc)
+                                          : 0.0;
+        __syncthreads();
+        pol_solve(p, Fg, Sg, L.rb, L.xt);
+        for (int i = tid; i < m; i += T) {  // dy = (Ared dx - r_y) / delta
+            const int fl = L.ct[i];
+            if (!fl) continue;
+            const double adx = row_dot(p, L.Acsc, L.xt, i), ax = AX[i];
+            if (fl & 1) YL[i] += (adx - (L.lo[i] - ax)) * idelta;
+            if (fl & 2) YU[i] += (adx - (L.up[i] - ax)) * idelta;
+        }
+        __syncthreads();
+        for (int pc = tid; pc < npad; pc += T) X[pc] += L.xt[pc];
+        __syncthreads();
+    }
+    // polished (x, z, y): y from y_red (lower copy first, as get_ypol_from_yred),
+    // then project_normalcone; residuals as update_info(polish = 1)
+    const double* Eg = p.E + b * m;
+    const double* Dg = p.D + b * npad;
+    const bool unscaled = p.scaling && !p.scaled_term;
+    double nrm[2] = {0.0, 0.0};
+    double* Zp = AX;     // polished z
+    double* Yp = L.w;    // polished y
+    for (int i = tid; i < m; i += T) {
+        const int fl = L.ct[i];
+        const double ax = row_dot(p, L.Acsc, X, i);
+        const double yv = (fl & 1) ? YL[i] : ((fl & 2) ? YU[i] : 0.0);
+        const double t = ax + yv;
+        const double zn = cmin(cmax(t, L.lo[i]), L.up[i]);
+        Zp[i] = zn;
+        Yp[i] = t - zn;
+        const double pr = ax - zn;
+        nrm[0] = cmax(nrm[0], fabs(unscaled ? pr / Eg[i] : pr));
+    }
+    __syncthreads();
+    double obj[1] = {0.0};
+    for (int pc = tid; pc < npad; pc += T) {
+        if (p.pad_var[pc] < 0) continue;
+        const double px = psym_dot(p, L.Pv, X, pc), aty = col_dot(p, L.Acsc, Yp, pc), q = L.qv[pc];
+        const double d = (q + px) + aty;
+        nrm[1] = cmax(nrm[1], fabs(unscaled ? d / Dg[pc] : d));
+        obj[0] += X[pc] * (0.5 * px + q);
+    }
+    block_max<T>(nrm, L.red);
+    block_sum<T>(obj, L.red);
+    const double ppri = m == 0 ? 0.0 : nrm[0], pdua = unscaled ? cinv * nrm[1] : nrm[1];
+    const double pri0 = p.pri[b], dua0 = p.dua[b];
+    const bool take = (ppri < pri0 && pdua < dua0) || (ppri < pri0 && dua0 < 1e-10) || (pdua < dua0 && pri0 < 1e-10);
+    if (take) {
+        for (int pc = tid; pc < npad; pc += T) {
+            const int j = p.pad_var[pc];
+            if (j >= 0 && xo) xo[b * n + j] = p.scaling ? Dg[pc] * X[pc] : X[pc];
+            p.x[b * npad + pc] = X[pc];
+        }
+        for (int i = tid; i < m; i += T) {
+            if (yo) yo[b * m + i] = p.scaling ? (Eg[i] * Yp[i]) * cinv : Yp[i];
+            p.y[b * m + i] = Yp[i];
+            p.z[b * m + i] = Zp[i];
+        }
+    }
+    if (tid == 0) {
+        p.pstat[b] = take ? 1 : -1;
+        if (take) {
+            p.obj[b] = p.scaling ? obj[0] * cinv : obj[0];
+            p.pri[b] = ppri;
+            p.dua[b] = pdua;
+        }
+    }
+}
+
+hipError_t launch_polish(const KParams& p, long B, double* xo, double* yo, hipStream_t st) {
+    const size_t lds = lds_solve_bytes(p);
+    hipError_t e = hipFuncSetAttribute((const void*)k_polish, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_polish, dim3((unsigned)B), dim3(T), lds, st, p, xo, yo);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------ launcher --
 size_t lds_solve_bytes(const KParams& p) {
     const size_t mp = (size_t)solve_mpad(p.m);
@@ -563,7 +740,8 @@ int solve_mode(int variant) {  // what factorize stores for the variant (KParams
     }
 }
 
-hipError_t launch_solve(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st) {
+static hipError_t launch_solve_only(const KParams& p, long B, double* xo, double* yo, int factor_only,
+                                    hipStream_t st) {
     const size_t lds = lds_solve_bytes(p);
     switch (p.variant) {
         case 0: return go<4, 8, 6, 1, 1, 4, true>(p, B, xo, yo, factor_only, st, lds);
@@ -578,6 +756,12 @@ hipError_t launch_solve(const KParams& p, long B, double* xo, double* yo, int fa
         case 11: case 12: case 13: return launch_solve_big(p, B, xo, yo, factor_only, st);
         default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_solve(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st) {
+    hipError_t e = launch_solve_only(p, B, xo, yo, factor_only, st);
+    if (e != hipSuccess || factor_only || !p.polish) return e;
+    return launch_polish(p, B, xo, yo, st);
 }
 
 }  // namespace mpcqp

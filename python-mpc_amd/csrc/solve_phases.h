@@ -143,11 +143,14 @@ __device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restri
 //   2: the blocks of L^{-1}:  G_kj = (-1)^{k-j} F_k F_{k-1} .. F_{j+1}  (j < k), amax x 32
 //      each, in Hg at pair (k, j) -> k(k-1)/2 + j, row stride 32 (three-phase solve).
 // Returns false on a non-positive pivot (OSQP: "problem non convex").
-template <int TT, class KP>
+// POL: the polish system P + delta I + A' diag(w) A instead (solve.hip::k_polish): row
+// weights w_i = (number of active copies of row i, from ct bits 0/1) * rho with
+// rho = 1 / delta, diagonal delta, factor stored as in mode 1.
+template <int TT, class KP, bool POL = false>
 __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, double* __restrict__ Fg,
                                           double* __restrict__ Hg, double* __restrict__ Sg) {
     const int tid = threadIdx.x;
-    const int nb = p.nb, amax = p.amax, ntgt = p.ntgt, tmax = p.term_max, mode = p.mode;
+    const int nb = p.nb, amax = p.amax, ntgt = p.ntgt, tmax = p.term_max, mode = POL ? 1 : p.mode;
     const long gstride = (long)amax * S;
     const int2* __restrict__ tt = (const int2*)p.tterm;
     bool ok = true;
@@ -164,7 +167,7 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
     for (int k = 0; k < nb; ++k) {
         for (int e = tid; e < SS; e += TT) { DK[e] = 0.0; EK[e] = 0.0; }
         __syncthreads();
-        if (tid < S) DK[tid * S + tid] = p.pad_var[k * S + tid] >= 0 ? p.sigma : 1.0;
+        if (tid < S) DK[tid * S + tid] = p.pad_var[k * S + tid] >= 0 ? (POL ? p.delta : p.sigma) : 1.0;
         __syncthreads();
         // every target has one owner: its terms are summed in plan order
 #pragma unroll 1
@@ -174,7 +177,8 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
             for (int j = 0; j < tmax; ++j) {
                 const int2 w = tt[(long)j * ntgt + t];
                 const int a = w.x & 0xFFFF, bb = (int)((unsigned)w.x >> 16), r = w.y;
-                acc += r < 0 ? L.Pv[a] : rho_of(L.ct[r], rho) * L.Acsc[a] * L.Acsc[bb];
+                const double wr = POL ? (double)((L.ct[r] & 1) + ((L.ct[r] >> 1) & 1)) * rho : rho_of(L.ct[r], rho);
+                acc += r < 0 ? L.Pv[a] : wr * L.Acsc[a] * L.Acsc[bb];
             }
             const int tg = p.asm_tgt[t];
             if (tg < SS) DK[tg] += acc;
@@ -687,6 +691,13 @@ __device__ __noinline__ void finalize_nl(const KParams* gp, long b, double* __re
     finalize_ph<TT>(gp, b, xo, yo, cinv, rho, status, info_iter, rho_updates);
 }
 
+template <int TT>
+__device__ __noinline__ bool factorize_pol_nl(const KParams* gp, long b) {
+    KPc& p = kconst(gp);
+    SL2 c = carve(p);
+    return factorize<TT, KPc, true>(p, c.L, 1.0 / p.delta, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
+                                    p.Si + b * (long)p.nb * SS);
+}
 template <int TT>
 __device__ __forceinline__ bool factorize_ph(const KParams* gp, long b, double rho) {
     KPc& p = kconst(gp);

@@ -71,6 +71,7 @@ class _Settings(C.Structure):
         ("warm_start", C.c_int32), ("adaptive_rho", C.c_int32),
         ("adaptive_rho_interval", C.c_int32), ("scaled_termination", C.c_int32),
         ("polish", C.c_int32), ("verbose", C.c_int32),
+        ("delta", C.c_double), ("polish_refine_iter", C.c_int32),
     ]
 
 
@@ -118,6 +119,7 @@ def lib():
     L.mpcqp_solve_batch.argtypes = [vp, dp, dp, i32p, i32p]
     L.mpcqp_get_info_batch.argtypes = [vp, dp, dp, dp, dp, i32p]
     L.mpcqp_get_certificates.argtypes = [vp, dp, dp]
+    L.mpcqp_get_polish_status.argtypes = [vp, i32p]
     L.mpcqp_create.argtypes = [C.c_int32, C.c_int32, i32p, i32p, i32p, i32p, C.c_int64,
                                _P(_Settings), C.c_int32, hp]
     L.mpcqp_setup_device.argtypes = [vp, vp, vp, vp, vp, vp, vp]
@@ -158,7 +160,7 @@ def _check(code, what):
 
 
 _SETTING_NAMES = {f[0] for f in _Settings._fields_}
-_IGNORED = {"linsys_solver", "delta", "polish_refine_iter", "time_limit", "adaptive_rho_fraction"}
+_IGNORED = {"linsys_solver", "time_limit", "adaptive_rho_fraction"}
 
 
 def _make_settings(**kw) -> _Settings:
@@ -313,9 +315,11 @@ class OSQPBatch:
         _check(lib().mpcqp_get_info_batch(h, _dp(obj), _dp(pri), _dp(dua), _dp(rho), _ip(ru)), "info")
         pc = np.empty((B, m)); dc = np.empty((B, n))
         _check(lib().mpcqp_get_certificates(h, _dp(pc), _dp(dc)), "certificates")
+        sp = np.empty(B, np.int32)
+        _check(lib().mpcqp_get_polish_status(h, _ip(sp)), "polish status")
         return SimpleNamespace(x=x, y=y, status_val=st, iter=it, obj_val=obj, pri_res=pri, dua_res=dua,
                                rho_estimate=rho, rho_updates=ru, prim_inf_cert=pc, dual_inf_cert=dc,
-                               solve_time=solve_time,
+                               status_polish=sp, solve_time=solve_time,
                                status=[STATUS.get(int(v), "unknown") for v in st])
 
     def plan_info(self):
@@ -380,13 +384,14 @@ class OSQP:
         r = self._b.solve()
         sv = int(r.status_val[0])
         info = SimpleNamespace(
-            iter=int(r.iter[0]), status=STATUS.get(sv, "unknown"), status_val=sv, status_polish=0,
+            iter=int(r.iter[0]), status=STATUS.get(sv, "unknown"), status_val=sv,
+            status_polish=int(r.status_polish[0]),
             obj_val=float(r.obj_val[0]), pri_res=float(r.pri_res[0]), dua_res=float(r.dua_res[0]),
             setup_time=self._b.setup_time, solve_time=r.solve_time, update_time=self._update_time,
             polish_time=0.0, run_time=r.solve_time, rho_updates=int(r.rho_updates[0]),
             rho_estimate=float(r.rho_estimate[0]))
         return SimpleNamespace(x=r.x[0], y=r.y[0], info=info, prim_inf_cert=r.prim_inf_cert[0],
-                               dua_inf_cert=r.dual_inf_cert[0])
+                               dual_inf_cert=r.dual_inf_cert[0], dua_inf_cert=r.dual_inf_cert[0])
 
 
 class DeviceBatch:

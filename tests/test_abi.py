@@ -44,6 +44,7 @@ def test_default_settings_are_osqp_06():
     assert (s.eps_abs, s.eps_rel, s.eps_prim_inf, s.eps_dual_inf) == (1e-3, 1e-3, 1e-4, 1e-4)
     assert (s.max_iter, s.scaling, s.check_termination, s.warm_start) == (4000, 10, 25, 1)
     assert (s.adaptive_rho, s.adaptive_rho_tolerance, s.polish) == (1, 5.0, 0)
+    assert (s.delta, s.polish_refine_iter) == (1e-6, 3)
 
 
 def _kkt_pattern(P, A):
@@ -102,8 +103,10 @@ def test_setup_validation_errors():
         osqp_amd.OSQP().setup(P, q, A, l, u, max_iter=0)
     with pytest.raises(ValueError):
         osqp_amd.OSQP().setup(P, q[:1], A, l, u)
-    with pytest.raises(NotImplementedError):
-        osqp_amd.OSQP().setup(P, q, A, l, u, polish=True)
+    with pytest.raises(ValueError):
+        osqp_amd.OSQP().setup(P, q, A, l, u, polish=True, delta=-1.0)
+    with pytest.raises(ValueError):
+        osqp_amd.OSQP().setup(P, q, A, l, u, polish=True, polish_refine_iter=-1)
 
 
 def test_no_cpu_fallback_without_device():

@@ -208,3 +208,43 @@ def test_cfg5_warm_started_batch():
     du = np.abs(rg.x[:, b["u_block"]] - bo.x[:, b["u_block"]]).max(axis=1)
     assert np.all(du[same_iter] < U_TOL), du.max()
     assert bo.iter.mean() < r0.iter.mean()
+
+
+@pytest.mark.parametrize("name", ["vanilla_n20.npz", "slack_n20.npz", "dyn_incr_n50.npz", "kin_incr_n40.npz"])
+def test_polish_matches_oracle(golden, name):
+    """polish=True (OSQP 0.6 polish.c): same accept / reject decision
+    as the oracle; an accepted polished point is the reduced KKT solution, so x and y
+    agree to far below the ADMM tolerance."""
+    g = golden(name)
+    if g["q"].ndim == 2:
+        P = g["P"].copy(); A = g["A"].copy()
+        if "Px" in g:
+            P.data = g["Px"][0].copy(); A.data = g["Ax"][0].copy()
+        q, l, u = g["q"][0], g["l"][0], g["u"][0]
+    else:
+        P, A, q, l, u = g["P"], g["A"], g["q"], g["l"], g["u"]
+    s = dict(_settings(g), polish=True)
+    o = pyoracle.OSQP(); o.setup(P, q, A, l, u, **s); ro = o.solve()
+    d = OSQP(); d.setup(P, q, A, l, u, **s); rd = d.solve()
+    assert rd.info.status == ro.info.status and rd.info.iter == ro.info.iter
+    assert rd.info.status_polish == ro.info.status_polish
+    scale = max(1.0, np.abs(ro.x).max())
+    tol = 1e-8 if ro.info.status_polish == 1 else 1e-6
+    assert np.abs(rd.x - ro.x).max() < tol * scale
+    assert np.abs(rd.y - ro.y).max() < 100 * tol * max(1.0, np.abs(ro.y).max())
+    if ro.info.status_polish == 1:
+        assert rd.info.pri_res < 1e-9 and rd.info.dua_res < 1e-9
+
+
+def test_polish_batch_cfg2():
+    b = mpc.make_batch(2, B=256)
+    bo = pyoracle.solve_batch(b["P"], b["A"], b["Px"], b["q"], b["Ax"], b["l"], b["u"], nthreads=16,
+                              warm_start=True, polish=True)
+    bg = OSQPBatch()
+    bg.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], warm_start=True, polish=True)
+    rg = bg.solve()
+    assert (rg.status_polish == 1).mean() > 0.9
+    same = rg.iter == bo.iter
+    assert same.mean() >= 0.99
+    du = np.abs(rg.x[:, b["u_block"]] - bo.x[:, b["u_block"]]).max(axis=1)
+    assert np.all(du[same] < 1e-6), du.max()

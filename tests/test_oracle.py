@@ -147,3 +147,34 @@ def test_oracle_batch_warm_start_matches_single():
         o.warm_start(x=x0[t], y=y0[t])
         r = o.solve()
         assert r.info.iter == rw.iter[t] and np.array_equal(r.x, rw.x[t])
+
+
+@pytest.mark.parametrize("name", ["vanilla_n20.npz", "slack_n20.npz"])
+def test_oracle_polish_reaches_the_optimum(golden, name):
+    """polish (OSQP 0.6 polish.c restated): on the reference's lane-keeping QPs the
+    active-set guess is right, the polished point is accepted and is the exact
+    optimum -- the tight-eps ADMM solution agrees with it."""
+    P, q, A, l, u, s = next(instances(golden, name))
+    o = pyoracle.OSQP()
+    o.setup(P, q, A, l, u, polish=True)
+    r = o.solve()
+    assert r.info.status == "solved" and r.info.status_polish == 1
+    st, pri, comp = kkt_residuals(P, q, A, l, u, r.x, r.y)
+    assert max(st, pri) < 1e-9
+    t = pyoracle.OSQP()
+    t.setup(P, q, A, l, u, eps_abs=1e-11, eps_rel=1e-11, max_iter=200000)
+    rt = t.solve()
+    assert np.abs(r.x - rt.x).max() < 1e-6 * max(1.0, np.abs(rt.x).max())
+
+
+def test_oracle_polish_rejected_keeps_admm_solution(golden):
+    """incremental-dynamic QP: the polished point does not lower both residuals, so
+    OSQP keeps the ADMM iterate (status_polish -1) -- identical to polish off."""
+    P, q, A, l, u, s = next(instances(golden, "dyn_incr_n50.npz"))
+    r = []
+    for pol in (False, True):
+        o = pyoracle.OSQP()
+        o.setup(P, q, A, l, u, polish=pol, warm_start=False)
+        r.append(o.solve())
+    assert r[1].info.status_polish == -1 and r[0].info.status_polish == 0
+    assert np.array_equal(r[0].x, r[1].x)
