@@ -676,7 +676,7 @@ size_t lds_solve_bytes(const KParams& p) {
 }
 
 size_t lds_kernel_bytes(const KParams& p) {
-    return p.variant >= 11 && p.variant <= 13 ? lds_solve_bytes_big(p) : lds_solve_bytes(p);
+    return p.variant >= 11 && p.variant <= 14 ? lds_solve_bytes_big(p) : lds_solve_bytes(p);
 }
 
 template <int NB, int A, int K, int CS, int RS, int W, bool TRI = false>
@@ -711,6 +711,9 @@ bool variant_fits(const KParams& p, int v) {
             return p.nb > 4 && p.nb <= nbm && p.amax <= 16 && p.bmax <= 16 && p.gk <= 8 && csb <= csm && rsb <= rsm &&
                    lds_solve_bytes_big(p) <= 160 * 1024;
         }
+        case 14:
+            return p.nb > 4 && p.nb <= 8 && p.amax <= 16 && p.bmax <= 16 && p.gk <= 8 && p.npad <= 256 &&
+                   p.m <= 256 && lds_solve_bytes_big(p) <= 160 * 1024;
         default: return false;
     }
 }
@@ -727,6 +730,7 @@ int solve_threads(int variant) {
         case 8: case 9: return 64;
         case 10: return 128;
         case 11: case 12: case 13: return kThreadsBig;
+        case 14: return 128;
         default: return T;
     }
 }
@@ -735,7 +739,7 @@ int solve_mode(int variant) {  // what factorize stores for the variant (KParams
     switch (variant) {
         case 0: case 8: case 9: case 10: return 2;
         case 1: case 2: case 3: case 7: return 1;
-        case 11: case 12: case 13: return 3;  // two-sided factor (solve_big.hip)
+        case 11: case 12: case 13: case 14: return 3;  // two-sided factor (solve_big.hip)
         default: return 0;
     }
 }
@@ -753,7 +757,7 @@ static hipError_t launch_solve_only(const KParams& p, long B, double* xo, double
         case 6: return go<0, 32, 16, 8, 8, 1>(p, B, xo, yo, factor_only, st, lds);
         case 7: return go<4, 8, 6, 1, 1, 4, false>(p, B, xo, yo, factor_only, st, lds);
         case 8: case 9: case 10: return launch_solve_wave(p, B, xo, yo, factor_only, st);
-        case 11: case 12: case 13: return launch_solve_big(p, B, xo, yo, factor_only, st);
+        case 11: case 12: case 13: case 14: return launch_solve_big(p, B, xo, yo, factor_only, st);
         default: return hipErrorInvalidValue;
     }
 }

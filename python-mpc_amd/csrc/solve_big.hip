@@ -27,6 +27,8 @@
 // the CPU oracle.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "solve_phases.h"
 
 namespace mpcqp {
@@ -51,11 +53,13 @@ constexpr int FGS = 40;
 // steps instead of nb.  Stored: Sg[k] = S_k^{-1} / M^{-1} / T_k^{-1};  Fg[k] rows
 // < amax = F_k (k = 1..p);  Hg[k] rows < bmax = G_k's tail rows (k = p..nb-2).
 // X2: four scratch tiles besides SLds' three.  False on a non-positive pivot.
-template <class KP>
+template <int TT, class KP>
 __device__ __forceinline__ bool factorize2(const KP& p, SLds& L, double* __restrict__ X2, double rho,
                                            double* __restrict__ Fg, double* __restrict__ Hg,
                                            double* __restrict__ Sg) {
-    const int tid = threadIdx.x, half = tid >> 8, u = tid & 255;
+    constexpr int HT = TT / 2;      // threads per chain
+    constexpr int NF = 16 * S / HT;  // per-thread F / G buffer (amax, bmax <= 16)
+    const int tid = threadIdx.x, half = tid / HT, u = tid % HT;
     const int nb = p.nb, amax = p.amax, bmax = p.bmax, pm = p.pmeet, ntgt = p.ntgt, tmax = p.term_max;
     const int nst = max(pm, nb - 1 - pm);
     const int2* __restrict__ tt = (const int2*)p.tterm;
@@ -92,20 +96,20 @@ __device__ __forceinline__ bool factorize2(const KP& p, SLds& L, double* __restr
         }
     };
     // F_k = E_k S_{k-1}^{-1} (rows < amax) -> f, Fg[k]
-    auto top_f = [&](int k, double (&f)[2]) {
+    auto top_f = [&](int k, double (&f)[NF]) {
         int nf = 0;
 #pragma unroll 1
-        for (int o = u; o < amax * S; o += 256, ++nf) {
+        for (int o = u; o < amax * S; o += HT, ++nf) {
             const int r = o >> 5, j = o & (S - 1);
             double sacc = 0.0;
 #pragma unroll 8
             for (int l = 0; l < S; ++l) sacc += EK[r * S + l] * SP[l * S + j];
-            f[nf & 1] = sacc;
+            f[nf & (NF - 1)] = sacc;
             Fg[(long)k * SS + o] = sacc;
         }
     };
     // G_k = E_{k+1}' T_{k+1}^{-1} on block k's tail rows (E_{k+1} in EKp, T^{-1} in SP2) -> g, Hg[k]
-    auto bot_g = [&](int k, int toff, double (&g)[2], int t0, int stride) {
+    auto bot_g = [&](int k, int toff, double (&g)[NF], int t0, int stride) {
         int ng = 0;
 #pragma unroll 1
         for (int o = t0; o < bmax * S; o += stride, ++ng) {
@@ -113,7 +117,7 @@ __device__ __forceinline__ bool factorize2(const KP& p, SLds& L, double* __restr
             double sacc = 0.0;
 #pragma unroll 1
             for (int r = 0; r < amax; ++r) sacc += EKp[r * S + toff + a] * SP2[r * S + j];
-            g[ng & 1] = sacc;
+            g[ng & (NF - 1)] = sacc;
             Hg[(long)k * SS + o] = sacc;
         }
     };
@@ -145,27 +149,27 @@ __device__ __forceinline__ bool factorize2(const KP& p, SLds& L, double* __restr
         const int kt = s, kb = nb - 1 - s;
         const bool top = half == 0 && s < pm, bot = half == 1 && s < nb - 1 - pm;
         const int toffb = kb < nb - 1 ? p.toff[kb] : 0;
-        if (top) init(kt, DK, EK, u, 256);
-        if (bot) init(kb, DK2, EK2, u, 256);
+        if (top) init(kt, DK, EK, u, HT);
+        if (bot) init(kb, DK2, EK2, u, HT);
         __syncthreads();
-        if (top) assemble(kt, DK, EK, u, 256);
-        if (bot) assemble(kb, DK2, EK2, u, 256);
+        if (top) assemble(kt, DK, EK, u, HT);
+        if (bot) assemble(kb, DK2, EK2, u, HT);
         __syncthreads();
         FPH(8)
-        double f[2] = {0.0, 0.0};
+        double f[NF];
         if (top && kt > 0) top_f(kt, f);
-        if (bot && kb < nb - 1) bot_g(kb, toffb, f, u, 256);
+        if (bot && kb < nb - 1) bot_g(kb, toffb, f, u, HT);
         __syncthreads();  // every read of S_{k-1}^{-1} / T_{k+1}^{-1} done
         {
             int nf = 0;
             if (top && kt > 0)
-                for (int o = u; o < amax * S; o += 256, ++nf) SP[o] = f[nf & 1];
+                for (int o = u; o < amax * S; o += HT, ++nf) SP[o] = f[nf & (NF - 1)];
             if (bot && kb < nb - 1)
-                for (int o = u; o < bmax * S; o += 256, ++nf) SP2[o] = f[nf & 1];
+                for (int o = u; o < bmax * S; o += HT, ++nf) SP2[o] = f[nf & (NF - 1)];
         }
         __syncthreads();
-        if (top && kt > 0) top_corr(DK, u, 256);
-        if (bot && kb < nb - 1) bot_corr(DK2, toffb, u, 256);
+        if (top && kt > 0) top_corr(DK, u, HT);
+        if (bot && kb < nb - 1) bot_corr(DK2, toffb, u, HT);
         __syncthreads();
         FPH(9)
         // wave 0 inverts the top tile, wave 4 the bottom one, at the same time
@@ -176,9 +180,9 @@ __device__ __forceinline__ bool factorize2(const KP& p, SLds& L, double* __restr
             const bool okw = gj_wave<true>(DK, EK, Sg + (long)kt * SS);
             if (tid == 0) okslot[0] = okw ? 1.0 : 0.0;
         }
-        if (tid >= 256 && tid < 320 && botw) {
+        if (tid >= HT && tid < HT + 64 && botw) {
             const bool okw = gj_wave<true>(DK2, EKp, Sg + (long)kb * SS);
-            if (tid == 256) okslot2[0] = okw ? 1.0 : 0.0;
+            if (tid == HT) okslot2[0] = okw ? 1.0 : 0.0;
         }
         __syncthreads();
         if (topw && !(okslot[0] > 0.5)) ok = false;
@@ -194,26 +198,26 @@ __device__ __forceinline__ bool factorize2(const KP& p, SLds& L, double* __restr
     // middle block: both corrections, then its inverse
     {
         const int toffp = pm < nb - 1 ? p.toff[pm] : 0;
-        init(pm, DK, EK, tid, TB);
+        init(pm, DK, EK, tid, TT);
         __syncthreads();
-        assemble(pm, DK, EK, tid, TB);
+        assemble(pm, DK, EK, tid, TT);
         __syncthreads();
         FPH(8)
-        double f[2] = {0.0, 0.0};
+        double f[NF];
         if (half == 0 && pm > 0) top_f(pm, f);
-        if (half == 1 && pm < nb - 1) bot_g(pm, toffp, f, u, 256);
+        if (half == 1 && pm < nb - 1) bot_g(pm, toffp, f, u, HT);
         __syncthreads();
         {
             int nf = 0;
             if (half == 0 && pm > 0)
-                for (int o = u; o < amax * S; o += 256, ++nf) SP[o] = f[nf & 1];
+                for (int o = u; o < amax * S; o += HT, ++nf) SP[o] = f[nf & (NF - 1)];
             if (half == 1 && pm < nb - 1)
-                for (int o = u; o < bmax * S; o += 256, ++nf) SP2[o] = f[nf & 1];
+                for (int o = u; o < bmax * S; o += HT, ++nf) SP2[o] = f[nf & (NF - 1)];
         }
         __syncthreads();
-        if (pm > 0) top_corr(DK, tid, TB);
+        if (pm > 0) top_corr(DK, tid, TT);
         __syncthreads();
-        if (pm < nb - 1) bot_corr(DK, toffp, tid, TB);
+        if (pm < nb - 1) bot_corr(DK, toffp, tid, TT);
         __syncthreads();
         FPH(9)
         double* okslot = EK + 2 * S;
@@ -229,12 +233,12 @@ __device__ __forceinline__ bool factorize2(const KP& p, SLds& L, double* __restr
     return ok;
 }
 
-template <class KP>
+template <int TT, class KP>
 __device__ __noinline__ bool factorize2_nl(const KP* gp, long b, double rho, double* X2) {
     const KPc& p = kconst(gp);
     SL2 C = carve(p);
-    return factorize2(p, C.L, X2, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
-                      p.Si + b * (long)p.nb * SS);
+    return factorize2<TT>(p, C.L, X2, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
+                          p.Si + b * (long)p.nb * SS);
 }
 
 // The factor on chip for the two-sided sweep.  Thread t: half h = t / 256 (0 top,
@@ -372,6 +376,166 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
 #undef SPH
 }
 
+// ---------------------------------------------------------------------------
+// The two-wave variant (k_solve_b<128, ...>: nb <= 8, cfg 3/4's slack layout): one
+// wave per chain, so a sweep step is ordered by the wave's own instruction stream
+// (LDS fences + wave_barrier, no s_barrier) and the two chains run side by side;
+// only the meeting point needs the workgroup.  Lane (i, h) = (lane / 2, lane % 2)
+// holds Inv[s][c] = Inv_s[i][16 h + c] (c < 16) of its chain's slot-s tile; a tile
+// row is a 2-lane sum.  F / G rows live in LDS (FGS stride) for the low-rank updates
+// (rows < amax / bmax, the same lanes) and, transposed, for the backward sweep.
+// rb is updated in place: the destination rows' old values are read off the
+// critical path; the bottom chain's correction of the middle block goes to corB
+// (negated).
+template <int NS>
+struct TwoSidedW {
+    double Inv[NS][16];
+    __device__ __forceinline__ void load(int nb, int pm, int amax, int bmax, const double* __restrict__ Fg,
+                                         const double* __restrict__ Hg, const double* __restrict__ Sg,
+                                         double* __restrict__ Fc, double* __restrict__ Gc) {
+        const int tid = threadIdx.x, wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63,
+                  i = lane >> 1, h = lane & 1;
+        const int nbot = nb - 1 - pm;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const bool have = wv == 0 ? s <= pm : s < nbot;
+            const int k = wv == 0 ? s : nb - 1 - s;
+            const double* src = Sg + (long)k * SS + i * S + 16 * h;
+#pragma unroll
+            for (int c = 0; c < 16; c += 2) {
+                double2 t2 = have ? *(const double2*)(src + c) : make_double2(0.0, 0.0);
+                Inv[s][c] = t2.x;
+                Inv[s][c + 1] = t2.y;
+            }
+        }
+        for (int o = tid; o < pm * amax * S; o += 128) {
+            const int q = o >> 5, j = o & (S - 1), k = q / amax, r = q - k * amax;
+            Fc[q * FGS + j] = Fg[(long)(k + 1) * SS + r * S + j];
+        }
+        for (int o = tid; o < nbot * bmax * S; o += 128) {
+            const int q = o >> 5, j = o & (S - 1), k = q / bmax, r = q - k * bmax;
+            Gc[q * FGS + j] = Hg[(long)(pm + k) * SS + r * S + j];
+        }
+    }
+};
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int NS>
+__device__ __forceinline__ void wave_twisted_solve(const TwoSidedW<NS>& R, const KParams& p, const double* Fc,
+                                                   const double* Gc, const int* toffL, double* rb, double* xt,
+                                                   double* corB, long long* pacc) {
+#ifdef MPCQP_PHASE_PROF
+    long long t0s = clock64();
+#define SPH(k) if (pacc && threadIdx.x == 0) { const long long t_ = clock64(); pacc[k] += t_ - t0s; t0s = t_; }
+#else
+#define SPH(k)
+#endif
+    int opq = 0;
+    asm volatile("" : "+s"(opq));
+    const int tid = threadIdx.x, wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = (tid & 63) + opq,
+              i = lane >> 1, h = lane & 1;
+    const int nb = p.nb, pm = p.pmeet, amax = p.amax, bmax = p.bmax, nbot = nb - 1 - pm;
+    const int nmine = wv ? nbot : pm, lim = wv ? bmax : amax;
+    const bool writer = h == 0, lowrank = i < lim;
+#pragma unroll
+    for (int s = 1; s <= NS; ++s) {
+        if (s <= nmine) {
+            const int ks = wv ? nb - s : s - 1, kd = wv ? nb - 1 - s : s;
+            const bool mid = wv && kd == pm;
+            double* dst = mid ? corB + i : rb + kd * S + (wv ? toffL[kd] : 0) + i;
+            const double old = (writer && lowrank && !mid) ? *dst : 0.0;
+            const double* v = A16(rb + ks * S + 16 * h);
+            double vv[16];
+#pragma unroll
+            for (int c = 0; c < 16; c += 2) {
+                const double2 t2 = *(const double2*)(v + c);
+                vv[c] = t2.x;
+                vv[c + 1] = t2.y;
+            }
+            double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+            for (int c = 0; c < 16; c += 2) {
+                a0 += R.Inv[s - 1][c] * vv[c];
+                a1 += R.Inv[s - 1][c + 1] * vv[c + 1];
+            }
+            double t = a0 + a1;
+            t += dpp<0xB1>(t);
+            if (lowrank) {
+                const double* f = A16((wv ? Gc + (kd - pm) * bmax * FGS : Fc + (s - 1) * amax * FGS) + i * FGS + 16 * h);
+                double b0 = 0.0, b1 = 0.0;
+#pragma unroll
+                for (int c = 0; c < 16; c += 2) {
+                    const double2 f2 = *(const double2*)(f + c);
+                    b0 += f2.x * vv[c];
+                    b1 += f2.y * vv[c + 1];
+                }
+                double cc = b0 + b1;
+                cc += dpp<0xB1>(cc);
+                if (writer) *dst = old - cc;
+            }
+            if (writer) xt[ks * S + i] = t;
+            wave_sync();
+        }
+    }
+    __syncthreads();
+    SPH(12)
+    if (wv == 0) {  // middle: x_p = M^{-1} (w_p with the bottom chain's correction in corB)
+        const int toffp = toffL[pm];
+        const double* v = A16(rb + pm * S + 16 * h);
+        double vv[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+            const int a = 16 * h + c - toffp;
+            vv[c] = v[c] + ((pm < nb - 1 && a >= 0 && a < bmax) ? corB[a & 15] : 0.0);
+        }
+        double t = 0.0;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            if (s == pm) {
+                double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+                for (int c = 0; c < 16; c += 2) {
+                    a0 += R.Inv[s][c] * vv[c];
+                    a1 += R.Inv[s][c + 1] * vv[c + 1];
+                }
+                t = a0 + a1;
+            }
+        }
+        t += dpp<0xB1>(t);
+        if (writer) xt[pm * S + i] = t;
+    }
+    __syncthreads();
+    SPH(13)
+#pragma unroll
+    for (int s = 1; s <= NS; ++s) {
+        if (s <= nmine) {
+            const int k = wv ? pm + s : pm - s;
+            const double* x1 = xt + (wv ? (k - 1) * S + toffL[k - 1] : (k + 1) * S);
+            const double* hr = (wv ? Gc + (k - 1 - pm) * bmax * FGS : Fc + k * amax * FGS) + i;
+            const double tk = xt[k * S + i];
+            double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+            for (int c = 0; c < 8; c += 2) {
+                const int r0 = h + 2 * c, r1 = h + 2 * c + 2;
+                if (r0 < lim) a0 += hr[r0 * FGS] * x1[r0];
+                if (r1 < lim) a1 += hr[r1 * FGS] * x1[r1];
+            }
+            double a = a0 + a1;
+            a += dpp<0xB1>(a);
+            if (writer) xt[k * S + i] = tk - a;
+            wave_sync();
+        }
+    }
+    __syncthreads();
+    SPH(14)
+#undef SPH
+}
+
 // doubles of the F / G region: F_k rows (k = 1..p), G_k tail rows (k = p..nb-2), and
 // at least the four scratch tiles factorize2 needs
 __host__ __device__ inline int big_fg_len(const KParams& p) {
@@ -388,8 +552,10 @@ __device__ __forceinline__ double* big_fc(const SLds& L) {
     return A16((double*)c);
 }
 
-template <int SL, int K, int CS, int RS>
-__global__ __launch_bounds__(TB, 1) void k_solve_b(KParams p, double* __restrict__ xo, double* __restrict__ yo,
+// TTK = 512: TwoSided / twisted_solve (nb up to 24); TTK = 128: TwoSidedW / wave_twisted_solve (nb <= 8).
+// NS: the most steps one chain takes, max(p, nb-1-p).
+template <int TTK, int NS, int K, int CS, int RS>
+__global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restrict__ xo, double* __restrict__ yo,
                                                    int factor_only) {
     const int tid = threadIdx.x;
     const long b = blockIdx.x;
@@ -407,8 +573,8 @@ __global__ __launch_bounds__(TB, 1) void k_solve_b(KParams p, double* __restrict
     const double* Sg = p.Si + b * (long)nb * SS;
 
     if (p.err[b]) {  // invalid data (flagged by setup/update): NaN outputs
-        for (int j = tid; j < n; j += TB) if (xo) xo[b * n + j] = __builtin_nan("");
-        for (int i = tid; i < m; i += TB) if (yo) yo[b * m + i] = __builtin_nan("");
+        for (int j = tid; j < n; j += TTK) if (xo) xo[b * n + j] = __builtin_nan("");
+        for (int i = tid; i < m; i += TTK) if (yo) yo[b * m + i] = __builtin_nan("");
         if (tid == 0) p.status[b] = MPCQP_NON_CVX_;
         return;
     }
@@ -426,25 +592,25 @@ __global__ __launch_bounds__(TB, 1) void k_solve_b(KParams p, double* __restrict
     double rho = p.scal[b * 4 + 2];
     const double sigma = p.sigma, alpha = p.alpha;
     const bool warm = p.warm_start != 0;
-    for (int e = tid; e < nnzA; e += TB) L.Acsc[e] = p.Ax[b * nnzA + p.acsc_v[e]];
+    for (int e = tid; e < nnzA; e += TTK) L.Acsc[e] = p.Ax[b * nnzA + p.acsc_v[e]];
     if (tid == 0) L.Acsc[nnzA] = 0.0;  // the gather lists' padding slot
-    for (int v = tid; v < nnzP; v += TB) L.Pv[v] = p.Px[b * nnzP + v];
+    for (int v = tid; v < nnzP; v += TTK) L.Pv[v] = p.Px[b * nnzP + v];
     if (tid == 0) L.Pv[nnzP] = 0.0;
-    for (int i = tid; i < m; i += TB) {
+    for (int i = tid; i < m; i += TTK) {
         L.lo[i] = p.l[b * m + i];
         L.up[i] = p.u[b * m + i];
         L.ct[i] = p.ct[b * m + i];
         Z[i] = warm ? p.z[b * m + i] : 0.0;
         dY[i] = 0.0;
     }
-    for (int pc = tid; pc < npad; pc += TB) {
+    for (int pc = tid; pc < npad; pc += TTK) {
         L.qv[pc] = p.q[b * npad + pc];
         X[pc] = warm ? p.x[b * npad + pc] : 0.0;
     }
     if (tid < 16) L.res[tid] = 0.0;
     if (tid < 4) L.flag[tid] = 0;
-    for (int k = tid; k < nb; k += TB) toffL[k] = p.toff[k];
-    for (int e = tid; e < 2 * npad; e += TB) L.cor[e] = 0.0;  // corT | corB of the sweep (cor, tv)
+    for (int k = tid; k < nb; k += TTK) toffL[k] = p.toff[k];
+    for (int e = tid; e < 2 * npad; e += TTK) L.cor[e] = 0.0;  // corT | corB of the sweep (cor, tv)
 
     int status = MPCQP_UNSOLVED_, rho_updates = 0, iter = 0, info_iter = 0;
     bool can_check = false, need_factor = true;
@@ -452,7 +618,7 @@ __global__ __launch_bounds__(TB, 1) void k_solve_b(KParams p, double* __restrict
     double y[RS];
 #pragma unroll
     for (int s = 0; s < RS; ++s) {
-        const int i = tid + s * TB;
+        const int i = tid + s * TTK;
         y[s] = (i < m && warm) ? p.y[b * m + i] : 0.0;
     }
     PH(5)
@@ -460,11 +626,11 @@ __global__ __launch_bounds__(TB, 1) void k_solve_b(KParams p, double* __restrict
         __syncthreads();
         if (need_factor) {  // start, and after a rho change
             need_factor = false;
-            const bool ok = factorize2_nl(p.self, b, rho, Fc);  // scratch tiles in the F/G region
+            const bool ok = factorize2_nl<TTK>(p.self, b, rho, Fc);  // scratch tiles in the F/G region
             if (!ok) {
                 if (iter == 0) {
-                    for (int j = tid; j < n; j += TB) if (xo) xo[b * n + j] = __builtin_nan("");
-                    for (int i = tid; i < m; i += TB) if (yo) yo[b * m + i] = __builtin_nan("");
+                    for (int j = tid; j < n; j += TTK) if (xo) xo[b * n + j] = __builtin_nan("");
+                    for (int i = tid; i < m; i += TTK) if (yo) yo[b * m + i] = __builtin_nan("");
                     if (tid == 0) p.status[b] = MPCQP_NON_CVX_;
                     return;
                 }
@@ -476,13 +642,13 @@ __global__ __launch_bounds__(TB, 1) void k_solve_b(KParams p, double* __restrict
             PH(0)
         }
         // ---- run state (re-derived at every run start; nothing but scalars lives across calls) ----
-        TwoSided<SL> RF;
+        std::conditional_t<TTK == 512, TwoSided<NS + 1>, TwoSidedW<NS>> RF;
         RF.load(nb, p.pmeet, amax, p.bmax, Fg, Hg, Sg, Fc, Gc);
         int cvar[CS];
         Gather<K> cg[CS];
 #pragma unroll
         for (int s = 0; s < CS; ++s) {
-            const int pc = tid + s * TB;
+            const int pc = tid + s * TTK;
             cvar[s] = pc < npad ? p.pad_var[pc] : -1;
             if (pc < npad) cg[s].load(p.gcol + (long)pc * kGS);
             else cg[s].clear(nnzA);
@@ -490,7 +656,7 @@ __global__ __launch_bounds__(TB, 1) void k_solve_b(KParams p, double* __restrict
         Gather<K> rg[RS];
 #pragma unroll
         for (int s = 0; s < RS; ++s) {
-            const int i = tid + s * TB;
+            const int i = tid + s * TTK;
             if (i < m) {
                 rg[s].load(p.grow + (long)i * kGS);
                 L.w[i] = rho_of(L.ct[i], rho) * Z[i] - y[s];  // w = rho z_prev - y (rho may be new)
@@ -513,22 +679,24 @@ __global__ __launch_bounds__(TB, 1) void k_solve_b(KParams p, double* __restrict
             // rhs = sigma x_prev - q + A' (rho z_prev - y)
 #pragma unroll
             for (int s = 0; s < CS; ++s) {
-                const int pc = tido + s * TB;
+                const int pc = tido + s * TTK;
                 if (pc < npad)
                     L.rb[pc] = cvar[s] >= 0 ? (sigma * X[pc] - L.qv[pc]) + cg[s].dot(L.Acsc, L.w) : 0.0;
             }
             __syncthreads();
             PH(1)
 #ifdef MPCQP_PHASE_PROF
-            twisted_solve<SL>(RF, p, Fc, Gc, toffL, L.rb, L.xt, L.cor, L.tv, prof ? L.pacc : nullptr);
+            long long* pacc = prof ? L.pacc : nullptr;
 #else
-            twisted_solve<SL>(RF, p, Fc, Gc, toffL, L.rb, L.xt, L.cor, L.tv, nullptr);
+            long long* pacc = nullptr;
 #endif
+            if constexpr (TTK == 512) twisted_solve<NS + 1>(RF, p, Fc, Gc, toffL, L.rb, L.xt, L.cor, L.tv, pacc);
+            else wave_twisted_solve<NS>(RF, p, Fc, Gc, toffL, L.rb, L.xt, L.cor, pacc);
             PH(2)
             // z~ = A x~ ; relaxed + projected z ; y ; next w.   x update; deltas for the checks.
 #pragma unroll
             for (int s = 0; s < RS; ++s) {
-                const int i = tido + s * TB;
+                const int i = tido + s * TTK;
                 if (i < m) {
                     const double zt = rg[s].dot(L.Acsc, L.xt);
                     const signed char cl = L.ct[i];
@@ -545,7 +713,7 @@ __global__ __launch_bounds__(TB, 1) void k_solve_b(KParams p, double* __restrict
             }
 #pragma unroll
             for (int s = 0; s < CS; ++s) {
-                const int pc = tido + s * TB;
+                const int pc = tido + s * TTK;
                 if (pc < npad) {
                     const double xold = X[pc];
                     const double xn = alpha * L.xt[pc] + (1.0 - alpha) * xold;
@@ -557,17 +725,17 @@ __global__ __launch_bounds__(TB, 1) void k_solve_b(KParams p, double* __restrict
             PH(3)
         }
 #pragma unroll
-        for (int s = 0; s < RS; ++s) { const int i = tid + s * TB; if (i < m) L.ys[i] = y[s]; }
+        for (int s = 0; s < RS; ++s) { const int i = tid + s * TTK; if (i < m) L.ys[i] = y[s]; }
         __syncthreads();
         // ---- out-of-line phases ----
         can_check = p.check_term && (iter % p.check_term == 0);
         const bool do_rho = p.adaptive_rho && p.rho_interval && (iter % p.rho_interval == 0);
         if (!can_check && !do_rho) break;  // max_iter reached
-        update_info_nl<TB>(p.self, b, cinv);
+        update_info_nl<TTK>(p.self, b, cinv);
         info_iter = iter;
         bool stop = false;
         if (can_check) {
-            status = check_termination_nl<TB>(p.self, b, cval, cinv, 0);
+            status = check_termination_nl<TTK>(p.self, b, cval, cinv, 0);
             stop = status != MPCQP_UNSOLVED_;
         }
         if (!stop && do_rho) {
@@ -588,19 +756,19 @@ __global__ __launch_bounds__(TB, 1) void k_solve_b(KParams p, double* __restrict
         if (stop || iter >= p.max_iter) break;
     }
     if (!can_check && status == MPCQP_UNSOLVED_) {
-        update_info_nl<TB>(p.self, b, cinv);
+        update_info_nl<TTK>(p.self, b, cinv);
         info_iter = iter;
-        status = check_termination_nl<TB>(p.self, b, cval, cinv, 0);
+        status = check_termination_nl<TTK>(p.self, b, cval, cinv, 0);
     }
     const bool has_sol = !(status == MPCQP_PRIMAL_INFEASIBLE_ || status == MPCQP_PRIMAL_INFEASIBLE_INACCURATE_ ||
                            status == MPCQP_DUAL_INFEASIBLE_ || status == MPCQP_DUAL_INFEASIBLE_INACCURATE_ ||
                            status == MPCQP_NON_CVX_);
-    if (has_sol) objective_nl<TB>(p.self, cinv);
+    if (has_sol) objective_nl<TTK>(p.self, cinv);
     if (status == MPCQP_UNSOLVED_) {
-        status = check_termination_nl<TB>(p.self, b, cval, cinv, 1);
+        status = check_termination_nl<TTK>(p.self, b, cval, cinv, 1);
         if (status == MPCQP_UNSOLVED_) status = MPCQP_MAX_ITER_REACHED_;
     }
-    finalize_nl<TB>(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates);
+    finalize_nl<TTK>(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates);
 #ifdef MPCQP_PHASE_PROF
     if (prof) {
         __syncthreads();
@@ -622,21 +790,22 @@ size_t lds_solve_bytes_big(const KParams& p) {
     return lds_solve_bytes(p) + 16 + sizeof(double) * (size_t)big_fg_len(p) + sizeof(int) * (size_t)p.nb;
 }
 
-template <int SL, int K, int CS, int RS>
+template <int TTK, int NS, int K, int CS, int RS>
 static hipError_t go_b(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st) {
     const size_t lds = lds_solve_bytes_big(p);
-    auto k = k_solve_b<SL, K, CS, RS>;
+    auto k = k_solve_b<TTK, NS, K, CS, RS>;
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(TB), lds, st, p, xo, yo, fo);
+    hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(TTK), lds, st, p, xo, yo, fo);
     return hipGetLastError();
 }
 
 hipError_t launch_solve_big(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st) {
     switch (p.variant) {
-        case 11: return go_b<7, 8, 1, 2>(p, B, xo, yo, factor_only, st);    // nb <= 12
-        case 12: return go_b<10, 8, 2, 2>(p, B, xo, yo, factor_only, st);   // nb <= 18
-        case 13: return go_b<13, 8, 2, 3>(p, B, xo, yo, factor_only, st);   // nb <= 24
+        case 11: return go_b<512, 6, 8, 1, 2>(p, B, xo, yo, factor_only, st);   // nb <= 12
+        case 12: return go_b<512, 9, 8, 2, 2>(p, B, xo, yo, factor_only, st);   // nb <= 18
+        case 13: return go_b<512, 12, 8, 2, 3>(p, B, xo, yo, factor_only, st);  // nb <= 24
+        case 14: return go_b<128, 4, 8, 2, 2>(p, B, xo, yo, factor_only, st);   // nb <= 8, two waves
         default: return hipErrorInvalidValue;
     }
 }
