@@ -26,6 +26,12 @@ namespace mpcqp {
 
 // ------------------------------------------------------------------ setup --
 // osqp_setup: copy, Ruiz-scale (scale_data), classify rows (set_rho_vec).
+// The plan's index arrays from pad_var to a_c (one contiguous span of the flat plan,
+// api.hip::upload_plan) are staged in LDS once, so the ten scaling passes chase
+// LDS indices instead of dependent global loads.
+__host__ __device__ inline long setup_span(const KParams& p) { return (long)(p.asm_blk_ptr - p.pad_var); }
+
+template <bool STAGE>  // false: plans whose index span does not fit in LDS read it from the plan
 __global__ __launch_bounds__(T) void k_setup(KParams p, const double* __restrict__ Px_in,
                                              const double* __restrict__ Ax_in,
                                              const double* __restrict__ q_in,
@@ -44,11 +50,22 @@ __global__ __launch_bounds__(T) void k_setup(KParams p, const double* __restrict
     double* Et = Ev + m;
     double* red = Et + m;
     int* flag = (int*)(red + 64);
+    int* ix = STAGE ? flag + 4 : (int*)p.pad_var;  // the staged index span
+    if (STAGE) {
+        const long span = setup_span(p);
+        for (long o = tid; o < span; o += T) ix[o] = p.pad_var[o];
+    }
+    auto rebase = [&](const int* a) __attribute__((always_inline)) { return ix + (a - p.pad_var); };
+    const int *pad_var = ix, *psym_ptr = rebase(p.psym_ptr), *psym_v = rebase(p.psym_v);
+    const int *acsc_ptr = rebase(p.acsc_ptr), *acsc_v = rebase(p.acsc_v);
+    const int *acsr_ptr = rebase(p.acsr_ptr), *acsr_v = rebase(p.acsr_v);
+    const int *p_r = rebase(p.p_r), *p_c = rebase(p.p_c), *a_r = rebase(p.a_r), *a_c = rebase(p.a_c);
 
     for (int i = tid; i < nnzP; i += T) Pv[i] = Px_in[b * nnzP + i];
     for (int i = tid; i < nnzA; i += T) Av[i] = Ax_in[b * nnzA + i];
+    __syncthreads();  // the staged indices
     for (int pc = tid; pc < npad; pc += T) {
-        int j = p.pad_var[pc];
+        int j = pad_var[pc];
         qv[pc] = j >= 0 ? q_in[b * n + j] : 0.0;
         Dv[pc] = 1.0;
     }
@@ -60,28 +77,28 @@ __global__ __launch_bounds__(T) void k_setup(KParams p, const double* __restrict
         // compute_inf_norm_cols_KKT + limit_scaling + sqrt + reciprocal
         for (int pc = tid; pc < npad; pc += T) {
             double d = 1.0;
-            if (p.pad_var[pc] >= 0) {
+            if (pad_var[pc] >= 0) {
                 double d1 = 0.0, d2 = 0.0;
-                for (int e = p.psym_ptr[pc]; e < p.psym_ptr[pc + 1]; ++e) d1 = cmax(fabs(Pv[p.psym_v[e]]), d1);
-                for (int e = p.acsc_ptr[pc]; e < p.acsc_ptr[pc + 1]; ++e) d2 = cmax(fabs(Av[p.acsc_v[e]]), d2);
+                for (int e = psym_ptr[pc]; e < psym_ptr[pc + 1]; ++e) d1 = cmax(fabs(Pv[psym_v[e]]), d1);
+                for (int e = acsc_ptr[pc]; e < acsc_ptr[pc + 1]; ++e) d2 = cmax(fabs(Av[acsc_v[e]]), d2);
                 d = 1.0 / sqrt(limit_scaling(cmax(d1, d2)));
             }
             Dt[pc] = d;
         }
         for (int i = tid; i < m; i += T) {
             double e = 0.0;
-            for (int q = p.acsr_ptr[i]; q < p.acsr_ptr[i + 1]; ++q) e = cmax(fabs(Av[p.acsr_v[q]]), e);
+            for (int q = acsr_ptr[i]; q < acsr_ptr[i + 1]; ++q) e = cmax(fabs(Av[acsr_v[q]]), e);
             Et[i] = 1.0 / sqrt(limit_scaling(e));
         }
         __syncthreads();
         // P <- D P D ; A <- E A D ; q <- D q ; D <- D Dt ; E <- E Et
         for (int v = tid; v < nnzP; v += T) {
-            double x = Pv[v] * Dt[p.p_r[v]];
-            Pv[v] = x * Dt[p.p_c[v]];
+            double x = Pv[v] * Dt[p_r[v]];
+            Pv[v] = x * Dt[p_c[v]];
         }
         for (int v = tid; v < nnzA; v += T) {
-            double x = Av[v] * Et[p.a_r[v]];
-            Av[v] = x * Dt[p.a_c[v]];
+            double x = Av[v] * Et[a_r[v]];
+            Av[v] = x * Dt[a_c[v]];
         }
         for (int pc = tid; pc < npad; pc += T) { qv[pc] *= Dt[pc]; Dv[pc] *= Dt[pc]; }
         for (int i = tid; i < m; i += T) Ev[i] *= Et[i];
@@ -89,9 +106,9 @@ __global__ __launch_bounds__(T) void k_setup(KParams p, const double* __restrict
         // cost normalisation: mean column inf-norm of P vs ||q||_inf
         double acc[1] = {0.0}, mq[1] = {0.0};
         for (int pc = tid; pc < npad; pc += T) {
-            if (p.pad_var[pc] < 0) continue;
+            if (pad_var[pc] < 0) continue;
             double d1 = 0.0;
-            for (int e = p.psym_ptr[pc]; e < p.psym_ptr[pc + 1]; ++e) d1 = cmax(fabs(Pv[p.psym_v[e]]), d1);
+            for (int e = psym_ptr[pc]; e < psym_ptr[pc + 1]; ++e) d1 = cmax(fabs(Pv[psym_v[e]]), d1);
             acc[0] += d1;
             mq[0] = cmax(mq[0], fabs(qv[pc]));
         }
@@ -225,15 +242,22 @@ __global__ __launch_bounds__(T) void k_warm(KParams p, const double* __restrict_
 }
 
 // ------------------------------------------------------------ launchers --
-size_t lds_setup_bytes(const KParams& p) {
+static size_t lds_setup_base(const KParams& p) {
     return sizeof(double) * ((size_t)p.nnzP + p.nnzA + 3 * (size_t)p.npad + 2 * (size_t)p.m + 64) + 16;
+}
+static bool setup_staged(const KParams& p) {
+    return lds_setup_base(p) + sizeof(int) * (size_t)setup_span(p) <= 96 * 1024;
+}
+size_t lds_setup_bytes(const KParams& p) {
+    return lds_setup_base(p) + (setup_staged(p) ? sizeof(int) * (size_t)setup_span(p) : 0);
 }
 hipError_t launch_setup(const KParams& p, long B, const double* Px, const double* Ax, const double* q,
                         const double* l, const double* u, hipStream_t st) {
     size_t lds = lds_setup_bytes(p);
-    hipError_t e = hipFuncSetAttribute((const void*)k_setup, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    auto k = setup_staged(p) ? k_setup<true> : k_setup<false>;
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_setup, dim3((unsigned)B), dim3(T), lds, st, p, Px, Ax, q, l, u);
+    hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(T), lds, st, p, Px, Ax, q, l, u);
     return hipGetLastError();
 }
 hipError_t launch_update(const KParams& p, long B, const double* q, const double* l, const double* u,

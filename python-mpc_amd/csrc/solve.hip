@@ -702,9 +702,11 @@ bool variant_fits(const KParams& p, int v) {
         case 4: return p.gk <= 8 && cs <= 2 && rs <= 4;
         case 5: return p.gk <= 8 && cs <= 4 && rs <= 4;
         case 6: return p.gk <= 16 && cs <= 8 && rs <= 8;
-        case 8: return p.nb == 4 && p.amax <= 8 && p.gk <= 6 && p.m <= 3 * 64 && lds_solve_bytes(p) < 65536;
-        case 9: return p.nb == 4 && p.amax <= 8 && p.gk <= 8 && p.m <= 4 * 64 && lds_solve_bytes(p) < 65536;
-        case 10: return p.nb == 4 && p.amax <= 8 && p.gk <= 6 && p.m <= 2 * 128 && lds_solve_bytes(p) < 65536;
+        // the one-wave kernels' rows i = lane + 64 s, s < RS, must cover exactly the padded rows
+        // (solve_mpad): RS = 3 for 128 < m <= 192, RS = 4 for 192 < m <= 256
+        case 8: return p.nb == 4 && p.amax <= 8 && p.gk <= 6 && solve_mpad(p.m) == 3 * 64 && lds_solve_bytes(p) < 65536;
+        case 9: return p.nb == 4 && p.amax <= 8 && p.gk <= 8 && solve_mpad(p.m) == 4 * 64 && lds_solve_bytes(p) < 65536;
+        case 10: return p.nb == 4 && p.amax <= 8 && p.gk <= 6 && p.pk <= 4 && p.m <= 2 * 128 && lds_solve_bytes(p) < 65536;
         case 11: case 12: case 13: {
             const int nbm = v == 11 ? 12 : v == 12 ? 18 : 24, csm = v == 11 ? 1 : 2, rsm = v == 13 ? 3 : 2;
             const int csb = (p.npad + kThreadsBig - 1) / kThreadsBig, rsb = (p.m + kThreadsBig - 1) / kThreadsBig;

@@ -447,7 +447,7 @@ __global__ __launch_bounds__(TW, 1) void k_solve_w(KParams p, double* __restrict
 // Per-wave LDS for those: cw[w][block][8] (in cor), tw[w][block][8] (in tv).
 constexpr int T2 = 128;
 
-template <int K, int RS>
+template <int K, int RS, int KPK>
 __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restrict__ xo, double* __restrict__ yo,
                                                     int factor_only) {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -554,6 +554,12 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
         const unsigned abase = lds_addr(L.Acsc), wbase = lds_addr(L.w), xbase = lds_addr(L.xt);
         GatherW<K> cg;
         cg.load(p.gcol + (long)pc * kGS, abase, wbase);
+        // for the inline termination check: the column's P list (addresses of Pv / X),
+        // the scalings D of the column and E of the rows
+        const unsigned Xbase = lds_addr(C.X);
+        GatherW<KPK> pg;
+        pg.load(p.gpsym + (long)pc * kGS, lds_addr(L.Pv), Xbase);
+        const double Dv = p.D[b * npad + pc];
         // phase-C slots (pair, j) of the lane; pair NP is the zero block
         int gslot[3], tslot[3];
         {
@@ -569,7 +575,7 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
             }
         }
         GatherW<K> rg[RS];
-        double y[RS], Z[RS], dy[RS], rv[RS], rvi[RS];
+        double y[RS], Z[RS], dy[RS], rv[RS], rvi[RS], Ev[RS];
         int ri[RS];
         const double r_hi = RHO_EQ_OVER_RHO_INEQ * rho;
 #pragma unroll
@@ -577,6 +583,7 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
             const int i = min(tid + s * T2, mp - 1);  // lanes past the padded rows repeat the inert last row
             ri[s] = i;
             dy[s] = 0.0;
+            Ev[s] = i < m ? p.E[b * m + i] : 1.0;
             if (i < m) rg[s].load(p.grow + (long)i * kGS, abase, xbase);
             else rg[s].clear(abase + 8u * nnzA, xbase);
             y[s] = L.ys[i];
@@ -738,16 +745,156 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
 #pragma unroll
         for (int s = 0; s < RS; ++s) { L.ys[ri[s]] = y[s]; C.Z[ri[s]] = Z[s]; C.dY[ri[s]] = dy[s]; }
         __syncthreads();
-        // ---- out-of-line phases (only scalars live across these calls) ----
         can_check = p.check_term && (iter % p.check_term == 0);
         const bool do_rho = p.adaptive_rho && p.rho_interval && (iter % p.rho_interval == 0);
         if (!can_check && !do_rho) break;  // max_iter reached
-        update_info_nl<T2>(p.self, b, cinv);
         info_iter = iter;
         bool stop = false;
-        if (can_check) {
-            status = check_termination_nl<T2>(p.self, b, cval, cinv, 0);
-            stop = status != MPCQP_UNSOLVED_;
+        {
+            // ---- inline update_info + check_termination (OSQP 0.6 update_info,
+            // check_termination, is_primal_infeasible, is_dual_infeasible; the same
+            // arithmetic as solve_phases.h::update_info_ph / check_termination_ph) on the
+            // register-resident gather lists: no dependent global loads, no calls ----
+            const bool unscale = p.scaling && !p.scaled_term;
+            const unsigned ysbase = lds_addr(L.ys), dYbase = lds_addr(C.dY), dxbase = lds_addr(L.dx);
+            double mx[17], sm[2] = {0.0, 0.0}, adx[RS];
+#pragma unroll
+            for (int k = 0; k < 17; ++k) mx[k] = 0.0;
+#pragma unroll
+            for (int s = 0; s < RS; ++s) {  // rows: A x, z, the projected delta y, A dx
+                const bool ok = tid + s * T2 < m;
+                double ax = 0.0, ad = 0.0;
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const unsigned e = rg[s].e[k], va = e >> 16;
+                    const double a = lds_at(e & 0xFFFFu);
+                    ax += a * lds_at(va - xbase + Xbase);
+                    ad += a * lds_at(va - xbase + dxbase);
+                }
+                adx[s] = ad;
+                const double zi = Z[s], pr = ax - zi, ei = 1.0 / Ev[s];
+                const double lo = L.lo[ri[s]], up = L.up[ri[s]];
+                double d = dy[s];
+                if (up > OSQP_INFTY * MIN_SCALING) d = (lo < -OSQP_INFTY * MIN_SCALING) ? 0.0 : cmin(d, 0.0);
+                else if (lo < -OSQP_INFTY * MIN_SCALING) d = cmax(d, 0.0);
+                if (ok) {
+                    mx[0] = cmax(mx[0], fabs(ei * pr));
+                    mx[2] = cmax(mx[2], fabs(ei * zi));
+                    mx[3] = cmax(mx[3], fabs(ei * ax));
+                    mx[7] = cmax(mx[7], fabs(pr));
+                    mx[9] = cmax(mx[9], fabs(zi));
+                    mx[10] = cmax(mx[10], fabs(ax));
+                    mx[14] = cmax(mx[14], fabs(unscale ? Ev[s] * d : d));
+                    sm[0] += up * cmax(d, 0.0) + lo * cmin(d, 0.0);
+                    C.dY[ri[s]] = d;  // projected in place, as OSQP's is_primal_infeasible
+                }
+            }
+            {  // the lane's column: P x, A' y, P dx, and the delta x norm
+                double px = 0.0, pdx = 0.0, aty = 0.0;
+#pragma unroll
+                for (int k = 0; k < KPK; ++k) {
+                    const unsigned e = pg.e[k], va = e >> 16;
+                    const double pv = lds_at(e & 0xFFFFu);
+                    px += pv * lds_at(va);
+                    pdx += pv * lds_at(va - Xbase + dxbase);
+                }
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const unsigned e = cg.e[k];
+                    aty += lds_at(e & 0xFFFFu) * lds_at((e >> 16) - wbase + ysbase);
+                }
+                if (cv) {
+                    const double d = (Q + px) + aty, di = 1.0 / Dv;
+                    mx[1] = fabs(di * d);
+                    mx[4] = fabs(di * Q);
+                    mx[5] = fabs(di * aty);
+                    mx[6] = fabs(di * px);
+                    mx[8] = fabs(d);
+                    mx[11] = fabs(Q);
+                    mx[12] = fabs(aty);
+                    mx[13] = fabs(px);
+                    mx[15] = fabs(unscale ? Dv * DX : DX);
+                    mx[16] = fabs(unscale ? pdx * di : pdx);
+                }
+            }
+            // q' dx with the out-of-line phases' column-per-thread order (column tid)
+            if (p.pad_var[tid] >= 0) sm[1] = L.qv[tid] * L.dx[tid];
+            block_max<T2, 17>(mx, L.red);
+            block_sum<T2, 2>(sm, L.red);
+            Res R;
+            if (unscale) {
+                R.pri = mx[0]; R.dua = cinv * mx[1];
+                R.nz = mx[2]; R.nax = mx[3]; R.nq = mx[4]; R.naty = mx[5]; R.npx = mx[6];
+            } else {
+                R.pri = mx[7]; R.dua = mx[8];
+                R.nz = mx[9]; R.nax = mx[10]; R.nq = mx[11]; R.naty = mx[12]; R.npx = mx[13];
+            }
+            R.rpri = mx[7]; R.rdua = mx[8]; R.rz = mx[9]; R.rax = mx[10]; R.rq = mx[11]; R.raty = mx[12]; R.rpx = mx[13];
+            if (m == 0) R.pri = 0.0;
+            if (tid == 0) R.save(L.res);
+            if (can_check) {
+                int st = MPCQP_UNSOLVED_;
+                double obj = 0.0;
+                bool done = false;
+                if (R.pri > OSQP_INFTY || R.dua > OSQP_INFTY) {
+                    st = MPCQP_NON_CVX_;
+                    obj = __builtin_nan("");
+                    done = true;
+                } else {
+                    const bool prim_ok = m == 0 || R.pri < p.eps_abs + p.eps_rel * cmax(R.nz, R.nax);
+                    double mxd = cmax(cmax(R.nq, R.naty), R.npx);
+                    if (unscale) mxd *= cinv;
+                    const bool dual_ok = R.dua < p.eps_abs + p.eps_rel * mxd;
+                    bool prim_inf = false, dual_inf = false;
+                    if (!prim_ok || !dual_ok) {  // infeasibility certificates (uniform branch)
+                        __syncthreads();  // the projected delta y
+                        const double norm_dy = mx[14], norm_dx = mx[15], epi = p.eps_pinf, edi = p.eps_dinf;
+                        double na[1] = {0.0};
+                        double a = 0.0;
+#pragma unroll
+                        for (int k = 0; k < K; ++k) {
+                            const unsigned e = cg.e[k];
+                            a += lds_at(e & 0xFFFFu) * lds_at((e >> 16) - wbase + dYbase);
+                        }
+                        if (cv) na[0] = fabs(unscale ? a * (1.0 / Dv) : a);
+                        bool viol = false;
+#pragma unroll
+                        for (int s = 0; s < RS; ++s) {
+                            if (!(tid + s * T2 < m)) continue;
+                            const double ar = unscale ? adx[s] * (1.0 / Ev[s]) : adx[s];
+                            const double lo = L.lo[ri[s]], up = L.up[ri[s]];
+                            if ((up < OSQP_INFTY * MIN_SCALING && ar > edi * norm_dx) ||
+                                (lo > -OSQP_INFTY * MIN_SCALING && ar < -edi * norm_dx))
+                                viol = true;
+                        }
+                        block_max<T2, 1>(na, L.red);
+                        viol = block_any<T2>(viol, L.flag);
+                        const double cs = unscale ? cval : 1.0;
+                        prim_inf = !prim_ok && m != 0 && norm_dy > epi && sm[0] < epi * norm_dy && na[0] < epi * norm_dy;
+                        dual_inf = !dual_ok && norm_dx > edi && sm[1] < cs * edi * norm_dx && mx[16] < cs * edi * norm_dx &&
+                                   !viol;
+                    }
+                    if (prim_ok && dual_ok) {
+                        st = MPCQP_SOLVED_;
+                        done = true;
+                    } else if (prim_inf) {
+                        st = MPCQP_PRIMAL_INFEASIBLE_;
+                        obj = OSQP_INFTY;
+                        if (tid == 0) L.flag[3] = unscale;
+                        done = true;
+                    } else if (dual_inf) {
+                        st = MPCQP_DUAL_INFEASIBLE_;
+                        obj = -OSQP_INFTY;
+                        if (tid == 0) L.flag[2] = unscale;
+                        done = true;
+                    }
+                }
+                __syncthreads();
+                if (done && tid == 0) { L.flag[1] = st; L.res[14] = obj; }
+                __syncthreads();
+                status = done ? st : MPCQP_UNSOLVED_;
+                stop = done;
+            }
         }
         if (!stop && do_rho) {
             Res R;
@@ -798,9 +945,9 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
 #undef PH
 }
 
-template <int K, int RS>
+template <int K, int RS, int KPK>
 static hipError_t go_w2(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st, size_t lds) {
-    auto k = k_solve_w2<K, RS>;
+    auto k = k_solve_w2<K, RS, KPK>;
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(T2), lds, st, p, xo, yo, fo);
@@ -822,7 +969,7 @@ hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, i
     switch (p.variant) {
         case 8: return go_w<6, 3>(p, B, xo, yo, factor_only, st, lds);
         case 9: return go_w<8, 4>(p, B, xo, yo, factor_only, st, lds);
-        case 10: return go_w2<6, 2>(p, B, xo, yo, factor_only, st, lds);
+        case 10: return go_w2<6, 2, 4>(p, B, xo, yo, factor_only, st, lds);
         default: return hipErrorInvalidValue;
     }
 }
