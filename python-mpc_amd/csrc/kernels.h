@@ -8,6 +8,7 @@ namespace mpcqp {
 
 constexpr int kThreads = 256;
 constexpr int kThreadsBig = 512;  // solve_big.hip (long horizons)
+constexpr int kDenseR = 104;      // solve_dense.hip: register row length of M^{-1} (variables per QP)
 constexpr int kProfSlots = 16;  // factor, rhs, bt_solve, update, checks, tail, total cycles, total 100 MHz ticks,
                                 // factor split: assembly, F/S products, Gauss-Jordan, block epilogue,
                                 // solve split (wave kernels): phase A, phase B, phase C, spare
@@ -67,6 +68,9 @@ int solve_mode(int variant);
 int solve_threads(int variant);  // workgroup size of the variant's kernel
 bool variant_fits(const KParams& p, int variant);
 hipError_t launch_solve(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st);
+// dense-inverse kernel (solve_dense.hip), variant 16, and its LDS bytes
+hipError_t launch_solve_dense(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st);
+size_t lds_dense_bytes(const KParams& p);
 // solution polishing (OSQP 0.6 polish.c) after the solve; launch_solve runs it when p.polish
 hipError_t launch_polish(const KParams& p, long B, double* xo, double* yo, hipStream_t st);
 // one-wave-per-QP kernel (solve_wave.hip), variants 8 and 9

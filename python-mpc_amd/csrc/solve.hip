@@ -667,15 +667,10 @@ hipError_t launch_polish(const KParams& p, long B, double* xo, double* yo, hipSt
 }
 
 // ------------------------------------------------------------ launcher --
-size_t lds_solve_bytes(const KParams& p) {
-    const size_t mp = (size_t)solve_mpad(p.m);
-    return sizeof(double) * ((size_t)al2(p.nnzA + 1) + (size_t)al2(p.nnzP + 1) + 3 * mp + 2 * (size_t)p.npad +
-                             (size_t)solve_vlen(p.m, p.npad, p.nb, p.amax, p.mode) + 160 + (size_t)p.nb * S +
-                             (size_t)p.npad) +
-           mp + 64;
-}
+size_t lds_solve_bytes(const KParams& p) { return lds_base_bytes(p); }
 
 size_t lds_kernel_bytes(const KParams& p) {
+    if (p.variant == 16) return lds_dense_bytes(p);
     return p.variant >= 11 && p.variant <= 14 ? lds_solve_bytes_big(p) : lds_solve_bytes(p);
 }
 
@@ -716,12 +711,15 @@ bool variant_fits(const KParams& p, int v) {
         case 14:
             return p.nb > 4 && p.nb <= 8 && p.amax <= 16 && p.bmax <= 16 && p.gk <= 8 && p.npad <= 256 &&
                    p.m <= 256 && lds_solve_bytes_big(p) <= 160 * 1024;
+        case 16:  // dense inverse: one variable per lane pair of a 256-thread workgroup, packed LDS addresses
+            return p.n <= kDenseR && p.npad <= 128 && p.gk <= 6 && p.pk <= 4 && p.m <= 2 * 128 &&
+                   lds_dense_bytes(p) < 65536;
         default: return false;
     }
 }
 
 int solve_variant(const KParams& p) {
-    static const int order[] = {10, 8, 9, 0, 1, 2, 3, 11, 12, 13, 4, 5, 6};
+    static const int order[] = {10, 8, 9, 0, 1, 2, 3, 11, 12, 13, 4, 5, 6};  // 14, 16: MPCQP_VARIANT only
     for (int v : order)
         if (variant_fits(p, v)) return v;
     return -1;
@@ -733,6 +731,7 @@ int solve_threads(int variant) {
         case 10: return 128;
         case 11: case 12: case 13: return kThreadsBig;
         case 14: return 128;
+        case 16: return 256;
         default: return T;
     }
 }
@@ -740,7 +739,7 @@ int solve_threads(int variant) {
 int solve_mode(int variant) {  // what factorize stores for the variant (KParams::mode)
     switch (variant) {
         case 0: case 8: case 9: case 10: return 2;
-        case 1: case 2: case 3: case 7: return 1;
+        case 1: case 2: case 3: case 7: case 16: return 1;  // (16: no factor stored; dx aliases rb)
         case 11: case 12: case 13: case 14: return 3;  // two-sided factor (solve_big.hip)
         default: return 0;
     }
@@ -759,6 +758,7 @@ static hipError_t launch_solve_only(const KParams& p, long B, double* xo, double
         case 6: return go<0, 32, 16, 8, 8, 1>(p, B, xo, yo, factor_only, st, lds);
         case 7: return go<4, 8, 6, 1, 1, 4, false>(p, B, xo, yo, factor_only, st, lds);
         case 8: case 9: case 10: return launch_solve_wave(p, B, xo, yo, factor_only, st);
+        case 16: return launch_solve_dense(p, B, xo, yo, factor_only, st);
         case 11: case 12: case 13: case 14: return launch_solve_big(p, B, xo, yo, factor_only, st);
         default: return hipErrorInvalidValue;
     }

@@ -329,6 +329,16 @@ struct SL2 {  // full carve (SLds + the solve-kernel-only arrays)
 __host__ __device__ inline long al2(long x) { return (x + 1) & ~1L; }
 #define A16(ptr) ((double*)__builtin_assume_aligned((ptr), 16))
 
+// bytes of the carve below (what lds_solve_bytes reports)
+template <class KP>
+__host__ __device__ inline size_t lds_base_bytes(const KP& p) {
+    const size_t mp = (size_t)solve_mpad(p.m);
+    return sizeof(double) * ((size_t)al2(p.nnzA + 1) + (size_t)al2(p.nnzP + 1) + 3 * mp + 2 * (size_t)p.npad +
+                             (size_t)solve_vlen(p.m, p.npad, p.nb, p.amax, p.mode) + 160 + (size_t)p.nb * S +
+                             (size_t)p.npad) +
+           mp + 64;
+}
+
 template <class KP>
 __device__ __forceinline__ SL2 carve(const KP& p) {
     extern __shared__ __attribute__((aligned(16))) double sm[];

@@ -1,0 +1,46 @@
+// wave_util.h -- LDS addressing helpers shared by the wave-level solve kernels
+// (solve_wave.hip, solve_dense.hip): packed gather lists with absolute LDS byte
+// addresses and 16-byte LDS reads.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace mpcqp {
+
+// Gather list with absolute LDS byte addresses: (vector address << 16) | (A value
+// address); one v_and / v_lshrrev per operand (the wave kernel's LDS is < 64 KiB).
+// Built at run start from the plan's (vector index << 16) | (A position) lists.
+template <int K>
+struct GatherW {
+    unsigned e[K];
+    __device__ __forceinline__ void load(const int* list, unsigned abase, unsigned vbase) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const unsigned raw = (unsigned)list[k];
+            e[k] = (((raw >> 16) * 8u + vbase) << 16) | ((raw & 0xFFFFu) * 8u + abase);
+        }
+    }
+    __device__ __forceinline__ void clear(unsigned zero_addr, unsigned vbase) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) e[k] = (vbase << 16) | zero_addr;
+    }
+};
+// 16-byte LDS reads (ds_read_b128) of two consecutive doubles at a 16-byte aligned address
+__device__ __forceinline__ void ld2(const double* p, double& a, double& b) {
+    const double2 v = *(const double2*)p;
+    a = v.x;
+    b = v.y;
+}
+typedef __attribute__((address_space(3))) const double lds_cdouble;
+typedef __attribute__((address_space(3))) const char lds_cchar;
+__device__ __forceinline__ double lds_at(unsigned byte_addr) { return *(lds_cdouble*)(unsigned long)byte_addr; }
+struct alignas(16) dpair { double x, y; };
+__device__ __forceinline__ void lds_at2(unsigned byte_addr, double& a, double& b) {
+    __attribute__((address_space(3))) const dpair* v = (__attribute__((address_space(3))) const dpair*)(unsigned long)byte_addr;
+    a = v->x;
+    b = v->y;
+}
+__device__ __forceinline__ unsigned lds_addr(const void* p) {  // LDS byte address of a shared pointer
+    return (unsigned)(unsigned long)(lds_cchar*)p;
+}
+
+}  // namespace mpcqp
