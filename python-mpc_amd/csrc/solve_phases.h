@@ -163,15 +163,18 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
 #else
 #define FPH(k)
 #endif
-#pragma unroll 1
-    for (int k = 0; k < nb; ++k) {
-        for (int e = tid; e < SS; e += TT) { DK[e] = 0.0; EK[e] = 0.0; }
-        __syncthreads();
-        if (tid < S) DK[tid * S + tid] = p.pad_var[k * S + tid] >= 0 ? (POL ? p.delta : p.sigma) : 1.0;
-        __syncthreads();
+    // Assembly of block k's D_k (sigma I + the plan's terms) and E_k (rows < amax) by the
+    // threads t0, t0 + nt, ...; sync() orders the zeroing before the targets' sums.
+    auto assemble = [&](const int k, double* __restrict__ D, double* __restrict__ E, const int t0, const int nt,
+                        auto sync) __attribute__((always_inline)) {
+        for (int e = 2 * t0; e < SS; e += 2 * nt) *(double2*)(D + e) = make_double2(0.0, 0.0);
+        for (int e = 2 * t0; e < amax * S; e += 2 * nt) *(double2*)(E + e) = make_double2(0.0, 0.0);
+        sync();
+        if (t0 < S) D[t0 * S + t0] = p.pad_var[k * S + t0] >= 0 ? (POL ? p.delta : p.sigma) : 1.0;
+        sync();
         // every target has one owner: its terms are summed in plan order
 #pragma unroll 1
-        for (int t = p.asm_blk_ptr[k] + tid; t < p.asm_blk_ptr[k + 1]; t += TT) {
+        for (int t = p.asm_blk_ptr[k] + t0; t < p.asm_blk_ptr[k + 1]; t += nt) {
             double acc = 0.0;
 #pragma unroll 4
             for (int j = 0; j < tmax; ++j) {
@@ -181,10 +184,32 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
                 acc += r < 0 ? L.Pv[a] : wr * L.Acsc[a] * L.Acsc[bb];
             }
             const int tg = p.asm_tgt[t];
-            if (tg < SS) DK[tg] += acc;
-            else EK[tg - SS] += acc;
+            if (tg < SS) D[tg] += acc;
+            else E[tg - SS] += acc;
         }
+    };
+    auto block_sync = []() __attribute__((always_inline)) { __syncthreads(); };
+    auto wave_sync = []() __attribute__((always_inline)) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    // OVL (two waves, E_k within half a tile): while wave 0 inverts S_k, wave 1 assembles
+    // D_{k+1} into SP (dead once F_k's products are done) and E_{k+1} into the other half
+    // of the E tile; the half holding E_k (dead as well) is the Gauss-Jordan buffer.
+    const bool OVL = TT == 128 && !POL && amax * S <= SS / 2;
+    auto Eh = [&](int k) __attribute__((always_inline)) { return OVL ? EK + (k & 1) * (SS / 2) : EK; };
+    if (OVL) {
+        assemble(0, DK, Eh(0), tid, TT, block_sync);
         __syncthreads();
+    }
+#pragma unroll 1
+    for (int k = 0; k < nb; ++k) {
+        double* const Ek = Eh(k);
+        if (!OVL) {
+            assemble(k, DK, EK, tid, TT, block_sync);
+            __syncthreads();
+        }
         FPH(8)
         if (k > 0) {
             // F_k = E_k S_{k-1}^{-1} (rows < amax), then written over S_{k-1}^{-1}'s tile
@@ -196,7 +221,7 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
                 const int r = o >> 5, j = o & (S - 1);
                 double sacc = 0.0;
 #pragma unroll 8
-                for (int l = 0; l < S; ++l) sacc += EK[r * S + l] * SP[l * S + j];
+                for (int l = 0; l < S; ++l) sacc += Ek[r * S + l] * SP[l * S + j];
                 f[nf & (NF - 1)] = sacc;
                 if (mode < 2) Fg[(long)k * SS + r * S + j] = sacc;
                 if (mode == 0) Hg[(long)(k - 1) * SS + j * S + r] = sacc;
@@ -228,7 +253,7 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
                 const int r = o / amax, c = o - r * amax;
                 double sacc = 0.0;
 #pragma unroll 8
-                for (int l = 0; l < S; ++l) sacc += SP[r * S + l] * EK[c * S + l];
+                for (int l = 0; l < S; ++l) sacc += SP[r * S + l] * Ek[c * S + l];
                 DK[r * S + c] -= sacc;
             }
             __syncthreads();
@@ -236,17 +261,19 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
         FPH(9)
         {
             // one wave inverts the tile (no barrier per pivot); the verdict goes through LDS
-            double* okslot = EK + 2 * S;
+            double* okslot = Ek + 2 * S;
             if (tid < 64) {
-                const bool okw = gj_wave<(TT > 128)>(DK, EK, Sg + (long)k * SS);
+                const bool okw = gj_wave<(TT > 128)>(DK, Ek, Sg + (long)k * SS);
                 if (tid == 0) okslot[0] = okw ? 1.0 : 0.0;
+            } else if (OVL && tid < 128 && k + 1 < nb) {
+                assemble(k + 1, SP, Eh(k + 1), tid - 64, 64, wave_sync);
             }
             __syncthreads();
             if (!(okslot[0] > 0.5)) ok = false;
             FPH(10)
         }
-        double* t = SP; SP = DK; DK = t;  // S_k^{-1} becomes "previous"
-        __syncthreads();
+        double* t = SP; SP = DK; DK = t;  // S_k^{-1} becomes "previous" (OVL: D_{k+1} is in DK now)
+        if (!OVL) __syncthreads();
         FPH(11)
     }
 #undef FPH

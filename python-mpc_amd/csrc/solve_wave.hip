@@ -903,6 +903,7 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
             p.prof[b * kProfSlots + 2] = L.pacc[12] + L.pacc[13] + L.pacc[14];
             p.prof[b * kProfSlots + 6] = clock64() - t0c;
             p.prof[b * kProfSlots + 7] = wall_clock64() - t0w;
+            p.prof[b * kProfSlots + 15] = t0w;  // absolute start (100 MHz): dispatch order / residency
         }
     }
 #endif

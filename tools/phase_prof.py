@@ -51,6 +51,15 @@ def main():
     names = ["factor", "rhs", "bt_solve", "update", "checks", "tail"]
     print(f"config {args.config} B={B} plan={s.plan_info()} kernel_ms={kt['solve_ms']:.3f}")
     slow = int(np.argmax(pt[:, 7]))
+    if pt[:, 15].any():  # absolute start stamps (two-wave kernel): residency rounds and the critical instance
+        st = pt[:, 15] - pt[:, 15].min()
+        end = st + pt[:, 7]
+        last = int(np.argmax(end))
+        q = np.percentile(st, [50, 75, 90, 100]) * 1e-2
+        print(f"starts (us after the first): p50 {q[0]:.1f} p75 {q[1]:.1f} p90 {q[2]:.1f} max {q[3]:.1f}; "
+              f"started within 2 us: {int((st < 200).sum())} of {len(st)}")
+        print(f"last to finish: instance {last} started {st[last] * 1e-2:.1f} us, ran {pt[last, 7] * 1e-2:.1f} us, "
+              f"iters {it[last]:.0f}; span {end.max() * 1e-2:.1f} us")
     for label, row, its in (("slowest", pt[slow], it[slow]), ("mean", pt.mean(0), it.mean())):
         tot = row[6]
         mhz = row[6] / (row[7] * 10e-3) if row[7] else 0
