@@ -515,11 +515,12 @@ int mpcqp_solve_device(mpcqp_handle* h, double* dx, double* dy, int32_t* dstatus
     HIPCHK(hipSetDevice(s.dev));
     HIPCHK(hipEventRecord(s.ev0, st));
     if (int e = ev_begin(h, h->ev_solve, st)) return e;
-    HIPCHK(launch_solve(s.kp, s.B, dx, dy, 0, st));
+    KParams k = s.kp;  // the solve kernel writes status / iter into the caller's arrays as well
+    k.ostat = dstatus;
+    k.oiter = diters;
+    HIPCHK(launch_solve(k, s.B, dx, dy, 0, st));
     if (int e = ev_end(h, h->ev_solve, st)) return e;
     HIPCHK(hipEventRecord(s.ev1, st));
-    if (dstatus) HIPCHK(hipMemcpyAsync(dstatus, s.kp.status, sizeof(int) * s.B, hipMemcpyDeviceToDevice, st));
-    if (diters) HIPCHK(hipMemcpyAsync(diters, s.kp.iter, sizeof(int) * s.B, hipMemcpyDeviceToDevice, st));
     h->timed = true;
     return 0;
 }

@@ -42,6 +42,7 @@ struct KParams {
     double *obj, *pri, *dua, *rho_est;
     signed char* ct;
     int *status, *iter, *rho_upd, *err;
+    int *ostat, *oiter;  // per-call copies of status / iter (mpcqp_solve_device's outputs), or null
     const struct KParams* self;  // device copy of this block (read by the out-of-line device functions)
     long long* prof;  // optional per-instance phase timers (MPCQP_PHASE_PROF=1), kProfSlots each
     // settings

@@ -273,7 +273,7 @@ __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ 
     if (p.err[b]) {  // invalid data (flagged by setup/update): NaN outputs
         for (int j = tid; j < n; j += T) if (xo) xo[b * n + j] = __builtin_nan("");
         for (int i = tid; i < m; i += T) if (yo) yo[b * m + i] = __builtin_nan("");
-        if (tid == 0) p.status[b] = MPCQP_NON_CVX_;
+        if (tid == 0) fail_status(p, b);
         return;
     }
 
@@ -334,7 +334,7 @@ __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ 
                 if (iter == 0) {
                     for (int j = tid; j < n; j += T) if (xo) xo[b * n + j] = __builtin_nan("");
                     for (int i = tid; i < m; i += T) if (yo) yo[b * m + i] = __builtin_nan("");
-                    if (tid == 0) p.status[b] = MPCQP_NON_CVX_;
+                    if (tid == 0) fail_status(p, b);
                     return;
                 }
                 status = MPCQP_NON_CVX_;
@@ -471,7 +471,7 @@ __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ 
         status = check_termination_nl<T>(p.self, b, cval, cinv, 1);
         if (status == MPCQP_UNSOLVED_) status = MPCQP_MAX_ITER_REACHED_;
     }
-    finalize_nl<T>(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates);
+    finalize_nl<T>(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates, p.ostat, p.oiter);
 #ifdef MPCQP_PHASE_PROF
     if (prof) {
         __syncthreads();

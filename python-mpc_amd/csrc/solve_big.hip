@@ -575,7 +575,7 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
     if (p.err[b]) {  // invalid data (flagged by setup/update): NaN outputs
         for (int j = tid; j < n; j += TTK) if (xo) xo[b * n + j] = __builtin_nan("");
         for (int i = tid; i < m; i += TTK) if (yo) yo[b * m + i] = __builtin_nan("");
-        if (tid == 0) p.status[b] = MPCQP_NON_CVX_;
+        if (tid == 0) fail_status(p, b);
         return;
     }
 
@@ -631,7 +631,7 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
                 if (iter == 0) {
                     for (int j = tid; j < n; j += TTK) if (xo) xo[b * n + j] = __builtin_nan("");
                     for (int i = tid; i < m; i += TTK) if (yo) yo[b * m + i] = __builtin_nan("");
-                    if (tid == 0) p.status[b] = MPCQP_NON_CVX_;
+                    if (tid == 0) fail_status(p, b);
                     return;
                 }
                 status = MPCQP_NON_CVX_;
@@ -768,7 +768,7 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
         status = check_termination_nl<TTK>(p.self, b, cval, cinv, 1);
         if (status == MPCQP_UNSOLVED_) status = MPCQP_MAX_ITER_REACHED_;
     }
-    finalize_nl<TTK>(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates);
+    finalize_nl<TTK>(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates, p.ostat, p.oiter);
 #ifdef MPCQP_PHASE_PROF
     if (prof) {
         __syncthreads();

@@ -405,6 +405,15 @@ struct Shared {
     int* flag;    // [0] scratch, [1] status, [2] dx_scaled, [3] dy_scaled
 };
 
+// status "non convex" of an early exit (invalid data, first factorisation failed), with
+// the per-call copies mpcqp_solve_device asks for
+template <class KP>
+__device__ __forceinline__ void fail_status(const KP& p, long b) {
+    p.status[b] = MPCQP_NON_CVX_;
+    if (p.ostat) p.ostat[b] = MPCQP_NON_CVX_;
+    if (p.oiter) p.oiter[b] = p.iter[b];
+}
+
 // ---- out-of-line phases: everything they need is in LDS or in the plan ----
 // dot of a packed gather list (value index | vector index << 16) with cnt entries
 __device__ __forceinline__ double list_dot(const int* __restrict__ list, int cnt, const double* V, const double* v) {
@@ -655,7 +664,7 @@ __device__ __noinline__ void objective_nl(const KParams* gp, double cinv) {
 template <int TT>
 __device__ __forceinline__ void finalize_ph(const KParams* gp, long b, double* __restrict__ xo,
                                          double* __restrict__ yo, double cinv, double rho, int status,
-                                         int info_iter, int rho_updates) {
+                                         int info_iter, int rho_updates, int* ostat, int* oiter) {
     KPc& p = kconst(gp);
     SL2 c = carve(p);
     const int tid = threadIdx.x, n = p.n, m = p.m, npad = p.npad;
@@ -713,6 +722,8 @@ __device__ __forceinline__ void finalize_ph(const KParams* gp, long b, double* _
     if (tid == 0) {
         p.status[b] = status;
         p.iter[b] = info_iter;
+        if (ostat) ostat[b] = status;
+        if (oiter) oiter[b] = info_iter;
         p.rho_upd[b] = rho_updates;
         p.obj[b] = obj;
         p.pri[b] = R.pri;
@@ -724,8 +735,8 @@ __device__ __forceinline__ void finalize_ph(const KParams* gp, long b, double* _
 template <int TT>
 __device__ __noinline__ void finalize_nl(const KParams* gp, long b, double* __restrict__ xo,
                                          double* __restrict__ yo, double cinv, double rho, int status,
-                                         int info_iter, int rho_updates) {
-    finalize_ph<TT>(gp, b, xo, yo, cinv, rho, status, info_iter, rho_updates);
+                                         int info_iter, int rho_updates, int* ostat, int* oiter) {
+    finalize_ph<TT>(gp, b, xo, yo, cinv, rho, status, info_iter, rho_updates, ostat, oiter);
 }
 
 template <int TT>

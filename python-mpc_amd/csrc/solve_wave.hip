@@ -68,7 +68,7 @@ __global__ __launch_bounds__(TW, 1) void k_solve_w(KParams p, double* __restrict
     if (p.err[b]) {  // invalid data (flagged by setup/update): NaN outputs
         for (int j = lane; j < n; j += TW) if (xo) xo[b * n + j] = __builtin_nan("");
         for (int i = lane; i < m; i += TW) if (yo) yo[b * m + i] = __builtin_nan("");
-        if (lane == 0) p.status[b] = MPCQP_NON_CVX_;
+        if (lane == 0) fail_status(p, b);
         return;
     }
 
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(TW, 1) void k_solve_w(KParams p, double* __restrict
                 if (iter == 0) {
                     for (int j = lane; j < n; j += TW) if (xo) xo[b * n + j] = __builtin_nan("");
                     for (int i = lane; i < m; i += TW) if (yo) yo[b * m + i] = __builtin_nan("");
-                    if (lane == 0) p.status[b] = MPCQP_NON_CVX_;
+                    if (lane == 0) fail_status(p, b);
                     return;
                 }
                 status = MPCQP_NON_CVX_;
@@ -380,7 +380,7 @@ __global__ __launch_bounds__(TW, 1) void k_solve_w(KParams p, double* __restrict
         status = check_termination_nl<TW>(p.self, b, cval, cinv, 1);
         if (status == MPCQP_UNSOLVED_) status = MPCQP_MAX_ITER_REACHED_;
     }
-    finalize_nl<TW>(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates);
+    finalize_nl<TW>(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates, p.ostat, p.oiter);
 #ifdef MPCQP_PHASE_PROF
     if (prof) {
         __syncthreads();
@@ -430,7 +430,7 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
     if (p.err[b]) {  // invalid data (flagged by setup/update): NaN outputs
         for (int j = tid; j < n; j += T2) if (xo) xo[b * n + j] = __builtin_nan("");
         for (int i = tid; i < m; i += T2) if (yo) yo[b * m + i] = __builtin_nan("");
-        if (tid == 0) p.status[b] = MPCQP_NON_CVX_;
+        if (tid == 0) fail_status(p, b);
         return;
     }
 
@@ -482,7 +482,7 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
                 if (iter == 0) {
                     for (int j = tid; j < n; j += T2) if (xo) xo[b * n + j] = __builtin_nan("");
                     for (int i = tid; i < m; i += T2) if (yo) yo[b * m + i] = __builtin_nan("");
-                    if (tid == 0) p.status[b] = MPCQP_NON_CVX_;
+                    if (tid == 0) fail_status(p, b);
                     return;
                 }
                 status = MPCQP_NON_CVX_;
@@ -890,7 +890,7 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
         status = check_termination_nl<T2>(p.self, b, cval, cinv, 1);
         if (status == MPCQP_UNSOLVED_) status = MPCQP_MAX_ITER_REACHED_;
     }
-    finalize_nl<T2>(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates);
+    finalize_nl<T2>(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates, p.ostat, p.oiter);
 #ifdef MPCQP_PHASE_PROF
     if (prof) {
         __syncthreads();
