@@ -72,6 +72,7 @@ hipError_t launch_solve(const KParams& p, long B, double* xo, double* yo, int fa
 // dense-inverse kernel (solve_dense.hip), variant 16, and its LDS bytes
 hipError_t launch_solve_dense(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st);
 size_t lds_dense_bytes(const KParams& p);
+size_t lds_w2_bytes(const KParams& p);  // solve_wave.hip, variant 10
 // solution polishing (OSQP 0.6 polish.c) after the solve; launch_solve runs it when p.polish
 hipError_t launch_polish(const KParams& p, long B, double* xo, double* yo, hipStream_t st);
 // one-wave-per-QP kernel (solve_wave.hip), variants 8 and 9

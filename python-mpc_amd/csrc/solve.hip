@@ -671,6 +671,7 @@ size_t lds_solve_bytes(const KParams& p) { return lds_base_bytes(p); }
 
 size_t lds_kernel_bytes(const KParams& p) {
     if (p.variant == 16) return lds_dense_bytes(p);
+    if (p.variant == 10) return lds_w2_bytes(p);
     return p.variant >= 11 && p.variant <= 14 ? lds_solve_bytes_big(p) : lds_solve_bytes(p);
 }
 
@@ -701,7 +702,8 @@ bool variant_fits(const KParams& p, int v) {
         // (solve_mpad): RS = 3 for 128 < m <= 192, RS = 4 for 192 < m <= 256
         case 8: return p.nb == 4 && p.amax <= 8 && p.gk <= 6 && solve_mpad(p.m) == 3 * 64 && lds_solve_bytes(p) < 65536;
         case 9: return p.nb == 4 && p.amax <= 8 && p.gk <= 8 && solve_mpad(p.m) == 4 * 64 && lds_solve_bytes(p) < 65536;
-        case 10: return p.nb == 4 && p.amax <= 8 && p.gk <= 6 && p.pk <= 4 && p.m <= 2 * 128 && lds_solve_bytes(p) < 65536;
+        case 10:  // two workgroups per CU (one wave per SIMD): up to 80 KB of LDS each
+            return p.nb == 4 && p.amax <= 8 && p.gk <= 6 && p.pk <= 4 && p.m <= 2 * 128 && lds_w2_bytes(p) <= 80 * 1024;
         case 11: case 12: case 13: {
             const int nbm = v == 11 ? 12 : v == 12 ? 18 : 24, csm = v == 11 ? 1 : 2, rsm = v == 13 ? 3 : 2;
             const int csb = (p.npad + kThreadsBig - 1) / kThreadsBig, rsb = (p.m + kThreadsBig - 1) / kThreadsBig;

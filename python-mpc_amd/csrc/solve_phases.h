@@ -746,16 +746,18 @@ __device__ __noinline__ bool factorize_pol_nl(const KParams* gp, long b) {
     return factorize<TT, KPc, true>(p, c.L, 1.0 / p.delta, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
                                     p.Si + b * (long)p.nb * SS);
 }
+// sdst: where the S_k^{-1} tiles go (default: the workspace; the two-wave kernel keeps
+// them in LDS)
 template <int TT>
-__device__ __forceinline__ bool factorize_ph(const KParams* gp, long b, double rho) {
+__device__ __forceinline__ bool factorize_ph(const KParams* gp, long b, double rho, double* sdst) {
     KPc& p = kconst(gp);
     SL2 c = carve(p);
     return factorize<TT>(p, c.L, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
-                     p.Si + b * (long)p.nb * SS);
+                     sdst ? sdst : p.Si + b * (long)p.nb * SS);
 }
 template <int TT>
-__device__ __noinline__ bool factorize_nl(const KParams* gp, long b, double rho) {
-    return factorize_ph<TT>(gp, b, rho);
+__device__ __noinline__ bool factorize_nl(const KParams* gp, long b, double rho, double* sdst = nullptr) {
+    return factorize_ph<TT>(gp, b, rho, sdst);
 }
 
 

@@ -425,7 +425,9 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
     SL2 C = carve(p);
     SLds& L = C.L;
     const double* Hg = p.H + b * (long)p.nb * SS;
-    const double* Sg = p.Si + b * (long)p.nb * SS;
+    // S_k^{-1} stays in LDS after the carve (lds_w2_bytes): at one wave per SIMD two
+    // workgroups share a CU, so the LDS is there; nothing goes to / comes from the workspace
+    double* const Sg = C.L.Acsc + 2 * ((lds_base_bytes(p) + 15) / 16);
 
     if (p.err[b]) {  // invalid data (flagged by setup/update): NaN outputs
         for (int j = tid; j < n; j += T2) if (xo) xo[b * n + j] = __builtin_nan("");
@@ -477,7 +479,7 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
             // the factorisation scratch aliases ys: y waits in the workspace's y array
             if (iter > 0)
                 for (int i = tid; i < m; i += T2) p.y[b * m + i] = L.ys[i];
-            const bool ok = factorize_nl<T2>(p.self, b, rho);
+            const bool ok = factorize_nl<T2>(p.self, b, rho, Sg);
             if (!ok) {
                 if (iter == 0) {
                     for (int j = tid; j < n; j += T2) if (xo) xo[b * n + j] = __builtin_nan("");
@@ -506,10 +508,10 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
         {
             const double* src = Sg + (long)kb * SS + r * S;
 #pragma unroll
-            for (int c = 0; c < S; ++c) SB[c] = src[c];
+            for (int c = 0; c < S; c += 2) ld2(src + c, SB[c], SB[c + 1]);
             const double* srr = Sg + (long)jr * SS + rq * S + 8 * cq;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) SR[i] = srr[i];
+            for (int i = 0; i < 8; i += 2) ld2(srr + i, SR[i], SR[i + 1]);
         }
         const int pc = kb * S + r;
         const bool cv = p.pad_var[pc] >= 0;
@@ -928,13 +930,18 @@ static hipError_t go_w(const KParams& p, long B, double* xo, double* yo, int fo,
     return hipGetLastError();
 }
 
+// the two-wave kernel's LDS: the carve plus the nb S_k^{-1} tiles
+size_t lds_w2_bytes(const KParams& p) {
+    return 16 * ((lds_base_bytes(p) + 15) / 16) + sizeof(double) * (size_t)p.nb * SS;
+}
+
 // Wave-kernel instantiations (solve.hip::variant_fits gives their preconditions).
 hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st) {
     const size_t lds = lds_solve_bytes(p);
     switch (p.variant) {
         case 8: return go_w<6, 3>(p, B, xo, yo, factor_only, st, lds);
         case 9: return go_w<8, 4>(p, B, xo, yo, factor_only, st, lds);
-        case 10: return go_w2<6, 2, 4>(p, B, xo, yo, factor_only, st, lds);
+        case 10: return go_w2<6, 2, 4>(p, B, xo, yo, factor_only, st, lds_w2_bytes(p));
         default: return hipErrorInvalidValue;
     }
 }
