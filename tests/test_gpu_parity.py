@@ -260,3 +260,31 @@ def test_alternative_kernel_variants(monkeypatch, variant, cfg, B):
     b = mpc.make_batch(cfg, B=B)
     settings = dict(warm_start=True) if cfg == 3 else dict(polish=False, warm_start=False)
     _batch_parity(b, settings)
+
+
+@pytest.mark.parametrize("settings", [
+    dict(max_iter=30),                                   # stops between checks: approximate final check
+    dict(max_iter=60, check_termination=0),              # no termination checks at all
+    dict(adaptive_rho=False),                            # fixed rho: one factorisation
+    dict(adaptive_rho_interval=50),                      # rho updates between the default ones
+    dict(alpha=1.0, rho=0.5, sigma=1e-4),                # non-default ADMM parameters
+    dict(eps_abs=1e-5, eps_rel=1e-5),                    # tight tolerances: more iterations
+    dict(scaling=0),                                     # no Ruiz equilibration
+    dict(scaled_termination=True),                       # residuals in the scaled space
+])
+def test_settings_paths_match_oracle(settings):
+    """Settings the reference never changes but osqp.OSQP accepts, each steering a
+    different path of the two-wave kernel (check cadence, final approximate check,
+    rho adaptation, unscaled / scaled residuals), against the oracle on a cfg-2
+    batch; B = 96 is not a multiple of the residency round."""
+    b = mpc.make_batch(2, B=96, seed=7)
+    s = dict(warm_start=False, polish=False)
+    s.update(settings)
+    _batch_parity(b, s)
+
+
+@pytest.mark.parametrize("B", [1, 3])
+def test_tiny_batches(B):
+    """Batches smaller than a wave of instances (one and three QPs)."""
+    b = mpc.make_batch(3, B=B, seed=11)
+    _batch_parity(b, dict(warm_start=True), min_match=1.0)
