@@ -444,6 +444,13 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
 #else
 #define PH(k)
 #endif
+#ifdef MPCQP_CHECK_PROF  // diagnostic: slots 12-14 time the run end / reductions / certificates of a check
+#define PHL(k) PH(2)
+#define PHC(k) PH(k)
+#else
+#define PHL(k) PH(k)
+#define PHC(k)
+#endif
 
     const double cval = p.scal[b * 4 + 0], cinv = p.scal[b * 4 + 1];
     double rho = p.scal[b * 4 + 2];
@@ -610,7 +617,7 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            PH(12)
+            PHL(12)
             // B: own row t_kb[r] = S_kb^{-1}[r] (b_kb + c_kb); recomputed rows < 8 of t_jr
             double t;
             {
@@ -646,7 +653,7 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            PH(13)
+            PHL(13)
             // C: x~_kb[r] = t + sum_s G_{pair_s}[q][r] t_{j_s}[q]
             {
                 double gv[3][8], tq[3][8];
@@ -674,7 +681,7 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
                 X = xnew;
             }
             __syncthreads();
-            PH(14)
+            PHL(14)
             // z~ = A x~ ; relaxed + projected z ; y ; next w
             {
                 double av[RS][K], xv[RS][K], lo[RS], up[RS];
@@ -711,6 +718,7 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
 #pragma unroll
         for (int s = 0; s < RS; ++s) { L.ys[ri[s]] = y[s]; C.Z[ri[s]] = Z[s]; C.dY[ri[s]] = dy[s]; }
         __syncthreads();
+        PHC(12)
         can_check = p.check_term && (iter % p.check_term == 0);
         const bool do_rho = p.adaptive_rho && p.rho_interval && (iter % p.rho_interval == 0);
         if (!can_check && !do_rho) break;  // max_iter reached
@@ -787,6 +795,7 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
             if (p.pad_var[tid] >= 0) sm[1] = L.qv[tid] * L.dx[tid];
             block_max<T2, 17>(mx, L.red);
             block_sum<T2, 2>(sm, L.red);
+            PHC(13)
             Res R;
             if (unscale) {
                 R.pri = mx[0]; R.dua = cinv * mx[1];
@@ -862,6 +871,7 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
                 stop = done;
             }
         }
+        PHC(14)
         if (!stop && do_rho) {
             Res R;
             R.restore(L.res);
@@ -902,7 +912,9 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
             for (int k = 0; k < 6; ++k) p.prof[b * kProfSlots + k] = L.pacc[k];
 #pragma unroll
             for (int k = 8; k < 15; ++k) p.prof[b * kProfSlots + k] = L.pacc[k];
+#ifndef MPCQP_CHECK_PROF
             p.prof[b * kProfSlots + 2] = L.pacc[12] + L.pacc[13] + L.pacc[14];
+#endif
             p.prof[b * kProfSlots + 6] = clock64() - t0c;
             p.prof[b * kProfSlots + 7] = wall_clock64() - t0w;
             p.prof[b * kProfSlots + 15] = t0w;  // absolute start (100 MHz): dispatch order / residency
@@ -910,6 +922,8 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
     }
 #endif
 #undef PH
+#undef PHL
+#undef PHC
 }
 
 template <int K, int RS, int KPK>
