@@ -146,7 +146,8 @@ __global__ __launch_bounds__(T) void k_setup(KParams p, const double* __restrict
     }
     bad = block_any<T>(bad, flag);
     for (int i = tid; i < nnzP; i += T) p.Px[b * nnzP + i] = Pv[i];
-    for (int i = tid; i < nnzA; i += T) p.Ax[b * nnzA + i] = Av[i];
+    // scaled A in the padded-CSC order the solve kernels keep in LDS (one linear load there)
+    for (int e = tid; e < nnzA; e += T) p.Ax[b * nnzA + e] = Av[acsc_v[e]];
     for (int pc = tid; pc < npad; pc += T) {
         p.q[b * npad + pc] = qv[pc];
         p.D[b * npad + pc] = Dv[pc];
@@ -236,7 +237,7 @@ __global__ __launch_bounds__(T) void k_warm(KParams p, const double* __restrict_
     const double* x = p.x + b * npad;
     for (int i = tid; i < m; i += T) {
         double s = 0.0;
-        for (int e = p.acsr_ptr[i]; e < p.acsr_ptr[i + 1]; ++e) s += Ax[p.acsr_v[e]] * x[p.acsr_col[e]];
+        for (int e = p.acsr_ptr[i]; e < p.acsr_ptr[i + 1]; ++e) s += Ax[p.acsr_pos[e]] * x[p.acsr_col[e]];
         p.z[b * m + i] = s;
     }
 }

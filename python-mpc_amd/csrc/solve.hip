@@ -291,7 +291,7 @@ __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ 
     double rho = p.scal[b * 4 + 2];
     const double sigma = p.sigma, alpha = p.alpha;
     const bool warm = p.warm_start != 0;
-    for (int e = tid; e < nnzA; e += T) L.Acsc[e] = p.Ax[b * nnzA + p.acsc_v[e]];
+    for (int e = tid; e < nnzA; e += T) L.Acsc[e] = p.Ax[b * nnzA + e];
     if (tid == 0) L.Acsc[nnzA] = 0.0;  // the gather lists' padding slot
     for (int v = tid; v < nnzP; v += T) L.Pv[v] = p.Px[b * nnzP + v];
     if (tid == 0) L.Pv[nnzP] = 0.0;
@@ -555,7 +555,7 @@ __global__ __launch_bounds__(T) void k_polish(KParams p, double* __restrict__ xo
     const double cinv = p.scal[b * 4 + 1], idelta = 1.0 / p.delta;
     const double* Fg = p.F + b * (long)p.nb * SS;
     const double* Sg = p.Si + b * (long)p.nb * SS;
-    for (int e = tid; e < nnzA; e += T) L.Acsc[e] = p.Ax[b * nnzA + p.acsc_v[e]];
+    for (int e = tid; e < nnzA; e += T) L.Acsc[e] = p.Ax[b * nnzA + e];
     if (tid == 0) L.Acsc[nnzA] = 0.0;
     for (int v = tid; v < nnzP; v += T) L.Pv[v] = p.Px[b * nnzP + v];
     if (tid == 0) L.Pv[nnzP] = 0.0;

@@ -592,7 +592,7 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
     double rho = p.scal[b * 4 + 2];
     const double sigma = p.sigma, alpha = p.alpha;
     const bool warm = p.warm_start != 0;
-    for (int e = tid; e < nnzA; e += TTK) L.Acsc[e] = p.Ax[b * nnzA + p.acsc_v[e]];
+    for (int e = tid; e < nnzA; e += TTK) L.Acsc[e] = p.Ax[b * nnzA + e];
     if (tid == 0) L.Acsc[nnzA] = 0.0;  // the gather lists' padding slot
     for (int v = tid; v < nnzP; v += TTK) L.Pv[v] = p.Px[b * nnzP + v];
     if (tid == 0) L.Pv[nnzP] = 0.0;

@@ -94,7 +94,7 @@ __global__ __launch_bounds__(TD, 2) void k_solve_d(KParams p, double* __restrict
     double rho = p.scal[b * 4 + 2];
     const double sigma = p.sigma, alpha = p.alpha;
     const bool warm = p.warm_start != 0;
-    for (int e = tid; e < nnzA; e += TD) L.Acsc[e] = p.Ax[b * nnzA + p.acsc_v[e]];
+    for (int e = tid; e < nnzA; e += TD) L.Acsc[e] = p.Ax[b * nnzA + e];
     if (tid == 0) L.Acsc[nnzA] = 0.0;  // the gather lists' padding slot
     for (int v = tid; v < nnzP; v += TD) L.Pv[v] = p.Px[b * nnzP + v];
     if (tid == 0) L.Pv[nnzP] = 0.0;

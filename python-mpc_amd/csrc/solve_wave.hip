@@ -85,7 +85,7 @@ __global__ __launch_bounds__(TW, 1) void k_solve_w(KParams p, double* __restrict
     double rho = p.scal[b * 4 + 2];
     const double sigma = p.sigma, alpha = p.alpha;
     const bool warm = p.warm_start != 0;
-    for (int e = lane; e < nnzA; e += TW) L.Acsc[e] = p.Ax[b * nnzA + p.acsc_v[e]];
+    for (int e = lane; e < nnzA; e += TW) L.Acsc[e] = p.Ax[b * nnzA + e];
     if (lane == 0) L.Acsc[nnzA] = 0.0;  // the gather lists' padding slot
     for (int v = lane; v < nnzP; v += TW) L.Pv[v] = p.Px[b * nnzP + v];
     if (lane == 0) L.Pv[nnzP] = 0.0;
@@ -456,7 +456,7 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
     double rho = p.scal[b * 4 + 2];
     const double sigma = p.sigma, alpha = p.alpha;
     const bool warm = p.warm_start != 0;
-    for (int e = tid; e < nnzA; e += T2) L.Acsc[e] = p.Ax[b * nnzA + p.acsc_v[e]];
+    for (int e = tid; e < nnzA; e += T2) L.Acsc[e] = p.Ax[b * nnzA + e];
     if (tid == 0) L.Acsc[nnzA] = 0.0;  // the gather lists' padding slot
     for (int v = tid; v < nnzP; v += T2) L.Pv[v] = p.Px[b * nnzP + v];
     if (tid == 0) L.Pv[nnzP] = 0.0;
