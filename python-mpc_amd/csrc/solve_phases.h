@@ -75,11 +75,16 @@ __device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restri
         v[jj + 1] = t2.y;
     }
     double minpiv = 1.0;  // -1 once a pivot is not positive (NaN-safe running flag)
+    // Row scaling deferred: the lane keeps its row as sc * v.  Pivoting row p only sets
+    // its scale to 1 / piv (no pass over its elements), so every pivot step is one
+    // masked FMA pass; the true values are published per pivot (one multiply) and
+    // restored once at the end.  iv = 1 / sc, exactly piv for pivoted rows.
+    double sc = 1.0, iv = 1.0;
     auto pivot = [&](const int p, const int pj) __attribute__((always_inline)) {
         const int ph = p >> 4;
         double* rb = buf + (pj & 1) * S;
         if (h == ph) {
-            const double vp = Compact ? pick16(v, pj) : v[pj];
+            const double vp = sc * (Compact ? pick16(v, pj) : v[pj]);
             rb[i] = i < p ? -vp : vp;  // row p = +-column p
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -100,19 +105,19 @@ __device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restri
         double d = __builtin_amdgcn_rcp(piv);
         d = __builtin_fma(d, __builtin_fma(-piv, d, 1.0), d);
         d = __builtin_fma(d, __builtin_fma(-piv, d, 1.0), d);
-        // row update: the pivot row becomes row_p / piv, every other row loses M_ip / piv
-        // times row_p (measured: this form beats a branch-free keep * v - cd * row_p)
-        if (i == p) {
-#pragma unroll
-            for (int jj = 0; jj < 16; ++jj) v[jj] = rowv[jj] * d;
-        } else {
-            const double cd = colv * d;
+        // every other row loses M_ip / piv times row_p (in its own scale); row p keeps
+        // its elements and takes the scale 1 / piv
+        const double cd = (colv * d) * iv;
+        if (i != p) {
 #pragma unroll
             for (int jj = 0; jj < 16; ++jj) v[jj] = __builtin_fma(-cd, rowv[jj], v[jj]);
+        } else {
+            sc = d;
+            iv = piv;
         }
         if (h == ph) {
-            if (Compact) put16(v, pj, i == p ? d : -colv * d);
-            else v[pj] = i == p ? d : -colv * d;
+            if (Compact) put16(v, pj, i == p ? 1.0 : -cd);
+            else v[pj] = i == p ? 1.0 : -cd;
         }
     };
     if constexpr (Compact) {
@@ -124,8 +129,9 @@ __device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restri
     }
 #pragma unroll
     for (int jj = 0; jj < 16; jj += 2) {
-        *(double2*)(T + i * S + 16 * h + jj) = make_double2(v[jj], v[jj + 1]);
-        *(double2*)(Sgk + i * S + 16 * h + jj) = make_double2(v[jj], v[jj + 1]);
+        const double2 t2 = make_double2(sc * v[jj], sc * v[jj + 1]);
+        *(double2*)(T + i * S + 16 * h + jj) = t2;
+        *(double2*)(Sgk + i * S + 16 * h + jj) = t2;
     }
     return minpiv > 0.0;
 }
