@@ -134,7 +134,7 @@ size_t workspace_bytes(const Plan& pl, long B, bool with_io) {
     carve<double>(off, B * m); carve<double>(off, B * n);              // certificates
     for (int i = 0; i < 4; ++i) carve<double>(off, B);
     carve<signed char>(off, B * m);
-    for (int i = 0; i < 5; ++i) carve<int>(off, B);
+    for (int i = 0; i < 6; ++i) carve<int>(off, B);
     carve<long long>(off, B * kProfSlots);
     carve<KParams>(off, 1);
     if (with_io) {
@@ -188,6 +188,14 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
     k.rho_upd = (int*)(base + carve<int>(off, B));
     k.pstat = (int*)(base + carve<int>(off, B));
     k.err = (int*)(base + carve<int>(off, B));
+    {  // dispatch order (kernels.hip::k_order), identity until the first solve
+        int* ord = (int*)(base + carve<int>(off, B));
+        std::vector<int> id(B);
+        for (long i = 0; i < B; ++i) id[i] = (int)i;
+        HIPCHK(hipMemcpy(ord, id.data(), sizeof(int) * B, hipMemcpyHostToDevice));
+        k.order = ord;
+        if (const char* ev = getenv("MPCQP_DISPATCH"); ev && !strcmp(ev, "identity")) k.order = nullptr;  // A/B
+    }
     k.prof = nullptr;
     if (const char* ev = getenv("MPCQP_PHASE_PROF"); ev && ev[0] == '1')
         k.prof = (long long*)(base + carve<long long>(off, B * kProfSlots));
@@ -405,6 +413,7 @@ int mpcqp_solve_batch(mpcqp_handle* h, double* x, double* y, int32_t* status, in
         HIPCHK(hipEventRecord(s.ev0, s.stream));
         HIPCHK(launch_solve(s.kp, s.B, s.out_x, s.out_y, 0, s.stream));
         HIPCHK(hipEventRecord(s.ev1, s.stream));
+        HIPCHK(launch_order(s.kp, s.B, s.stream));
         if (x) HIPCHK(hipMemcpyAsync(x + s.b0 * n, s.out_x, sizeof(double) * s.B * n, hipMemcpyDeviceToHost, s.stream));
         if (y) HIPCHK(hipMemcpyAsync(y + s.b0 * m, s.out_y, sizeof(double) * s.B * m, hipMemcpyDeviceToHost, s.stream));
         if (status) HIPCHK(hipMemcpyAsync(status + s.b0, s.kp.status, sizeof(int) * s.B, hipMemcpyDeviceToHost, s.stream));
@@ -521,6 +530,7 @@ int mpcqp_solve_device(mpcqp_handle* h, double* dx, double* dy, int32_t* dstatus
     HIPCHK(launch_solve(k, s.B, dx, dy, 0, st));
     if (int e = ev_end(h, h->ev_solve, st)) return e;
     HIPCHK(hipEventRecord(s.ev1, st));
+    HIPCHK(launch_order(s.kp, s.B, st));
     h->timed = true;
     return 0;
 }

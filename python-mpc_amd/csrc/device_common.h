@@ -32,6 +32,11 @@ __device__ __forceinline__ KPc& kconst(const KParams* gp) {
 constexpr int S = kS;
 constexpr int SS = kS * kS;
 
+// the instance a solve-kernel workgroup works on (KParams::order); kept in an SGPR
+__device__ __forceinline__ long instance_of(const KParams& p) {
+    return p.order ? (long)__builtin_amdgcn_readfirstlane(p.order[blockIdx.x]) : (long)blockIdx.x;
+}
+
 __device__ __forceinline__ double cmax(double a, double b) { return a > b ? a : b; }
 __device__ __forceinline__ double cmin(double a, double b) { return a < b ? a : b; }
 __device__ __forceinline__ double limit_scaling(double d) {

@@ -50,6 +50,9 @@ struct KParams {
     int max_iter, scaling, check_term, warm_start, adaptive_rho, rho_interval, scaled_term;
     int polish, refine_iter;
     int* pstat;  // per instance: 0 polish not run, 1 polished solution taken, -1 rejected
+    // dispatch order of the solve kernels: workgroup slot -> instance, or null (identity).
+    // Rewritten after every solve by launch_order (longest previous solve first).
+    const int* order;
 };
 
 size_t lds_setup_bytes(const KParams& p);
@@ -64,6 +67,9 @@ hipError_t launch_setup(const KParams& p, long B, const double* Px, const double
 hipError_t launch_update(const KParams& p, long B, const double* q, const double* l, const double* u,
                          hipStream_t st);
 hipError_t launch_warm(const KParams& p, long B, const double* x, const double* y, hipStream_t st);
+// longest-processing-time dispatch: sort the instances by the iteration count of the
+// solve just run (descending) into p.order, for the next solve on this workspace
+hipError_t launch_order(const KParams& p, long B, hipStream_t st);
 int solve_variant(const KParams& p);  // -1: no instantiation fits the plan
 int solve_mode(int variant);
 int solve_threads(int variant);  // workgroup size of the variant's kernel

@@ -270,4 +270,48 @@ hipError_t launch_warm(const KParams& p, long B, const double* x, const double* 
     hipLaunchKernelGGL(k_warm, dim3((unsigned)B), dim3(T), 0, st, p, x, y);
     return hipGetLastError();
 }
+
+// ------------------------------------------------------------------ order --
+// Dispatch order for the next solve on this workspace: longest previous solve first.
+// A batch larger than the resident slots (cfg 2: 1024 instances, 512 two-wave
+// workgroups at once) runs in rounds, and the kernel ends with its slowest instance;
+// an instance that needs 350 ADMM iterations against a mean of 63 should start in
+// the first round, not 200 us late.  Consecutive solves on one handle (the receding-
+// horizon loop: update/setup, solve) see nearby problems, so the previous iteration
+// count predicts the next.  The order only moves instances between workgroup slots:
+// every instance's arithmetic, and so its result, is unchanged.
+// One workgroup: counting sort on iter >> shift (descending), 256 bins.
+constexpr int kOrderT = 1024, kOrderBins = 256;
+__global__ __launch_bounds__(kOrderT) void k_order(const int* __restrict__ iter, int* __restrict__ order, long B,
+                                                  int shift) {
+    __shared__ int cnt[kOrderBins];
+    const int t = threadIdx.x;
+    if (t < kOrderBins) cnt[t] = 0;
+    __syncthreads();
+    auto bin = [&](long i) {
+        const int k = iter[i] >> shift;
+        return kOrderBins - 1 - (k < kOrderBins - 1 ? k : kOrderBins - 1);
+    };
+    for (long i = t; i < B; i += kOrderT) atomicAdd(&cnt[bin(i)], 1);
+    __syncthreads();
+    if (t == 0) {
+        int s = 0;
+        for (int k = 0; k < kOrderBins; ++k) {
+            const int c = cnt[k];
+            cnt[k] = s;
+            s += c;
+        }
+    }
+    __syncthreads();
+    for (long i = t; i < B; i += kOrderT) order[atomicAdd(&cnt[bin(i)], 1)] = (int)i;
+}
+
+hipError_t launch_order(const KParams& p, long B, hipStream_t st) {
+    if (!p.order || B <= 256) return hipSuccess;  // up to 256 instances all start at once
+    int shift = 0;
+    while ((p.max_iter >> shift) >= kOrderBins) ++shift;
+    hipLaunchKernelGGL(k_order, dim3(1), dim3(kOrderT), 0, st, (const int*)p.iter, const_cast<int*>(p.order), B,
+                       shift);
+    return hipGetLastError();
+}
 }  // namespace mpcqp

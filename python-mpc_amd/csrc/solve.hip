@@ -255,7 +255,7 @@ template <int NB, int A, int K, int CS, int RS, int W, bool TRI>
 __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ xo, double* __restrict__ yo,
                                                 int factor_only) {
     const int tid = threadIdx.x;
-    const long b = blockIdx.x;
+    const long b = instance_of(p);
     const int n = p.n, m = p.m, npad = p.npad, nnzP = p.nnzP, nnzA = p.nnzA;
     SL2 C = carve(p);
     SLds& L = C.L;

@@ -558,7 +558,7 @@ template <int TTK, int NS, int K, int CS, int RS>
 __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restrict__ xo, double* __restrict__ yo,
                                                    int factor_only) {
     const int tid = threadIdx.x;
-    const long b = blockIdx.x;
+    const long b = instance_of(p);
     const int n = p.n, m = p.m, npad = p.npad, nnzP = p.nnzP, nnzA = p.nnzA, nb = p.nb, amax = p.amax;
     SL2 C = carve(p);
     SLds& L = C.L;

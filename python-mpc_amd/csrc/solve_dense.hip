@@ -64,7 +64,7 @@ __global__ __launch_bounds__(TD, 2) void k_solve_d(KParams p, double* __restrict
     static_assert(R % 4 == 0, "half rows must be whole 16-byte pairs");
     constexpr int H = R / 2;
     const int tid = threadIdx.x, jr = tid >> 1, h = tid & 1;  // row jr, half h
-    const long b = blockIdx.x;
+    const long b = instance_of(p);
     const int n = p.n, m = p.m, npad = p.npad, nnzP = p.nnzP, nnzA = p.nnzA;
     SL2 C = carve(p);
     SLds& L = C.L;

@@ -58,7 +58,7 @@ __global__ __launch_bounds__(TW, 1) void k_solve_w(KParams p, double* __restrict
     const int h = lane >> 5, r = lane & 31, rr = lane >> 3, ch = lane & 7;
     const int kb0 = h, kb1 = 3 - h;
     constexpr int NB = 4, NP = NB * (NB - 1) / 2;  // exactly four blocks (solve.hip::variant_fits)
-    const long b = blockIdx.x;
+    const long b = instance_of(p);
     const int n = p.n, m = p.m, npad = p.npad, nnzP = p.nnzP, nnzA = p.nnzA;
     SL2 C = carve(p);
     SLds& L = C.L;
@@ -420,7 +420,7 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
     const int jr = w ? 3 : 1 + h;              // block of the recomputed t rows
     const int rq = r >> 2, cq = r & 3;         // recomputed row / column chunk
     constexpr int NB = 4, NP = NB * (NB - 1) / 2;  // exactly four blocks (solve.hip::variant_fits)
-    const long b = blockIdx.x;
+    const long b = instance_of(p);
     const int n = p.n, m = p.m, npad = p.npad, nnzP = p.nnzP, nnzA = p.nnzA;
     SL2 C = carve(p);
     SLds& L = C.L;

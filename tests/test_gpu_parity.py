@@ -288,3 +288,42 @@ def test_tiny_batches(B):
     """Batches smaller than a wave of instances (one and three QPs)."""
     b = mpc.make_batch(3, B=B, seed=11)
     _batch_parity(b, dict(warm_start=True), min_match=1.0)
+
+
+@pytest.mark.parametrize("cfg,B", [(2, 1024), (3, 1024), (5, 320)])
+def test_longest_first_dispatch_is_result_neutral(monkeypatch, cfg, B):
+    """kernels.hip::k_order reorders the solve kernel's workgroups by the previous
+    solve's iteration counts.  One handle solves batch X (identity order; the order
+    is then set from X's counts), then setup()+solve() batch Y in the reordered
+    dispatch; that must be bit-identical to a handle that dispatches Y in identity
+    order (MPCQP_DISPATCH=identity).  An instance the reordered launch skipped would
+    still hold X's solution."""
+    import torch
+    from osqp_amd import DeviceBatch
+    bx, by = mpc.make_batch(cfg, B=B, seed=101), mpc.make_batch(cfg, B=B, seed=202)
+    s = {k: v for k, v in bx["settings"].items() if k != "verbose"}
+    s.update(warm_start=False, polish=False)
+    dev = torch.device("cuda", 0)
+    n, m = bx["n"], bx["m"]
+
+    def put(b):
+        return [torch.from_numpy(np.ascontiguousarray(b[k])).to(dev) for k in ("Px", "Ax", "q", "l", "u")]
+
+    def out():
+        return (torch.empty((B, n), dtype=torch.float64, device=dev), torch.empty((B, m), dtype=torch.float64, device=dev),
+                torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev))
+
+    X, Y = put(bx), put(by)
+    lpt = DeviceBatch(bx["P"], bx["A"], B, device=0, **s)
+    o1 = out()
+    lpt.setup(*X); lpt.solve(*o1)
+    lpt.setup(*Y); lpt.solve(*o1)
+    lpt.synchronize()
+    monkeypatch.setenv("MPCQP_DISPATCH", "identity")
+    ref = DeviceBatch(bx["P"], bx["A"], B, device=0, **s)
+    o0 = out()
+    ref.setup(*Y); ref.solve(*o0)
+    ref.synchronize()
+    for a, b in zip(o1, o0):
+        assert torch.equal(a, b)
+    assert o1[3].max().item() > o1[3].min().item()  # the counts vary, so the order is not the identity
