@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=None, help="instances per GPU (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-dispatch-ab", action="store_true",
+                    help="skip the identity-dispatch diagnostic (rocprof passes: one handle's launches only)")
     return ap.parse_args()
 
 
@@ -126,11 +128,11 @@ def main():
         xs, ys = warm_shift(b["N"], 8, 2, dx, dy)
         torch.cuda.synchronize()
 
-    def step():
-        solver.setup(dPx, dAx, dq, dl, du)
+    def step(sv=solver):
+        sv.setup(dPx, dAx, dq, dl, du)
         if warm:
-            solver.warm_start(xs, ys)
-        solver.solve(dx, dy, dst, dit)
+            sv.warm_start(xs, ys)
+        sv.solve(dx, dy, dst, dit)
 
     for _ in range(args.warmup):
         step()
@@ -156,6 +158,24 @@ def main():
     kt = solver.timing_read()
     solver.timing(False)
     dt = max_over_ranks(t1 - t0, world)
+
+    # Diagnostic A/B, outside the timed region and never `value`: the same steps on a
+    # handle that dispatches in identity order (MPCQP_DISPATCH=identity) instead of
+    # longest-previous-solve-first (kernels.hip::k_order).  The bench re-solves one
+    # batch, so there the previous iteration counts predict the next ones exactly.
+    value_identity = None
+    if not args.no_dispatch_ab:
+        os.environ["MPCQP_DISPATCH"] = "identity"
+        ident = DeviceBatch(P, A, B, device=local, **settings)
+        del os.environ["MPCQP_DISPATCH"]
+        step(ident)
+        ident.synchronize()
+        ta = time.perf_counter()
+        for _ in range(args.steps):
+            step(ident)
+        ident.synchronize()
+        value_identity = B * args.steps / (time.perf_counter() - ta)
+        del ident
 
     value = world * B * args.steps / dt
     nnzP, nnzA = P.nnz, A.nnz
@@ -219,6 +239,8 @@ def main():
                        "step": ("setup()+warm_start(previous solution shifted one stage)+solve()" if warm else
                                 "setup()+solve()") + " per instance, inputs resident in HBM",
                        "parallelism": f"batch-shard x{world}",
+                       "dispatch": "longest previous solve first (kernels.hip::k_order)",
+                       "value_identity_dispatch_rank0": value_identity,
                        "iters_mean": float(iters.mean()), "iters_max": int(iters.max()),
                        "solved_frac": float(np.mean(status == 1)),
                        "plan": {"nb": info["nb"], "block": S, "amax": info["amax"], "lds_bytes": info["lds_bytes_solve"],
