@@ -8,7 +8,12 @@ vehicle_lateral_mpc_slack_increment.py:32-43), fp64, synthetic initial states.
 One step = one pass of the hot path over the batch: osqp setup() + solve() for
 every instance (Ruiz scaling, KKT factorisation, ADMM to eps 1e-3, unscaling)
 -- the reference's per-call pattern (mpc_kinematics.py:194-198), with the
-inputs already resident in HBM when the timed region starts.
+inputs already resident in HBM when the timed region starts.  Every step solves
+a DIFFERENT batch: the same vehicles with their initial states jittered by
++-2 % of the D2 ranges (a receding-horizon proxy: nearby problems, as in the
+reference's closed loops), so the solver's longest-previous-solve-first
+dispatch (kernels.hip::k_order) predicts each step from the previous, different
+QP -- never from a repeat of the same one.
 
 Multi-GPU: one process per GPU (torch.distributed.run); every rank solves its
 own batch (weak scaling, no data-path collective); timing = barrier +
@@ -33,6 +38,16 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 import numpy as np  # noqa: E402
 
+JITTER = 0.02  # per-step jitter of the initial states, fraction of the D2 half-range
+# D2 ranges of the initial-state rows [:nx0] of l = u, per layout; the
+# jittered states are clipped to them (cfg 5's accel at its bound would make x~_0 infeasible)
+X0_RANGES = {
+    "vanilla": [(-.05, .05), (-.1, .1), (-10 * np.pi / 180, 10 * np.pi / 180), (-3., 3.)],
+    "slack": [(-.05, .05), (-.1, .1), (-10 * np.pi / 180, 10 * np.pi / 180), (-3., 3.),
+              (-5 * np.pi / 180, 5 * np.pi / 180)],
+    "dynamic": [(0., 0.), (0., 0.), (-np.pi / 8, np.pi / 8), (5., 25.), (-.5, .5), (-.2, .2),
+                (-5 * np.pi / 180, 5 * np.pi / 180), (-1., 1.)],
+}
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6  # MI355X fp64 vector peak (spec) -- diagnostic only
 
@@ -73,6 +88,27 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
+def bound_sequence(b, count, seed, to_dev):
+    from osqp_amd import mpc
+    """`count` distinct (l, u) device pairs of batch `b`: the first unchanged, each later
+    one with the initial-state rows (l = u = -x0) jittered (JITTER, clipped to the D2
+    ranges).  Everything else of the QP (P, A, q, the other bounds) is shared."""
+    rng = np.random.default_rng(seed + 7919)
+    lo, hi = (np.array(v) for v in zip(*X0_RANGES[mpc.CONFIGS[b["cfg"]]["layout"]]))
+    nx0 = lo.size
+    x0 = -b["l"][:, :nx0]
+    dl0, du0 = to_dev(b["l"]), to_dev(b["u"])
+    seq = [(dl0, du0)]
+    for _ in range(count - 1):
+        xt = np.clip(x0 + JITTER * 0.5 * (hi - lo) * rng.uniform(-1, 1, x0.shape), lo, hi)
+        dxt = to_dev(-xt)
+        dl, du = dl0.clone(), du0.clone()
+        dl[:, :nx0] = dxt
+        du[:, :nx0] = dxt
+        seq.append((dl, du))
+    return seq
+
+
 def pmc_traffic(workload, batch):
     """HBM bytes per k_solve launch from rocprofv3 PMC passes committed under
     profiles/ (tools/pmc_traffic.py writes profiles/traffic_<workload>_b<B>.json:
@@ -89,7 +125,7 @@ def main():
     args = parse()
     import torch
     import torch.distributed as dist
-    from osqp_amd import DeviceBatch, mpc, _drop_common_zeros
+    from osqp_amd import DeviceBatch, _drop_common_zeros
 
     world, rank, local = dist_env()
     if world > 1:
@@ -97,6 +133,7 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
+    from osqp_amd import mpc
     spec = mpc.CONFIGS[args.config]
     B = args.batch or (spec["B"] if args.config != 4 else spec["B"] // 8)
     b = mpc.make_batch(args.config, B=B, seed=instance_seed(args.config, rank))
@@ -108,7 +145,10 @@ def main():
     def to_dev(a, dtype=torch.float64):
         return torch.from_numpy(np.ascontiguousarray(a)).to(dev, dtype=dtype).contiguous()
 
-    dPx, dAx, dq, dl, du = (to_dev(a) for a in (Px, Ax, b["q"], b["l"], b["u"]))
+    dPx, dAx, dq = (to_dev(a) for a in (Px, Ax, b["q"]))
+    # the base batch, then one distinct batch per warmup and timed step
+    seq = bound_sequence(b, 1 + args.warmup + args.steps, instance_seed(args.config, rank), to_dev)
+    dl, du = seq[0]
     dx = torch.empty((B, n), dtype=torch.float64, device=dev)
     dy = torch.empty((B, m), dtype=torch.float64, device=dev)
     dst = torch.empty(B, dtype=torch.int32, device=dev)
@@ -128,17 +168,20 @@ def main():
         xs, ys = warm_shift(b["N"], 8, 2, dx, dy)
         torch.cuda.synchronize()
 
-    def step(sv=solver):
-        sv.setup(dPx, dAx, dq, dl, du)
+    def step(t, sv=solver):
+        sl, su = seq[t]
+        sv.setup(dPx, dAx, dq, sl, su)
         if warm:
             sv.warm_start(xs, ys)
         sv.solve(dx, dy, dst, dit)
 
-    for _ in range(args.warmup):
-        step()
+    step(0)  # the base batch: its statuses / iterations are the ones the CPU baseline is compared with
     solver.synchronize()
     status = dst.cpu().numpy()
     iters = dit.cpu().numpy()
+    for t in range(1, 1 + args.warmup):
+        step(t)
+    solver.synchronize()
 
     def barrier():
         if world > 1:
@@ -149,30 +192,31 @@ def main():
     solver.synchronize()
     solver.timing(True)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for t in range(1 + args.warmup, 1 + args.warmup + args.steps):
+        step(t)
     solver.synchronize()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
     kt = solver.timing_read()
+    iters_last = dit.cpu().numpy()  # the last timed step's batch (the flop model's iteration count)
     solver.timing(False)
     dt = max_over_ranks(t1 - t0, world)
 
-    # Diagnostic A/B, outside the timed region and never `value`: the same steps on a
-    # handle that dispatches in identity order (MPCQP_DISPATCH=identity) instead of
-    # longest-previous-solve-first (kernels.hip::k_order).  The bench re-solves one
-    # batch, so there the previous iteration counts predict the next ones exactly.
+    # Diagnostic A/B, outside the timed region and never `value`: the same sequence of
+    # batches on a handle that dispatches in identity order (MPCQP_DISPATCH=identity)
+    # instead of longest-previous-solve-first (kernels.hip::k_order).
     value_identity = None
     if not args.no_dispatch_ab:
         os.environ["MPCQP_DISPATCH"] = "identity"
         ident = DeviceBatch(P, A, B, device=local, **settings)
         del os.environ["MPCQP_DISPATCH"]
-        step(ident)
+        for t in range(1 + args.warmup):
+            step(t, ident)
         ident.synchronize()
         ta = time.perf_counter()
-        for _ in range(args.steps):
-            step(ident)
+        for t in range(1 + args.warmup, 1 + args.warmup + args.steps):
+            step(t, ident)
         ident.synchronize()
         value_identity = B * args.steps / (time.perf_counter() - ta)
         del ident
@@ -188,7 +232,7 @@ def main():
     # elementwise ~12 flops per row/column
     S = info["block"]
     flop_iter = 2 * (3 * info["nb"] * S * S + 2 * nnzA) + 12 * (n + m)
-    fp64_tflops = flop_iter * float(iters.astype(np.float64).sum()) / (solve_ms * 1e-3) / 1e12
+    fp64_tflops = flop_iter * float(iters_last.astype(np.float64).sum()) / (solve_ms * 1e-3) / 1e12
 
     traffic = pmc_traffic(spec["name"], B)
 
@@ -232,14 +276,16 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (seeded lane-tracking initial states, SURVEY.md §8d D2)",
+            "data": "synthetic (seeded lane-tracking initial states, SURVEY.md §8d D2, jittered per step)",
             "config": {"workload": spec["name"], "config_index": args.config, "batch_per_gpu": B,
                        "global_batch": world * B, "horizon_N": b["N"], "n": n, "m": m,
                        "nnz_triuP": nnzP, "nnz_A": nnzA, "eps_abs": 1e-3, "eps_rel": 1e-3,
-                       "step": ("setup()+warm_start(previous solution shifted one stage)+solve()" if warm else
-                                "setup()+solve()") + " per instance, inputs resident in HBM",
+                       "step": ("setup()+warm_start(base solution shifted one stage)+solve()" if warm else
+                                "setup()+solve()") + " per instance, inputs resident in HBM; a distinct batch per "
+                                f"step (initial states jittered +-{JITTER:.0%} of the D2 ranges)",
                        "parallelism": f"batch-shard x{world}",
-                       "dispatch": "longest previous solve first (kernels.hip::k_order)",
+                       "dispatch": "longest previous solve first (kernels.hip::k_order), predicted from the "
+                                   "previous step's different batch",
                        "value_identity_dispatch_rank0": value_identity,
                        "iters_mean": float(iters.mean()), "iters_max": int(iters.max()),
                        "solved_frac": float(np.mean(status == 1)),

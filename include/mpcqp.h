@@ -32,12 +32,15 @@
  * caller-allocated buffers.  Host-pointer entry points block until results
  * are on the host; *_device entry points take device pointers on the
  * handle's (single) device and enqueue on `stream` (hipStream_t, NULL = the
- * handle's own stream) without synchronising.  Calls on one handle must be
- * stream-ordered (one stream, or the caller's events between streams): they
- * share the handle's workspace, including the dispatch order each solve
- * rewrites for the next one (longest previous solve first; setting
- * MPCQP_DISPATCH=identity before mpcqp_create / mpcqp_setup_batch turns it
- * off).  The order moves instances between workgroups, never their results.
+ * handle's own stream) without synchronising.  Calls on one handle are
+ * stream-ordered by the library: they share the handle's workspace, including
+ * the dispatch order each solve rewrites for the next one (longest previous
+ * solve first; setting MPCQP_DISPATCH=identity before mpcqp_create /
+ * mpcqp_setup_batch turns it off), so a call enqueued on a different stream
+ * than the previous call on the handle first waits (hipStreamWaitEvent) for
+ * that call's work.  The caller still orders its own buffers (inputs written
+ * on another stream, outputs read elsewhere).  The order moves instances
+ * between workgroups, never their results.
  *
  * Errors: entry points return 0 on success or an MPCQP_E* code; the message
  * is in mpcqp_last_error() (thread-local).  Numerical outcomes never fail a

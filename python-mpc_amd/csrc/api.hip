@@ -66,6 +66,10 @@ struct Shard {
     long b0 = 0, B = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // stream ordering of the calls on the handle: the last call's work is recorded in
+    // last_ev on last_st, and a call on another stream waits for it first (enter/leave)
+    hipEvent_t last_ev = nullptr;
+    hipStream_t last_st = nullptr;
     int* dplan = nullptr;
     void* dws = nullptr;    // one allocation for the whole workspace
     void* dio = nullptr;    // staging for the host-pointer API
@@ -151,6 +155,7 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
     HIPCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
     HIPCHK(hipEventCreate(&s.ev0));
     HIPCHK(hipEventCreate(&s.ev1));
+    HIPCHK(hipEventCreateWithFlags(&s.last_ev, hipEventDisableTiming));
     if (int e = upload_plan(pl, s)) return e;
     const long B = s.B, n = pl.n, m = pl.m, np = pl.npad, nb = pl.nb;
     const long SS = (long)kS * kS;
@@ -230,6 +235,13 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
         k.variant = v;
     }
     k.mode = solve_mode(k.variant);
+    {  // resident solve workgroups: below this batch size the dispatch order is moot
+        int ncu = 0;
+        HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, s.dev));
+        const int occ = solve_blocks_per_cu(k);
+        if (occ < 0) return fail(MPCQP_EDEVICE, "occupancy query for solve variant %d failed", k.variant);
+        k.slots = (long)ncu * occ;
+    }
     k.self = (const KParams*)(base + carve<KParams>(off, 1));
     HIPCHK(hipMemcpy((void*)k.self, &k, sizeof(KParams), hipMemcpyHostToDevice));
     if (size_t lds = lds_kernel_bytes(k); lds > 160 * 1024)
@@ -304,6 +316,20 @@ int sync_all(mpcqp_handle* h) {
     return 0;
 }
 
+// Every call enqueues on one stream; work of the previous call on the handle that went
+// to another stream is waited for first.  The handle's workspace -- including the
+// dispatch order each solve rewrites for the next (kernels.hip::k_order) -- is then
+// never read by one stream while another writes it, whatever streams the caller uses.
+int stream_enter(Shard& s, hipStream_t st) {
+    if (s.last_st && s.last_st != st) HIPCHK(hipStreamWaitEvent(st, s.last_ev, 0));
+    return 0;
+}
+int stream_leave(Shard& s, hipStream_t st) {
+    HIPCHK(hipEventRecord(s.last_ev, st));
+    s.last_st = st;
+    return 0;
+}
+
 int check_err_flags(mpcqp_handle* h) {
     for (auto& s : h->shards) {
         std::vector<int> err(s.B);
@@ -364,7 +390,7 @@ int mpcqp_setup_batch(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi
         HIPCHK(hipMemcpyAsync(s.in_l, l + b0 * m, sizeof(double) * Bs * m, hipMemcpyHostToDevice, s.stream));
         HIPCHK(hipMemcpyAsync(s.in_u, u + b0 * m, sizeof(double) * Bs * m, hipMemcpyHostToDevice, s.stream));
         HIPCHK(launch_setup(s.kp, Bs, s.in_Px, s.in_Ax, s.in_q, s.in_l, s.in_u, s.stream));
-        return 0;
+        return stream_leave(s, s.stream);
     };
     for (auto& s : h->shards)
         if (int e = upload(s)) { mpcqp_free(h); return e; }
@@ -381,10 +407,12 @@ int mpcqp_update_batch(mpcqp_handle* h, const double* q, const double* l, const 
     const long n = h->n, m = h->m;
     for (auto& s : h->shards) {
         HIPCHK(hipSetDevice(s.dev));
+        if (int e = stream_enter(s, s.stream)) return e;
         if (q) HIPCHK(hipMemcpyAsync(s.in_q, q + s.b0 * n, sizeof(double) * s.B * n, hipMemcpyHostToDevice, s.stream));
         if (l) HIPCHK(hipMemcpyAsync(s.in_l, l + s.b0 * m, sizeof(double) * s.B * m, hipMemcpyHostToDevice, s.stream));
         if (u) HIPCHK(hipMemcpyAsync(s.in_u, u + s.b0 * m, sizeof(double) * s.B * m, hipMemcpyHostToDevice, s.stream));
         HIPCHK(launch_update(s.kp, s.B, q ? s.in_q : nullptr, l ? s.in_l : nullptr, u ? s.in_u : nullptr, s.stream));
+        if (int e = stream_leave(s, s.stream)) return e;
     }
     if (int e = sync_all(h)) return e;
     if (l || u) return check_err_flags(h);
@@ -396,9 +424,11 @@ int mpcqp_warm_start_batch(mpcqp_handle* h, const double* x, const double* y) {
     const long n = h->n, m = h->m;
     for (auto& s : h->shards) {
         HIPCHK(hipSetDevice(s.dev));
+        if (int e = stream_enter(s, s.stream)) return e;
         if (x) HIPCHK(hipMemcpyAsync(s.out_x, x + s.b0 * n, sizeof(double) * s.B * n, hipMemcpyHostToDevice, s.stream));
         if (y) HIPCHK(hipMemcpyAsync(s.out_y, y + s.b0 * m, sizeof(double) * s.B * m, hipMemcpyHostToDevice, s.stream));
         HIPCHK(launch_warm(s.kp, s.B, x ? s.out_x : nullptr, y ? s.out_y : nullptr, s.stream));
+        if (int e = stream_leave(s, s.stream)) return e;
         s.kp.warm_start = 1;
     }
     h->set.warm_start = 1;
@@ -410,6 +440,7 @@ int mpcqp_solve_batch(mpcqp_handle* h, double* x, double* y, int32_t* status, in
     const long n = h->n, m = h->m;
     for (auto& s : h->shards) {
         HIPCHK(hipSetDevice(s.dev));
+        if (int e = stream_enter(s, s.stream)) return e;
         HIPCHK(hipEventRecord(s.ev0, s.stream));
         HIPCHK(launch_solve(s.kp, s.B, s.out_x, s.out_y, 0, s.stream));
         HIPCHK(hipEventRecord(s.ev1, s.stream));
@@ -418,6 +449,7 @@ int mpcqp_solve_batch(mpcqp_handle* h, double* x, double* y, int32_t* status, in
         if (y) HIPCHK(hipMemcpyAsync(y + s.b0 * m, s.out_y, sizeof(double) * s.B * m, hipMemcpyDeviceToHost, s.stream));
         if (status) HIPCHK(hipMemcpyAsync(status + s.b0, s.kp.status, sizeof(int) * s.B, hipMemcpyDeviceToHost, s.stream));
         if (iters) HIPCHK(hipMemcpyAsync(iters + s.b0, s.kp.iter, sizeof(int) * s.B, hipMemcpyDeviceToHost, s.stream));
+        if (int e = stream_leave(s, s.stream)) return e;
     }
     if (int e = sync_all(h)) return e;
     float ms = 0.f;
@@ -494,27 +526,33 @@ int mpcqp_setup_device(mpcqp_handle* h, const double* dPx, const double* dAx, co
     Shard& s = h->shards[0];
     hipStream_t st = pick(s, stream);
     HIPCHK(hipSetDevice(s.dev));
+    if (int e = stream_enter(s, st)) return e;
     if (int e = ev_begin(h, h->ev_setup, st)) return e;
     HIPCHK(launch_setup(s.kp, s.B, dPx, dAx, dq, dl, du, st));
-    return ev_end(h, h->ev_setup, st);
+    if (int e = ev_end(h, h->ev_setup, st)) return e;
+    return stream_leave(s, st);
 }
 
 int mpcqp_update_device(mpcqp_handle* h, const double* dq, const double* dl, const double* du, void* stream) {
     if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "device entry points need a single-device handle");
     Shard& s = h->shards[0];
+    hipStream_t st = pick(s, stream);
     HIPCHK(hipSetDevice(s.dev));
-    HIPCHK(launch_update(s.kp, s.B, dq, dl, du, pick(s, stream)));
-    return 0;
+    if (int e = stream_enter(s, st)) return e;
+    HIPCHK(launch_update(s.kp, s.B, dq, dl, du, st));
+    return stream_leave(s, st);
 }
 
 int mpcqp_warm_start_device(mpcqp_handle* h, const double* dx, const double* dy, void* stream) {
     if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "device entry points need a single-device handle");
     Shard& s = h->shards[0];
+    hipStream_t st = pick(s, stream);
     HIPCHK(hipSetDevice(s.dev));
-    HIPCHK(launch_warm(s.kp, s.B, dx, dy, pick(s, stream)));
+    if (int e = stream_enter(s, st)) return e;
+    HIPCHK(launch_warm(s.kp, s.B, dx, dy, st));
     s.kp.warm_start = 1;
     h->set.warm_start = 1;
-    return 0;
+    return stream_leave(s, st);
 }
 
 int mpcqp_solve_device(mpcqp_handle* h, double* dx, double* dy, int32_t* dstatus, int32_t* diters, void* stream) {
@@ -522,6 +560,7 @@ int mpcqp_solve_device(mpcqp_handle* h, double* dx, double* dy, int32_t* dstatus
     Shard& s = h->shards[0];
     hipStream_t st = pick(s, stream);
     HIPCHK(hipSetDevice(s.dev));
+    if (int e = stream_enter(s, st)) return e;
     HIPCHK(hipEventRecord(s.ev0, st));
     if (int e = ev_begin(h, h->ev_solve, st)) return e;
     KParams k = s.kp;  // the solve kernel writes status / iter into the caller's arrays as well
@@ -532,7 +571,7 @@ int mpcqp_solve_device(mpcqp_handle* h, double* dx, double* dy, int32_t* dstatus
     HIPCHK(hipEventRecord(s.ev1, st));
     HIPCHK(launch_order(s.kp, s.B, st));
     h->timed = true;
-    return 0;
+    return stream_leave(s, st);
 }
 
 int mpcqp_synchronize(mpcqp_handle* h) {
@@ -624,6 +663,7 @@ void mpcqp_free(mpcqp_handle* h) {
         if (s.dplan) (void)hipFree(s.dplan);
         if (s.ev0) (void)hipEventDestroy(s.ev0);
         if (s.ev1) (void)hipEventDestroy(s.ev1);
+        if (s.last_ev) (void)hipEventDestroy(s.last_ev);
         if (s.stream) (void)hipStreamDestroy(s.stream);
     }
     delete h;

@@ -53,6 +53,7 @@ struct KParams {
     // dispatch order of the solve kernels: workgroup slot -> instance, or null (identity).
     // Rewritten after every solve by launch_order (longest previous solve first).
     const int* order;
+    long slots;  // workgroups of the solve kernel resident at once on the device (CUs x occupancy)
 };
 
 size_t lds_setup_bytes(const KParams& p);
@@ -75,15 +76,27 @@ int solve_mode(int variant);
 int solve_threads(int variant);  // workgroup size of the variant's kernel
 bool variant_fits(const KParams& p, int variant);
 hipError_t launch_solve(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st);
+// What a solve launch runs: the variant's kernel, workgroup size and dynamic LDS.  The
+// launch_solve_* functions given a non-null ref only fill it in (no launch).
+struct KernelRef {
+    const void* fn;
+    int threads;
+    size_t lds;
+};
+// resident workgroups of the variant's kernel per CU (hipOccupancyMaxActiveBlocksPerMultiprocessor)
+int solve_blocks_per_cu(const KParams& p);
 // dense-inverse kernel (solve_dense.hip), variant 16, and its LDS bytes
-hipError_t launch_solve_dense(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st);
+hipError_t launch_solve_dense(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st,
+                        KernelRef* ref = nullptr);
 size_t lds_dense_bytes(const KParams& p);
 size_t lds_w2_bytes(const KParams& p);  // solve_wave.hip, variant 10
 // solution polishing (OSQP 0.6 polish.c) after the solve; launch_solve runs it when p.polish
 hipError_t launch_polish(const KParams& p, long B, double* xo, double* yo, hipStream_t st);
 // one-wave-per-QP kernel (solve_wave.hip), variants 8 and 9
-hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st);
+hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st,
+                        KernelRef* ref = nullptr);
 // 512-thread long-horizon kernel (solve_big.hip), variants 11-13
-hipError_t launch_solve_big(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st);
+hipError_t launch_solve_big(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st,
+                        KernelRef* ref = nullptr);
 
 }  // namespace mpcqp

@@ -307,7 +307,9 @@ __global__ __launch_bounds__(kOrderT) void k_order(const int* __restrict__ iter,
 }
 
 hipError_t launch_order(const KParams& p, long B, hipStream_t st) {
-    if (!p.order || B <= 256) return hipSuccess;  // up to 256 instances all start at once
+    // a batch that fits the resident workgroup slots (CUs x the variant's occupancy,
+    // api.hip::alloc_shard) starts all at once: the order cannot move anything
+    if (!p.order || B <= p.slots) return hipSuccess;
     int shift = 0;
     while ((p.max_iter >> shift) >= kOrderBins) ++shift;
     hipLaunchKernelGGL(k_order, dim3(1), dim3(kOrderT), 0, st, (const int*)p.iter, const_cast<int*>(p.order), B,

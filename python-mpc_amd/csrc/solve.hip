@@ -676,8 +676,10 @@ size_t lds_kernel_bytes(const KParams& p) {
 }
 
 template <int NB, int A, int K, int CS, int RS, int W, bool TRI = false>
-static hipError_t go(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st, size_t lds) {
+static hipError_t go(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st, size_t lds,
+                     KernelRef* ref) {
     auto k = k_solve<NB, A, K, CS, RS, W, TRI>;
+    if (ref) { *ref = {(const void*)k, T, lds}; return hipSuccess; }
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(T), lds, st, p, xo, yo, fo);
@@ -748,22 +750,31 @@ int solve_mode(int variant) {  // what factorize stores for the variant (KParams
 }
 
 static hipError_t launch_solve_only(const KParams& p, long B, double* xo, double* yo, int factor_only,
-                                    hipStream_t st) {
+                                    hipStream_t st, KernelRef* ref = nullptr) {
     const size_t lds = lds_solve_bytes(p);
     switch (p.variant) {
-        case 0: return go<4, 8, 6, 1, 1, 4, true>(p, B, xo, yo, factor_only, st, lds);
-        case 1: return go<8, 8, 8, 1, 1, 4>(p, B, xo, yo, factor_only, st, lds);
-        case 2: return go<8, 16, 8, 1, 1, 2>(p, B, xo, yo, factor_only, st, lds);
-        case 3: return go<8, 16, 8, 1, 2, 2>(p, B, xo, yo, factor_only, st, lds);
-        case 4: return go<0, 32, 8, 2, 4, 2>(p, B, xo, yo, factor_only, st, lds);
-        case 5: return go<0, 32, 8, 4, 4, 2>(p, B, xo, yo, factor_only, st, lds);
-        case 6: return go<0, 32, 16, 8, 8, 1>(p, B, xo, yo, factor_only, st, lds);
-        case 7: return go<4, 8, 6, 1, 1, 4, false>(p, B, xo, yo, factor_only, st, lds);
-        case 8: case 9: case 10: return launch_solve_wave(p, B, xo, yo, factor_only, st);
-        case 16: return launch_solve_dense(p, B, xo, yo, factor_only, st);
-        case 11: case 12: case 13: case 14: return launch_solve_big(p, B, xo, yo, factor_only, st);
+        case 0: return go<4, 8, 6, 1, 1, 4, true>(p, B, xo, yo, factor_only, st, lds, ref);
+        case 1: return go<8, 8, 8, 1, 1, 4>(p, B, xo, yo, factor_only, st, lds, ref);
+        case 2: return go<8, 16, 8, 1, 1, 2>(p, B, xo, yo, factor_only, st, lds, ref);
+        case 3: return go<8, 16, 8, 1, 2, 2>(p, B, xo, yo, factor_only, st, lds, ref);
+        case 4: return go<0, 32, 8, 2, 4, 2>(p, B, xo, yo, factor_only, st, lds, ref);
+        case 5: return go<0, 32, 8, 4, 4, 2>(p, B, xo, yo, factor_only, st, lds, ref);
+        case 6: return go<0, 32, 16, 8, 8, 1>(p, B, xo, yo, factor_only, st, lds, ref);
+        case 7: return go<4, 8, 6, 1, 1, 4, false>(p, B, xo, yo, factor_only, st, lds, ref);
+        case 8: case 9: case 10: return launch_solve_wave(p, B, xo, yo, factor_only, st, ref);
+        case 16: return launch_solve_dense(p, B, xo, yo, factor_only, st, ref);
+        case 11: case 12: case 13: case 14: return launch_solve_big(p, B, xo, yo, factor_only, st, ref);
         default: return hipErrorInvalidValue;
     }
+}
+
+int solve_blocks_per_cu(const KParams& p) {
+    KernelRef r{};
+    if (launch_solve_only(p, 0, nullptr, nullptr, 0, nullptr, &r) != hipSuccess || !r.fn) return -1;
+    if (hipFuncSetAttribute(r.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)r.lds) != hipSuccess) return -1;
+    int nblk = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nblk, r.fn, r.threads, r.lds) != hipSuccess) return -1;
+    return nblk;
 }
 
 hipError_t launch_solve(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st) {

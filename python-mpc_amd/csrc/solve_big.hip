@@ -791,21 +791,23 @@ size_t lds_solve_bytes_big(const KParams& p) {
 }
 
 template <int TTK, int NS, int K, int CS, int RS>
-static hipError_t go_b(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st) {
+static hipError_t go_b(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st, KernelRef* ref) {
     const size_t lds = lds_solve_bytes_big(p);
     auto k = k_solve_b<TTK, NS, K, CS, RS>;
+    if (ref) { *ref = {(const void*)k, TTK, lds}; return hipSuccess; }
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(TTK), lds, st, p, xo, yo, fo);
     return hipGetLastError();
 }
 
-hipError_t launch_solve_big(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st) {
+hipError_t launch_solve_big(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st,
+                            KernelRef* ref) {
     switch (p.variant) {
-        case 11: return go_b<512, 6, 8, 1, 2>(p, B, xo, yo, factor_only, st);   // nb <= 12
-        case 12: return go_b<512, 9, 8, 2, 2>(p, B, xo, yo, factor_only, st);   // nb <= 18
-        case 13: return go_b<512, 12, 8, 2, 3>(p, B, xo, yo, factor_only, st);  // nb <= 24
-        case 14: return go_b<128, 4, 8, 2, 2>(p, B, xo, yo, factor_only, st);   // nb <= 8, two waves
+        case 11: return go_b<512, 6, 8, 1, 2>(p, B, xo, yo, factor_only, st, ref);   // nb <= 12
+        case 12: return go_b<512, 9, 8, 2, 2>(p, B, xo, yo, factor_only, st, ref);   // nb <= 18
+        case 13: return go_b<512, 12, 8, 2, 3>(p, B, xo, yo, factor_only, st, ref);  // nb <= 24
+        case 14: return go_b<128, 4, 8, 2, 2>(p, B, xo, yo, factor_only, st, ref);   // nb <= 8, two waves
         default: return hipErrorInvalidValue;
     }
 }

@@ -579,18 +579,20 @@ size_t lds_dense_bytes(const KParams& p) {
 }
 
 template <int R, int K, int RS, int KPK>
-static hipError_t go_d(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st) {
+static hipError_t go_d(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st, KernelRef* ref) {
     auto k = k_solve_d<R, K, RS, KPK>;
     const size_t lds = lds_dense_bytes(p);
+    if (ref) { *ref = {(const void*)k, TD, lds}; return hipSuccess; }
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(TD), lds, st, p, xo, yo, fo);
     return hipGetLastError();
 }
 
-hipError_t launch_solve_dense(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st) {
+hipError_t launch_solve_dense(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st,
+                              KernelRef* ref) {
     switch (p.variant) {
-        case 16: return go_d<kDenseR, 6, 1, 4>(p, B, xo, yo, factor_only, st);
+        case 16: return go_d<kDenseR, 6, 1, 4>(p, B, xo, yo, factor_only, st, ref);
         default: return hipErrorInvalidValue;
     }
 }

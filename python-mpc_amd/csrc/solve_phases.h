@@ -413,11 +413,14 @@ struct Shared {
 
 // status "non convex" of an early exit (invalid data, first factorisation failed), with
 // the per-call copies mpcqp_solve_device asks for
+// (no ADMM iteration ran: the iteration count is 0, not the previous solve's, which
+// k_order would otherwise take for a long solve)
 template <class KP>
 __device__ __forceinline__ void fail_status(const KP& p, long b) {
     p.status[b] = MPCQP_NON_CVX_;
+    p.iter[b] = 0;
     if (p.ostat) p.ostat[b] = MPCQP_NON_CVX_;
-    if (p.oiter) p.oiter[b] = p.iter[b];
+    if (p.oiter) p.oiter[b] = 0;
 }
 
 // ---- out-of-line phases: everything they need is in LDS or in the plan ----

@@ -927,8 +927,10 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
 }
 
 template <int K, int RS, int KPK>
-static hipError_t go_w2(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st, size_t lds) {
+static hipError_t go_w2(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st, size_t lds,
+                        KernelRef* ref) {
     auto k = k_solve_w2<K, RS, KPK>;
+    if (ref) { *ref = {(const void*)k, T2, lds}; return hipSuccess; }
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(T2), lds, st, p, xo, yo, fo);
@@ -936,8 +938,10 @@ static hipError_t go_w2(const KParams& p, long B, double* xo, double* yo, int fo
 }
 
 template <int K, int RS>
-static hipError_t go_w(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st, size_t lds) {
+static hipError_t go_w(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st, size_t lds,
+                       KernelRef* ref) {
     auto k = k_solve_w<K, RS>;
+    if (ref) { *ref = {(const void*)k, TW, lds}; return hipSuccess; }
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(TW), lds, st, p, xo, yo, fo);
@@ -950,12 +954,13 @@ size_t lds_w2_bytes(const KParams& p) {
 }
 
 // Wave-kernel instantiations (solve.hip::variant_fits gives their preconditions).
-hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st) {
+hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st,
+                             KernelRef* ref) {
     const size_t lds = lds_solve_bytes(p);
     switch (p.variant) {
-        case 8: return go_w<6, 3>(p, B, xo, yo, factor_only, st, lds);
-        case 9: return go_w<8, 4>(p, B, xo, yo, factor_only, st, lds);
-        case 10: return go_w2<6, 2, 4>(p, B, xo, yo, factor_only, st, lds_w2_bytes(p));
+        case 8: return go_w<6, 3>(p, B, xo, yo, factor_only, st, lds, ref);
+        case 9: return go_w<8, 4>(p, B, xo, yo, factor_only, st, lds, ref);
+        case 10: return go_w2<6, 2, 4>(p, B, xo, yo, factor_only, st, lds_w2_bytes(p), ref);
         default: return hipErrorInvalidValue;
     }
 }

@@ -327,3 +327,74 @@ def test_longest_first_dispatch_is_result_neutral(monkeypatch, cfg, B):
     for a, b in zip(o1, o0):
         assert torch.equal(a, b)
     assert o1[3].max().item() > o1[3].min().item()  # the counts vary, so the order is not the identity
+
+
+def test_invalid_update_reports_zero_iterations():
+    """An instance whose update() makes its bounds invalid (l > u) exits before any
+    ADMM iteration: status 'non convex' with NaN outputs (osqp refuses such data) and
+    an iteration count of 0 -- not the previous solve's count, which the next solve's
+    dispatch order (kernels.hip::k_order) would otherwise rank as a long solve."""
+    import torch
+    from osqp_amd import DeviceBatch
+    B = 8
+    b = mpc.make_batch(2, B=B, seed=5)
+    s = {k: v for k, v in b["settings"].items() if k != "verbose"}
+    dev = torch.device("cuda", 0)
+    X = [torch.from_numpy(np.ascontiguousarray(b[k])).to(dev) for k in ("Px", "Ax", "q", "l", "u")]
+    x = torch.empty((B, b["n"]), dtype=torch.float64, device=dev)
+    y = torch.empty((B, b["m"]), dtype=torch.float64, device=dev)
+    st = torch.empty(B, dtype=torch.int32, device=dev)
+    it = torch.empty(B, dtype=torch.int32, device=dev)
+    h = DeviceBatch(b["P"], b["A"], B, device=0, **s)
+    h.setup(*X)
+    h.solve(x, y, st, it)
+    h.synchronize()
+    assert (it.cpu().numpy() > 0).all()
+    bad = X[3].clone()
+    bad[3, 10] = X[4][3, 10] + 1.0  # lower bound above the upper one, instance 3 only
+    h.update(l=bad)
+    h.solve(x, y, st, it)
+    h.synchronize()
+    stv, itv = st.cpu().numpy(), it.cpu().numpy()
+    assert stv[3] == -7 and itv[3] == 0
+    assert torch.isnan(x[3]).all()
+    assert (stv[np.arange(B) != 3] == 1).all() and (itv[np.arange(B) != 3] > 0).all()
+
+
+def test_calls_on_different_streams_are_ordered():
+    """Consecutive calls on one handle enqueued on different streams, with no
+    synchronisation in between: the library orders each call after the previous one
+    (api.hip::stream_enter), so the results equal a single-stream run."""
+    import torch
+    from osqp_amd import DeviceBatch
+    B = 1024
+    bx, by = mpc.make_batch(2, B=B, seed=31), mpc.make_batch(2, B=B, seed=32)
+    s = {k: v for k, v in bx["settings"].items() if k != "verbose"}
+    s.update(warm_start=False)
+    dev = torch.device("cuda", 0)
+    n, m = bx["n"], bx["m"]
+
+    def put(b):
+        return [torch.from_numpy(np.ascontiguousarray(b[k])).to(dev) for k in ("Px", "Ax", "q", "l", "u")]
+
+    def out():
+        return (torch.empty((B, n), dtype=torch.float64, device=dev), torch.empty((B, m), dtype=torch.float64, device=dev),
+                torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev))
+
+    X, Y = put(bx), put(by)
+    torch.cuda.synchronize()
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    h = DeviceBatch(bx["P"], bx["A"], B, device=0, **s)
+    o1, o2 = out(), out()
+    h.setup(*X, stream=sa.cuda_stream)
+    h.solve(*o1, stream=sa.cuda_stream)   # k_order rewrites the dispatch order on sa ...
+    h.setup(*Y, stream=sb.cuda_stream)    # ... which this setup and solve on sb must wait for
+    h.solve(*o2, stream=sb.cuda_stream)
+    torch.cuda.synchronize()
+    ref = DeviceBatch(bx["P"], bx["A"], B, device=0, **s)
+    r1, r2 = out(), out()
+    ref.setup(*X); ref.solve(*r1)
+    ref.setup(*Y); ref.solve(*r2)
+    ref.synchronize()
+    for a, c in zip(o1 + o2, r1 + r2):
+        assert torch.equal(a, c)
