@@ -191,6 +191,95 @@ __device__ __forceinline__ void block_sum(double (&v)[K], double* red) {
     }
 }
 
+// ---- transposed multi-value reductions (the termination check's 17 maxima) ----
+// max of two non-negative doubles: v_max_f64 (one instruction; a NaN operand is
+// skipped, as OSQP's sequential vec_norm_inf skips it)
+__device__ __forceinline__ double vmax(double a, double b) { return __builtin_fmax(a, b); }
+
+// One transposed step over the lane pairs of DPP CTRL: lanes with `upper` keep the
+// upper half of the K values, the others the lower half, each max'ed with the
+// partner's copy (the odd value out pairs with 0, neutral for the non-negative
+// maxima).  K values in, (K+1)/2 out; 2 DPP moves + 5 VALU per value kept.
+template <int CTRL, int K>
+__device__ __forceinline__ void tmax_step(const double (&in)[K], double (&out)[(K + 1) / 2], bool upper) {
+    constexpr int H = (K + 1) / 2;
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        const double lo = in[j];
+        const double hi = j + H < K ? in[j + H] : 0.0;
+        out[j] = vmax(upper ? hi : lo, dpp<CTRL>(upper ? lo : hi));
+    }
+}
+
+// max with the lane 16 (xor-like: odd/even DPP rows) or 32 (half-waves) away:
+// v_permlane16/32_swap of both dwords, every lane keeps the larger value
+template <bool HALF>
+__device__ __forceinline__ double xmax_swap(double v) {
+    const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+    const auto l = HALF ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
+                        : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto h = HALF ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
+                        : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    return vmax(__hiloint2double((int)h[0], (int)l[0]), __hiloint2double((int)h[1], (int)l[1]));
+}
+
+// Workgroup max of K non-negative values per thread plus workgroup sums of KS values,
+// results in every thread.  The maxima are reduced transposed: two DPP steps split the
+// K values over the lanes of a quad (lane bits 0, 1), the rest of the wave reduces the
+// remaining (K+3)/4 values per lane over the lanes of equal quad position (row_ror 4 / 8,
+// permlane16 / 32 swaps), and one LDS round combines the waves -- about a sixth of the
+// instructions of K separate DPP trees.  The sums keep block_sum's order (wave_sum, then
+// wave 0 + wave 1 + ...), so they are bit-identical to it.  red: 4 * NW * K2 + NW * KS
+// doubles, 16-byte aligned.
+template <int TT, int K, int KS>
+__device__ __forceinline__ void block_max_sum_tr(double (&v)[K], double (&sm)[KS], double* red) {
+    constexpr int NW = TT / 64, K1 = (K + 1) / 2, K2 = (K1 + 1) / 2;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    double t1[K1], t2[K2];
+    tmax_step<0xB1, K>(v, t1, lane & 1);          // quad_perm [1,0,3,2]: lane ^ 1
+    tmax_step<0x4E, K1>(t1, t2, (lane >> 1) & 1);  // quad_perm [2,3,0,1]: lane ^ 2
+#pragma unroll
+    for (int j = 0; j < K2; ++j) {
+        double x = t2[j];
+        x = vmax(x, dpp<0x124>(x));  // row_ror:4
+        x = vmax(x, dpp<0x128>(x));  // row_ror:8
+        x = xmax_swap<false>(x);
+        x = xmax_swap<true>(x);
+        t2[j] = x;
+    }
+    double s[KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) s[k] = wave_sum(sm[k]);
+    // lane q < 4 (quad position q = b0 + 2 b1) holds value j + K2 b1 + K1 b0
+    double* rs = red + 4 * NW * K2;
+    if (lane < 4) {
+#pragma unroll
+        for (int j = 0; j < K2; ++j) red[(lane * K2 + j) * NW + wid] = t2[j];
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < KS; ++k) rs[wid * KS + k] = s[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int b0 = k >= K1, r1 = k - K1 * b0, b1 = r1 >= K2, j = r1 - K2 * b1;
+        const double* src = red + ((b0 + 2 * b1) * K2 + j) * NW;
+        double r = src[0];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) r = vmax(r, src[w]);
+        v[k] = r;
+    }
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+        double r = rs[k];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) r += rs[w * KS + k];
+        sm[k] = r;
+    }
+    __syncthreads();
+}
+
 template <int TT>
 __device__ __forceinline__ bool block_any(bool f, int* flag) {
     if constexpr (TT == 64) {

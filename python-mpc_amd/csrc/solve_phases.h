@@ -80,6 +80,11 @@ __device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restri
     // masked FMA pass; the true values are published per pivot (one multiply) and
     // restored once at the end.  iv = 1 / sc, exactly piv for pivoted rows.
     double sc = 1.0, iv = 1.0;
+    // Branch-free pivot step (the rolled loop): after the publish, the pivot, the lane's
+    // column entry and the lane's half of row p are read together, so the row's LDS
+    // latency overlaps the reciprocal's Newton chain; the pivot row's own lane runs the
+    // FMA pass with a zero multiplier (v + (-0) * row == v exactly for finite rows).
+    // cfg 3 (256-thread kernel) Gauss-Jordan 868 k -> 787 k cycles per slowest solve.
     auto pivot = [&](const int p, const int pj) __attribute__((always_inline)) {
         const int ph = p >> 4;
         double* rb = buf + (pj & 1) * S;
@@ -90,6 +95,8 @@ __device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restri
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const double piv = rb[p];
+        const double mi = rb[i];
         double rowv[16];
 #pragma unroll
         for (int jj = 0; jj < 16; jj += 2) {
@@ -97,8 +104,6 @@ __device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restri
             rowv[jj] = r2.x;
             rowv[jj + 1] = r2.y;
         }
-        const double piv = rb[p];
-        const double mi = rb[i];
         const double colv = i < p ? -mi : mi;  // M_ip
         minpiv = piv > 0.0 ? minpiv : -1.0;
         // 1 / piv: hardware reciprocal and two Newton steps (full double precision)
@@ -107,25 +112,60 @@ __device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restri
         d = __builtin_fma(d, __builtin_fma(-piv, d, 1.0), d);
         // every other row loses M_ip / piv times row_p (in its own scale); row p keeps
         // its elements and takes the scale 1 / piv
-        const double cd = (colv * d) * iv;
-        if (i != p) {
+        const bool self = i == p;
+        const double cd = self ? 0.0 : (colv * d) * iv;
 #pragma unroll
-            for (int jj = 0; jj < 16; ++jj) v[jj] = __builtin_fma(-cd, rowv[jj], v[jj]);
-        } else {
-            sc = d;
-            iv = piv;
-        }
+        for (int jj = 0; jj < 16; ++jj) v[jj] = __builtin_fma(-cd, rowv[jj], v[jj]);
+        sc = self ? d : sc;
+        iv = self ? piv : iv;
         if (h == ph) {
-            if (Compact) put16(v, pj, i == p ? 1.0 : -cd);
-            else v[pj] = i == p ? 1.0 : -cd;
+            if (Compact) put16(v, pj, self ? 1.0 : -cd);
+            else v[pj] = self ? 1.0 : -cd;
         }
     };
     if constexpr (Compact) {
 #pragma unroll 1
         for (int p = 0; p < S; ++p) pivot(p, __builtin_amdgcn_readfirstlane(p & 15));
     } else {
+        // the unrolled loop keeps the divergent update: measured faster here than the
+        // branch-free step (cfg 2 Gauss-Jordan 233 k vs 275 k cycles per solve of the
+        // slowest instance), and as fast as a one-pivot lookahead variant (238 k)
+        auto pivot_br = [&](const int p, const int pj) __attribute__((always_inline)) {
+            const int ph = p >> 4;
+            double* rb = buf + (pj & 1) * S;
+            if (h == ph) {
+                const double vp = sc * v[pj];
+                rb[i] = i < p ? -vp : vp;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            double rowv[16];
 #pragma unroll
-        for (int p = 0; p < S; ++p) pivot(p, p & 15);
+            for (int jj = 0; jj < 16; jj += 2) {
+                const double2 r2 = *(const double2*)(rb + 16 * h + jj);
+                rowv[jj] = r2.x;
+                rowv[jj + 1] = r2.y;
+            }
+            const double piv = rb[p];
+            const double mi = rb[i];
+            const double colv = i < p ? -mi : mi;
+            minpiv = piv > 0.0 ? minpiv : -1.0;
+            double d = __builtin_amdgcn_rcp(piv);
+            d = __builtin_fma(d, __builtin_fma(-piv, d, 1.0), d);
+            d = __builtin_fma(d, __builtin_fma(-piv, d, 1.0), d);
+            const double cd = (colv * d) * iv;
+            if (i != p) {
+#pragma unroll
+                for (int jj = 0; jj < 16; ++jj) v[jj] = __builtin_fma(-cd, rowv[jj], v[jj]);
+            } else {
+                sc = d;
+                iv = piv;
+            }
+            if (h == ph) v[pj] = i == p ? 1.0 : -cd;
+        };
+#pragma unroll
+        for (int p = 0; p < S; ++p) pivot_br(p, p & 15);
     }
 #pragma unroll
     for (int jj = 0; jj < 16; jj += 2) {
@@ -246,9 +286,15 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
 #pragma unroll 1
                     for (int o = tid; o < amax * S; o += TT) {
                         const int r = o >> 5, c = o & (S - 1);
+                        // mode 2 has amax <= 8 (variant_fits): the 8 loads of G_{k-1,j} (global,
+                        // just written) go out together; rows >= amax stay inside the tile array
+                        double gv[8];
+#pragma unroll
+                        for (int l = 0; l < 8; ++l) gv[l] = Gp[l * S + c];
                         double sacc = 0.0;
-#pragma unroll 1
-                        for (int l = 0; l < amax; ++l) sacc += SP[r * S + l] * Gp[l * S + c];
+#pragma unroll
+                        for (int l = 0; l < 8; ++l)
+                            if (l < amax) sacc += SP[r * S + l] * gv[l];
                         Gk[o] = -sacc;
                     }
                 }

@@ -752,13 +752,13 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
                 if (up > OSQP_INFTY * MIN_SCALING) d = (lo < -OSQP_INFTY * MIN_SCALING) ? 0.0 : cmin(d, 0.0);
                 else if (lo < -OSQP_INFTY * MIN_SCALING) d = cmax(d, 0.0);
                 if (ok) {
-                    mx[0] = cmax(mx[0], fabs(ei * pr));
-                    mx[2] = cmax(mx[2], fabs(ei * zi));
-                    mx[3] = cmax(mx[3], fabs(ei * ax));
-                    mx[7] = cmax(mx[7], fabs(pr));
-                    mx[9] = cmax(mx[9], fabs(zi));
-                    mx[10] = cmax(mx[10], fabs(ax));
-                    mx[14] = cmax(mx[14], fabs(unscale ? Ev[s] * d : d));
+                    mx[0] = vmax(mx[0], fabs(ei * pr));
+                    mx[2] = vmax(mx[2], fabs(ei * zi));
+                    mx[3] = vmax(mx[3], fabs(ei * ax));
+                    mx[7] = vmax(mx[7], fabs(pr));
+                    mx[9] = vmax(mx[9], fabs(zi));
+                    mx[10] = vmax(mx[10], fabs(ax));
+                    mx[14] = vmax(mx[14], fabs(unscale ? Ev[s] * d : d));
                     sm[0] += up * cmax(d, 0.0) + lo * cmin(d, 0.0);
                     C.dY[ri[s]] = d;  // projected in place, as OSQP's is_primal_infeasible
                 }
@@ -793,8 +793,7 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
             }
             // q' dx with the out-of-line phases' column-per-thread order (column tid)
             if (p.pad_var[tid] >= 0) sm[1] = L.qv[tid] * L.dx[tid];
-            block_max<T2, 17>(mx, L.red);
-            block_sum<T2, 2>(sm, L.red);
+            block_max_sum_tr<T2, 17, 2>(mx, sm, L.red);
             PHC(13)
             Res R;
             if (unscale) {
