@@ -61,6 +61,10 @@ def parse():
     ap.add_argument("--batch", type=int, default=None, help="instances per GPU (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--separate-setup", action="store_true",
+                    help="setup() and solve() as two kernels (default: mpcqp_setup_solve_device, fused where possible)")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="diagnostic: no HIP events in the timed region (roofline kernel_ms from the untimed pass)")
     ap.add_argument("--no-dispatch-ab", action="store_true",
                     help="skip the identity-dispatch diagnostic (rocprof passes: one handle's launches only)")
     return ap.parse_args()
@@ -109,7 +113,15 @@ def bound_sequence(b, count, seed, to_dev):
     return seq
 
 
-def pmc_traffic(workload, batch):
+def solve_kernel_name(info, fused):
+    """The kernel the roofline times: the fused setup+solve kernel where the two-wave
+    variant runs it (solve_wave.hip::k_setup_solve_w2), else the solve kernel."""
+    if info["threads_per_qp"] == 128 and fused:
+        return "mpcqp::k_setup_solve_w2"
+    return {64: "mpcqp::k_solve_w", 128: "mpcqp::k_solve_w2"}.get(info["threads_per_qp"], "mpcqp::k_solve")
+
+
+def pmc_traffic(workload, batch, kernel):
     """HBM bytes per k_solve launch from rocprofv3 PMC passes committed under
     profiles/ (tools/pmc_traffic.py writes profiles/traffic_<workload>_b<B>.json:
     FETCH_SIZE and WRITE_SIZE from separate --pmc passes, FETCH_SIZE doubled per
@@ -118,7 +130,8 @@ def pmc_traffic(workload, batch):
     if not os.path.exists(path):
         return {}
     with open(path) as f:
-        return json.load(f)
+        t = json.load(f)
+    return t if t.get("kernel") == kernel else {}  # measured on another kernel: not this one's traffic
 
 
 def main():
@@ -168,12 +181,17 @@ def main():
         xs, ys = warm_shift(b["N"], 8, 2, dx, dy)
         torch.cuda.synchronize()
 
-    def step(t, sv=solver):
+    def step(t, sv=solver, fused=not args.separate_setup):
         sl, su = seq[t]
-        sv.setup(dPx, dAx, dq, sl, su)
-        if warm:
+        if warm:  # setup, then the warm start, then the solve
+            sv.setup(dPx, dAx, dq, sl, su)
             sv.warm_start(xs, ys)
-        sv.solve(dx, dy, dst, dit)
+            sv.solve(dx, dy, dst, dit)
+        elif fused:  # mpcqp_setup_solve_device: one kernel where the solve kernel allows it
+            sv.setup_solve(dPx, dAx, dq, sl, su, dx, dy, dst, dit)
+        else:
+            sv.setup(dPx, dAx, dq, sl, su)
+            sv.solve(dx, dy, dst, dit)
 
     step(0)  # the base batch: its statuses / iterations are the ones the CPU baseline is compared with
     solver.synchronize()
@@ -190,7 +208,9 @@ def main():
     barrier()
     torch.cuda.synchronize()
     solver.synchronize()
-    solver.timing(True)
+    fused = not (warm or args.separate_setup)
+    if not args.no_kernel_timing:  # one event pair per launch, on the solver's stream
+        solver.timing(True, setup=not fused)
     t0 = time.perf_counter()
     for t in range(1 + args.warmup, 1 + args.warmup + args.steps):
         step(t)
@@ -198,9 +218,16 @@ def main():
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
-    kt = solver.timing_read()
+    kt = solver.timing_read() if not args.no_kernel_timing else None
     iters_last = dit.cpu().numpy()  # the last timed step's batch (the flop model's iteration count)
     solver.timing(False)
+    if args.no_kernel_timing:  # diagnostic: kernel times from a few untimed steps
+        solver.timing(True, setup=not fused)
+        for t in range(1 + args.warmup, 1 + args.warmup + min(5, args.steps)):
+            step(t)
+        solver.synchronize()
+        kt = solver.timing_read()
+        solver.timing(False)
     dt = max_over_ranks(t1 - t0, world)
 
     # Diagnostic A/B, outside the timed region and never `value`: the same sequence of
@@ -225,7 +252,7 @@ def main():
     nnzP, nnzA = P.nnz, A.nnz
     bytes_per_solve = 8 * (nnzP + nnzA + n + 2 * m) + 8 * (n + m) + (8 * (n + m) if warm else 0)
     solve_ms = kt["solve_ms"] / max(1, kt["n_solve"])
-    setup_ms = kt["setup_ms"] / max(1, kt["n_setup"])
+    setup_ms = kt["setup_ms"] / kt["n_setup"] if kt["n_setup"] else None  # None: setup runs inside the fused kernel
     achieved = bytes_per_solve * B / (solve_ms * 1e-3) / 1e9
     info = solver.plan_info()
     # fp64 flop model per ADMM iteration (diagnostic): BT solve 3*nb*S^2 FMAs, A/A' products,
@@ -234,7 +261,7 @@ def main():
     flop_iter = 2 * (3 * info["nb"] * S * S + 2 * nnzA) + 12 * (n + m)
     fp64_tflops = flop_iter * float(iters_last.astype(np.float64).sum()) / (solve_ms * 1e-3) / 1e12
 
-    traffic = pmc_traffic(spec["name"], B)
+    traffic = pmc_traffic(spec["name"], B, solve_kernel_name(info, fused=fused))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -281,7 +308,10 @@ def main():
                        "global_batch": world * B, "horizon_N": b["N"], "n": n, "m": m,
                        "nnz_triuP": nnzP, "nnz_A": nnzA, "eps_abs": 1e-3, "eps_rel": 1e-3,
                        "step": ("setup()+warm_start(base solution shifted one stage)+solve()" if warm else
-                                "setup()+solve()") + " per instance, inputs resident in HBM; a distinct batch per "
+                                "setup()+solve()" + ("" if args.separate_setup else
+                                                     " (mpcqp_setup_solve_device: one call; one kernel for "
+                                                     "the two-wave variant)"))
+                               + " per instance, inputs resident in HBM; a distinct batch per "
                                 f"step (initial states jittered +-{JITTER:.0%} of the D2 ranges)",
                        "parallelism": f"batch-shard x{world}",
                        "dispatch": "longest previous solve first (kernels.hip::k_order), predicted from the "
@@ -294,7 +324,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic.get("bytes_per_launch"),
                          "traffic_source": traffic.get("source"),
-                         "kernel": {64: "mpcqp::k_solve_w", 128: "mpcqp::k_solve_w2"}.get(info["threads_per_qp"], "mpcqp::k_solve"),
+                         "kernel": solve_kernel_name(info, fused=fused),
                          "kernel_ms": solve_ms, "setup_kernel_ms": setup_ms,
                          "bytes_per_solve": bytes_per_solve, "launch_instances": B,
                          "fp64_tflops_model": fp64_tflops, "fp64_peak_tflops": FP64_PEAK_TFLOPS},

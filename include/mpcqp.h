@@ -142,15 +142,26 @@ int mpcqp_update_device(mpcqp_handle *h, const double *dq, const double *dl, con
 int mpcqp_warm_start_device(mpcqp_handle *h, const double *dx, const double *dy, void *stream);
 int mpcqp_solve_device(mpcqp_handle *h, double *dx, double *dy, int32_t *dstatus, int32_t *diters,
                        void *stream);
+/* setup + solve of the same inputs in one call: mpcqp_setup_device(dPx..du) followed by
+ * mpcqp_solve_device(dx, dy, dstatus, diters), with identical results.  Where the
+ * solve kernel allows it (the two-wave kernel of the N=20 lateral layouts) both run as
+ * ONE kernel: each workgroup scales its instance and solves it, so no setup kernel and
+ * no launch gap stand in front of the slowest instance.  The reference's per-call
+ * pattern prob.setup(...); prob.solve() (Control/MPC/mpc_kinematics.py:194-198,
+ * mpc_dynamics.py:392-396) maps onto it one-to-one. */
+int mpcqp_setup_solve_device(mpcqp_handle *h, const double *dPx, const double *dAx, const double *dq,
+                             const double *dl, const double *du, double *dx, double *dy, int32_t *dstatus,
+                             int32_t *diters, void *stream);
 int mpcqp_synchronize(mpcqp_handle *h);
 /* hipEvent-bracketed timing of the ADMM kernel launches of the last *_device
  * solve on the handle's stream: milliseconds, or -1 when unavailable. */
 double mpcqp_last_kernel_ms(mpcqp_handle *h);
 
-/* Kernel timing for bench.py's roofline: while enabled, every *_device setup /
- * solve launch is bracketed by a hipEvent pair on its stream (no host sync).
- * mpcqp_timing_read() waits for the recorded events, returns the summed
- * kernel milliseconds and launch counts, and clears the record. */
+/* Kernel timing for bench.py's roofline: while enabled, every *_device solve
+ * (enable bit 0) / setup (bit 1) launch is bracketed by a hipEvent pair on its
+ * stream (no host sync).  mpcqp_timing_read() waits for the recorded events,
+ * returns the summed kernel milliseconds and launch counts, and clears the
+ * record. */
 int mpcqp_timing(mpcqp_handle *h, int32_t enable);
 int mpcqp_timing_read(mpcqp_handle *h, double *setup_ms, int32_t *n_setup, double *solve_ms,
                       int32_t *n_solve);

@@ -66,8 +66,8 @@ struct Shard {
     long b0 = 0, B = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    // stream ordering of the calls on the handle: the last call's work is recorded in
-    // last_ev on last_st, and a call on another stream waits for it first (enter/leave)
+    // stream ordering of the calls on the handle: last_st is the stream of the last
+    // call; a call on another stream records last_ev there and waits for it (enter)
     hipEvent_t last_ev = nullptr;
     hipStream_t last_st = nullptr;
     int* dplan = nullptr;
@@ -88,8 +88,10 @@ struct mpcqp_handle {
     std::vector<Shard> shards;
     bool timed = false;
     double last_ms = -1.0;
-    bool collect = false;   // record hipEvent pairs around device launches
+    bool collect = false;        // record hipEvent pairs around device solve launches
+    bool collect_setup = false;  // ... and around device setup launches
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_setup, ev_solve;
+    std::pair<hipEvent_t, hipEvent_t> last_pair{nullptr, nullptr};  // events of the last device solve
 };
 
 namespace {
@@ -139,6 +141,7 @@ size_t workspace_bytes(const Plan& pl, long B, bool with_io) {
     for (int i = 0; i < 4; ++i) carve<double>(off, B);
     carve<signed char>(off, B * m);
     for (int i = 0; i < 6; ++i) carve<int>(off, B);
+    carve<int>(off, 1);  // done (fused order epilogue)
     carve<long long>(off, B * kProfSlots);
     carve<KParams>(off, 1);
     if (with_io) {
@@ -201,6 +204,7 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
         k.order = ord;
         if (const char* ev = getenv("MPCQP_DISPATCH"); ev && !strcmp(ev, "identity")) k.order = nullptr;  // A/B
     }
+    int* const done = (int*)(base + carve<int>(off, 1));  // zero from the memset above
     k.prof = nullptr;
     if (const char* ev = getenv("MPCQP_PHASE_PROF"); ev && ev[0] == '1')
         k.prof = (long long*)(base + carve<long long>(off, B * kProfSlots));
@@ -235,6 +239,10 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
         k.variant = v;
     }
     k.mode = solve_mode(k.variant);
+    // k_solve_w2 sorts the next dispatch order in its last workgroup (MPCQP_ORDER_KERNEL=1: k_order)
+    k.done = nullptr;
+    if (k.variant == 10 && k.order && !(getenv("MPCQP_ORDER_KERNEL") && getenv("MPCQP_ORDER_KERNEL")[0] == '1'))
+        k.done = done;
     {  // resident solve workgroups: below this batch size the dispatch order is moot
         int ncu = 0;
         HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, s.dev));
@@ -320,12 +328,21 @@ int sync_all(mpcqp_handle* h) {
 // to another stream is waited for first.  The handle's workspace -- including the
 // dispatch order each solve rewrites for the next (kernels.hip::k_order) -- is then
 // never read by one stream while another writes it, whatever streams the caller uses.
+// The event is recorded only on a change of stream (at that moment it covers everything
+// enqueued on the old stream), so a single-stream caller adds no packets between its
+// kernels.  A record that fails (the old stream was destroyed) falls back to a device
+// synchronisation.
 int stream_enter(Shard& s, hipStream_t st) {
-    if (s.last_st && s.last_st != st) HIPCHK(hipStreamWaitEvent(st, s.last_ev, 0));
+    if (!s.last_st || s.last_st == st) return 0;
+    if (hipEventRecord(s.last_ev, s.last_st) == hipSuccess) {
+        HIPCHK(hipStreamWaitEvent(st, s.last_ev, 0));
+    } else {
+        (void)hipGetLastError();
+        HIPCHK(hipDeviceSynchronize());
+    }
     return 0;
 }
 int stream_leave(Shard& s, hipStream_t st) {
-    HIPCHK(hipEventRecord(s.last_ev, st));
     s.last_st = st;
     return 0;
 }
@@ -527,9 +544,11 @@ int mpcqp_setup_device(mpcqp_handle* h, const double* dPx, const double* dAx, co
     hipStream_t st = pick(s, stream);
     HIPCHK(hipSetDevice(s.dev));
     if (int e = stream_enter(s, st)) return e;
-    if (int e = ev_begin(h, h->ev_setup, st)) return e;
+    if (h->collect_setup)
+        if (int e = ev_begin(h, h->ev_setup, st)) return e;
     HIPCHK(launch_setup(s.kp, s.B, dPx, dAx, dq, dl, du, st));
-    if (int e = ev_end(h, h->ev_setup, st)) return e;
+    if (h->collect_setup)
+        if (int e = ev_end(h, h->ev_setup, st)) return e;
     return stream_leave(s, st);
 }
 
@@ -561,15 +580,54 @@ int mpcqp_solve_device(mpcqp_handle* h, double* dx, double* dy, int32_t* dstatus
     hipStream_t st = pick(s, stream);
     HIPCHK(hipSetDevice(s.dev));
     if (int e = stream_enter(s, st)) return e;
-    HIPCHK(hipEventRecord(s.ev0, st));
-    if (int e = ev_begin(h, h->ev_solve, st)) return e;
+    // one event pair around the launch: the timing record's while timing is on, else
+    // the handle's own (mpcqp_last_kernel_ms)
+    if (h->collect) {
+        if (int e = ev_begin(h, h->ev_solve, st)) return e;
+    } else {
+        HIPCHK(hipEventRecord(s.ev0, st));
+    }
     KParams k = s.kp;  // the solve kernel writes status / iter into the caller's arrays as well
     k.ostat = dstatus;
     k.oiter = diters;
     HIPCHK(launch_solve(k, s.B, dx, dy, 0, st));
-    if (int e = ev_end(h, h->ev_solve, st)) return e;
-    HIPCHK(hipEventRecord(s.ev1, st));
-    HIPCHK(launch_order(s.kp, s.B, st));
+    if (h->collect) {
+        if (int e = ev_end(h, h->ev_solve, st)) return e;
+        h->last_pair = h->ev_solve.back();
+    } else {
+        HIPCHK(hipEventRecord(s.ev1, st));
+        h->last_pair = {s.ev0, s.ev1};
+    }
+    HIPCHK(launch_order(k, s.B, st));
+    h->timed = true;
+    return stream_leave(s, st);
+}
+
+int mpcqp_setup_solve_device(mpcqp_handle* h, const double* dPx, const double* dAx, const double* dq,
+                             const double* dl, const double* du, double* dx, double* dy, int32_t* dstatus,
+                             int32_t* diters, void* stream) {
+    if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "device entry points need a single-device handle");
+    Shard& s = h->shards[0];
+    hipStream_t st = pick(s, stream);
+    HIPCHK(hipSetDevice(s.dev));
+    if (int e = stream_enter(s, st)) return e;
+    if (h->collect) {
+        if (int e = ev_begin(h, h->ev_solve, st)) return e;
+    } else {
+        HIPCHK(hipEventRecord(s.ev0, st));
+    }
+    KParams k = s.kp;
+    k.ostat = dstatus;
+    k.oiter = diters;
+    HIPCHK(launch_setup_solve(k, s.B, dPx, dAx, dq, dl, du, dx, dy, st));
+    if (h->collect) {
+        if (int e = ev_end(h, h->ev_solve, st)) return e;
+        h->last_pair = h->ev_solve.back();
+    } else {
+        HIPCHK(hipEventRecord(s.ev1, st));
+        h->last_pair = {s.ev0, s.ev1};
+    }
+    HIPCHK(launch_order(k, s.B, st));
     h->timed = true;
     return stream_leave(s, st);
 }
@@ -580,12 +638,12 @@ int mpcqp_synchronize(mpcqp_handle* h) {
 }
 
 double mpcqp_last_kernel_ms(mpcqp_handle* h) {
-    if (!h || h->shards.size() != 1) return -1.0;
+    if (!h || h->shards.size() != 1 || !h->last_pair.first) return -1.0;
     Shard& s = h->shards[0];
     float ms = 0.f;
     if (hipSetDevice(s.dev) != hipSuccess) return -1.0;
-    if (hipEventSynchronize(s.ev1) != hipSuccess) return -1.0;
-    if (hipEventElapsedTime(&ms, s.ev0, s.ev1) != hipSuccess) return -1.0;
+    if (hipEventSynchronize(h->last_pair.second) != hipSuccess) return -1.0;
+    if (hipEventElapsedTime(&ms, h->last_pair.first, h->last_pair.second) != hipSuccess) return -1.0;
     return ms;
 }
 
@@ -610,7 +668,9 @@ int mpcqp_timing(mpcqp_handle* h, int32_t enable) {
     double t;
     if (int e = drain(h->ev_setup, &t)) return e;
     if (int e = drain(h->ev_solve, &t)) return e;
-    h->collect = enable != 0;
+    h->last_pair = {nullptr, nullptr};  // the drained events are gone
+    h->collect = (enable & 1) != 0;
+    h->collect_setup = (enable & 2) != 0;
     return 0;
 }
 
@@ -621,6 +681,7 @@ int mpcqp_timing_read(mpcqp_handle* h, double* setup_ms, int32_t* n_setup, doubl
     if (n_solve) *n_solve = (int32_t)h->ev_solve.size();
     if (int e = drain(h->ev_setup, setup_ms)) return e;
     if (int e = drain(h->ev_solve, solve_ms)) return e;
+    h->last_pair = {nullptr, nullptr};
     return 0;
 }
 

@@ -280,6 +280,53 @@ __device__ __forceinline__ void block_max_sum_tr(double (&v)[K], double (&sm)[KS
     __syncthreads();
 }
 
+// Dispatch order for the next solve, sorted by the workgroup that finishes LAST (the
+// counting sort of kernels.hip::k_order: 256 bins on iter >> shift, descending, stable in
+// instance order within a bin), so no separate kernel and no launch gap follow the solve.
+// Every workgroup arrives once on p.done after its instance's iteration count is written;
+// the last arrival has seen every count (release / acquire fences around the atomic),
+// and no workgroup of this launch still reads the order (all have finished).  smem:
+// 257 ints of LDS the caller no longer uses.
+template <int TT>
+__device__ __forceinline__ void order_epilogue(const KParams& p, int* smem) {
+    const long B = gridDim.x;
+    if (!p.done || !p.order || B <= p.slots || B > kOrderFuseMax) return;
+    const int tid = threadIdx.x;
+    int* cnt = smem;
+    int* last = smem + 256;
+    __syncthreads();  // the instance's results (iter by thread 0) are written
+    if (tid == 0) {
+        __threadfence();
+        *last = atomicAdd(p.done, 1) == (int)(B - 1);
+        __threadfence();
+    }
+    __syncthreads();
+    if (!*last) return;
+    int shift = 0;
+    while ((p.max_iter >> shift) >= 256) ++shift;
+    const int* iter = p.iter;
+    int* order = const_cast<int*>(p.order);
+    auto bin = [&](long i) {
+        const int k = __builtin_nontemporal_load(iter + i) >> shift;
+        return 255 - (k < 255 ? k : 255);
+    };
+    for (int k = tid; k < 256; k += TT) cnt[k] = 0;
+    __syncthreads();
+    for (long i = tid; i < B; i += TT) atomicAdd(&cnt[bin(i)], 1);
+    __syncthreads();
+    if (tid == 0) {
+        int s = 0;
+        for (int k = 0; k < 256; ++k) {
+            const int c = cnt[k];
+            cnt[k] = s;
+            s += c;
+        }
+        *p.done = 0;  // the next launch counts from zero
+    }
+    __syncthreads();
+    for (long i = tid; i < B; i += TT) order[atomicAdd(&cnt[bin(i)], 1)] = (int)i;
+}
+
 template <int TT>
 __device__ __forceinline__ bool block_any(bool f, int* flag) {
     if constexpr (TT == 64) {

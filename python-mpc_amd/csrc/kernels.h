@@ -54,7 +54,11 @@ struct KParams {
     // Rewritten after every solve by launch_order (longest previous solve first).
     const int* order;
     long slots;  // workgroups of the solve kernel resident at once on the device (CUs x occupancy)
+    // k_solve_w2 sorts the order itself in its last workgroup (device_common.h::order_epilogue)
+    // when the batch is at most kOrderFuseMax: arrival counter (zero between launches), or null
+    int* done;
 };
+constexpr long kOrderFuseMax = 16384;  // larger batches sort in k_order (1024 threads)
 
 size_t lds_setup_bytes(const KParams& p);
 size_t lds_solve_bytes(const KParams& p);
@@ -76,6 +80,10 @@ int solve_mode(int variant);
 int solve_threads(int variant);  // workgroup size of the variant's kernel
 bool variant_fits(const KParams& p, int variant);
 hipError_t launch_solve(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st);
+// setup + solve of the same inputs (solve_wave.hip): one fused kernel where the variant
+// allows it, else launch_setup then launch_solve
+hipError_t launch_setup_solve(const KParams& p, long B, const double* Px, const double* Ax, const double* q,
+                              const double* l, const double* u, double* xo, double* yo, hipStream_t st);
 // What a solve launch runs: the variant's kernel, workgroup size and dynamic LDS.  The
 // launch_solve_* functions given a non-null ref only fill it in (no launch).
 struct KernelRef {

@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 
 #include "device_common.h"
+#include "setup_r.h"
+#include "wave_util.h"
 
 namespace mpcqp {
 
@@ -164,6 +166,18 @@ __global__ __launch_bounds__(T) void k_setup(KParams p, const double* __restrict
     }
 }
 
+// ------------------------------------------------- setup, register lists --
+// setup_r.h::setup_r_body with 256 threads: one padded column and one row per thread
+template <int K, int KP, int AS, int PS>
+__global__ __launch_bounds__(T) void k_setup_r(KParams p, const double* __restrict__ Px_in,
+                                               const double* __restrict__ Ax_in,
+                                               const double* __restrict__ q_in,
+                                               const double* __restrict__ l_in,
+                                               const double* __restrict__ u_in) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    setup_r_body<T, K, KP, 1, AS, PS>(p, (long)blockIdx.x, Px_in, Ax_in, q_in, l_in, u_in, sm);
+}
+
 // ----------------------------------------------------------------- update --
 __global__ __launch_bounds__(T) void k_update(KParams p, const double* __restrict__ q_in,
                                               const double* __restrict__ l_in,
@@ -243,6 +257,11 @@ __global__ __launch_bounds__(T) void k_warm(KParams p, const double* __restrict_
 }
 
 // ------------------------------------------------------------ launchers --
+// diagnostic A/B switches read once per process (environment variable set to "1")
+static bool getenv_flag(const char* name) {
+    const char* v = getenv(name);
+    return v && v[0] == '1';
+}
 static size_t lds_setup_base(const KParams& p) {
     return sizeof(double) * ((size_t)p.nnzP + p.nnzA + 3 * (size_t)p.npad + 2 * (size_t)p.m + 64) + 16;
 }
@@ -252,8 +271,25 @@ static bool setup_staged(const KParams& p) {
 size_t lds_setup_bytes(const KParams& p) {
     return lds_setup_base(p) + (setup_staged(p) ? sizeof(int) * (size_t)setup_span(p) : 0);
 }
+// register-list setup (k_setup_r): one padded column and one row per thread, the
+// instantiation's list lengths and values per thread cover the plan; 0 = none fits
+static int setup_r_variant(const KParams& p) {
+    if (p.npad > T || p.m > T || p.pk > 4) return 0;
+    if (p.gk <= 6 && p.nnzA <= 2 * T && p.nnzP <= T) return 1;
+    if (p.gk <= 8 && p.nnzA <= 3 * T && p.nnzP <= T) return 2;
+    return 0;
+}
+
 hipError_t launch_setup(const KParams& p, long B, const double* Px, const double* Ax, const double* q,
                         const double* l, const double* u, hipStream_t st) {
+    if (const int v = setup_r_variant(p); v && !getenv_flag("MPCQP_SETUP_STAGED")) {
+        const size_t lds = lds_setup_r_bytes(p.nnzP, p.nnzA, p.npad, p.m);
+        auto k = v == 1 ? k_setup_r<6, 4, 2, 1> : k_setup_r<8, 4, 3, 1>;
+        hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(T), lds, st, p, Px, Ax, q, l, u);
+        return hipGetLastError();
+    }
     size_t lds = lds_setup_bytes(p);
     auto k = setup_staged(p) ? k_setup<true> : k_setup<false>;
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -310,6 +346,7 @@ hipError_t launch_order(const KParams& p, long B, hipStream_t st) {
     // a batch that fits the resident workgroup slots (CUs x the variant's occupancy,
     // api.hip::alloc_shard) starts all at once: the order cannot move anything
     if (!p.order || B <= p.slots) return hipSuccess;
+    if (p.done && B <= kOrderFuseMax) return hipSuccess;  // sorted by the solve kernel's last workgroup
     int shift = 0;
     while ((p.max_iter >> shift) >= kOrderBins) ++shift;
     hipLaunchKernelGGL(k_order, dim3(1), dim3(kOrderT), 0, st, (const int*)p.iter, const_cast<int*>(p.order), B,

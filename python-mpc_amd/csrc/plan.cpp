@@ -276,7 +276,7 @@ std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const
     pl.gcol.assign((size_t)pl.npad * kGS, pad);
     for (int pc = 0; pc < pl.npad; ++pc)
         for (int e = pl.acsc_ptr[pc], k = 0; e < pl.acsc_ptr[pc + 1]; ++e, ++k)
-            pl.gcol[(size_t)pc * kGS + k] = e | (pl.acsc_row[e] << 16);
+            pl.gcol[(size_t)k * pl.npad + pc] = e | (pl.acsc_row[e] << 16);
     // P by padded column (full symmetric), padded with (nnzP | 0): Pv[nnzP] is a zero slot
     pl.p_k = 0;
     for (int r = 0; r < pl.npad; ++r) pl.p_k = std::max(pl.p_k, pl.psym_ptr[r + 1] - pl.psym_ptr[r]);
@@ -285,11 +285,11 @@ std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const
     pl.gpsym.assign((size_t)pl.npad * kGS, pl.nnzP);
     for (int r = 0; r < pl.npad; ++r)
         for (int e = pl.psym_ptr[r], k = 0; e < pl.psym_ptr[r + 1]; ++e, ++k)
-            pl.gpsym[(size_t)r * kGS + k] = pl.psym_v[e] | (pl.psym_col[e] << 16);
+            pl.gpsym[(size_t)k * pl.npad + r] = pl.psym_v[e] | (pl.psym_col[e] << 16);
     pl.grow.assign((size_t)m * kGS, pad);
     for (int r = 0; r < m; ++r)
         for (int e = pl.acsr_ptr[r], k = 0; e < pl.acsr_ptr[r + 1]; ++e, ++k)
-            pl.grow[(size_t)r * kGS + k] = pl.acsr_pos[e] | (pl.acsr_col[e] << 16);
+            pl.grow[(size_t)k * m + r] = pl.acsr_pos[e] | (pl.acsr_col[e] << 16);
     return "";
 }
 

@@ -51,11 +51,13 @@ struct Plan {
     int max_level = 0;            // largest BFS level (diagnostic)
     int max_row_nnz = 0, max_col_nnz = 0;
     int gather_k = 0;             // max(max_row_nnz, max_col_nnz)
-    // packed gather lists: [npad*kGS] by padded column (A' w), [m*kGS] by row (A x):
-    // (position of the value in the padded-CSC order) | (vector index << 16), padding (nnzA | 0)
+    // packed gather lists: [kGS][npad] by padded column (A' w), [kGS][m] by row (A x):
+    // (position of the value in the padded-CSC order) | (vector index << 16), padding (nnzA | 0).
+    // Entry k of every column (row) is contiguous, so the kernels' per-lane list loads
+    // (lane = column / row) are coalesced.
     std::vector<int> gcol, grow;
     int p_k = 0;                  // max nonzeros per column of the symmetric P
-    std::vector<int> gpsym;       // [npad*kGS] P by padded column: (Pv index) | (padded column << 16)
+    std::vector<int> gpsym;       // [kGS][npad] P by padded column: (Pv index) | (padded column << 16)
     int amax = 0;                 // max over k of (last nonzero local row of E_k) + 1: F_k rows / H_{k-1} cols
     // the other side of the coupling: the columns of E_{k+1} (variables of block k that
     // couple to block k+1, its last BFS level) lie in [toff[k], toff[k] + bmax)

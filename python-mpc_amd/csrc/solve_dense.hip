@@ -146,24 +146,24 @@ __global__ __launch_bounds__(TD, 2) void k_solve_d(KParams p, double* __restrict
                     double* row = ST + (jr - c0) * R;
                     if (cv) {
                         row[jr] += sigma;
-                        const int* pl = p.gpsym + (long)pcs * kGS;
+                        const int* pl = p.gpsym + pcs;
 #pragma unroll 1
                         for (int k = 0; k < p.pk; ++k) {
-                            const unsigned e = (unsigned)pl[k];
+                            const unsigned e = (unsigned)pl[(long)k * npad];
                             const int idx = (int)(e & 0xFFFFu), j = p.pad_var[e >> 16];
                             if (idx < nnzP && j >= 0) row[j] += L.Pv[idx];
                         }
-                        const int* cl = p.gcol + (long)pcs * kGS;
+                        const int* cl = p.gcol + pcs;
 #pragma unroll 1
                         for (int k = 0; k < p.gk; ++k) {
-                            const unsigned e = (unsigned)cl[k];
+                            const unsigned e = (unsigned)cl[(long)k * npad];
                             const int a = (int)(e & 0xFFFFu), i = (int)(e >> 16);
                             if (a >= nnzA) continue;
                             const double wa = rho_of(L.ct[i], rho) * L.Acsc[a];
-                            const int* rl = p.grow + (long)i * kGS;
+                            const int* rl = p.grow + i;
 #pragma unroll 1
                             for (int k2 = 0; k2 < p.gk; ++k2) {
-                                const unsigned e2 = (unsigned)rl[k2];
+                                const unsigned e2 = (unsigned)rl[(long)k2 * m];
                                 const int a2 = (int)(e2 & 0xFFFFu), j = p.pad_var[e2 >> 16];
                                 if (a2 < nnzA && j >= 0) row[j] += wa * L.Acsc[a2];
                             }
@@ -261,7 +261,7 @@ __global__ __launch_bounds__(TD, 2) void k_solve_d(KParams p, double* __restrict
         const unsigned abase = lds_addr(L.Acsc), wbase = lds_addr(L.w), xbase = lds_addr(L.xt);
         const unsigned Xbase = lds_addr(C.X);
         GatherW<K> cg;
-        if (cv) cg.load(p.gcol + (long)pcs * kGS, abase, wbase);
+        if (cv) cg.load(p.gcol + pcs, npad, abase, wbase);
         else cg.clear(abase + 8u * nnzA, wbase);
         GatherW<K> rg[RS];
         double y[RS], Z[RS], dy[RS], rv[RS], rvi[RS];
@@ -272,7 +272,7 @@ __global__ __launch_bounds__(TD, 2) void k_solve_d(KParams p, double* __restrict
             const int i = min(tid + s * TD, mp - 1);  // lanes past the padded rows repeat the inert last row
             ri[s] = i;
             dy[s] = 0.0;
-            if (i < m) rg[s].load(p.grow + (long)i * kGS, abase, xbase);
+            if (i < m) rg[s].load(p.grow + i, m, abase, xbase);
             else rg[s].clear(abase + 8u * nnzA, xbase);
             y[s] = L.ys[i];
             Z[s] = C.Z[i];
@@ -379,7 +379,7 @@ __global__ __launch_bounds__(TD, 2) void k_solve_d(KParams p, double* __restrict
             const unsigned ysbase = lds_addr(L.ys), dYbase = lds_addr(C.dY), dxbase = lds_addr(L.dx);
             // (the scalings and the P list are only needed here: loaded per check)
             GatherW<KPK> pg;
-            if (cv) pg.load(p.gpsym + (long)pcs * kGS, lds_addr(L.Pv), Xbase);
+            if (cv) pg.load(p.gpsym + pcs, npad, lds_addr(L.Pv), Xbase);
             else pg.clear(lds_addr(L.Pv) + 8u * nnzP, Xbase);
             const double Dv = cv ? p.D[b * npad + pcs] : 1.0;
             double Ev[RS];

@@ -338,9 +338,9 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
 template <int K>
 struct Gather {
     unsigned e[K];
-    __device__ __forceinline__ void load(const int* list) {
+    __device__ __forceinline__ void load(const int* list, int stride) {  // list[k * stride]
 #pragma unroll
-        for (int k = 0; k < K; ++k) e[k] = (unsigned)list[k];
+        for (int k = 0; k < K; ++k) e[k] = (unsigned)list[(long)k * stride];
     }
     __device__ __forceinline__ void clear(int zero_pos) {
 #pragma unroll
@@ -471,26 +471,27 @@ __device__ __forceinline__ void fail_status(const KP& p, long b) {
 
 // ---- out-of-line phases: everything they need is in LDS or in the plan ----
 // dot of a packed gather list (value index | vector index << 16) with cnt entries
-__device__ __forceinline__ double list_dot(const int* __restrict__ list, int cnt, const double* V, const double* v) {
+__device__ __forceinline__ double list_dot(const int* __restrict__ list, int stride, int cnt, const double* V,
+                                           const double* v) {
     double acc = 0.0;
 #pragma unroll 4
     for (int k = 0; k < cnt; ++k) {
-        const unsigned e = (unsigned)list[k];
+        const unsigned e = (unsigned)list[(long)k * stride];
         acc += V[e & 0xFFFFu] * v[e >> 16];
     }
     return acc;
 }
 template <class KP>
 __device__ __forceinline__ double row_dot(const KP& p, const double* A, const double* v, int i) {
-    return list_dot(p.grow + (long)i * kGS, p.gk, A, v);
+    return list_dot(p.grow + i, p.m, p.gk, A, v);
 }
 template <class KP>
 __device__ __forceinline__ double col_dot(const KP& p, const double* A, const double* v, int pc) {
-    return list_dot(p.gcol + (long)pc * kGS, p.gk, A, v);
+    return list_dot(p.gcol + pc, p.npad, p.gk, A, v);
 }
 template <class KP>
 __device__ __forceinline__ double psym_dot(const KP& p, const double* Pv, const double* v, int pc) {
-    return list_dot(p.gpsym + (long)pc * kGS, p.pk, Pv, v);
+    return list_dot(p.gpsym + pc, p.npad, p.pk, Pv, v);
 }
 
 // update_info: residuals and the norms of their tolerances (OSQP compute_pri_res /

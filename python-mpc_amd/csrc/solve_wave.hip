@@ -30,6 +30,9 @@
 // vehicle_lateral_mpc_slack_increment.py:248 / Control/MPC/mpc_dynamics.py:396).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
+#include "setup_r.h"
 #include "solve_phases.h"
 #include "wave_util.h"
 
@@ -160,7 +163,7 @@ __global__ __launch_bounds__(TW, 1) void k_solve_w(KParams p, double* __restrict
             X[e] = C.X[pc];
             Q[e] = L.qv[pc];
             DX[e] = 0.0;
-            cg[e].load(p.gcol + (long)pc * kGS, abase, wbase);
+            cg[e].load(p.gcol + pc, npad, abase, wbase);
         }
         GatherW<K> rg[RS];
         double y[RS], Z[RS], dy[RS], rv[RS], rvi[RS];
@@ -169,7 +172,7 @@ __global__ __launch_bounds__(TW, 1) void k_solve_w(KParams p, double* __restrict
         for (int s = 0; s < RS; ++s) {
             const int i = lane + s * TW;  // < mp
             dy[s] = 0.0;
-            if (i < m) rg[s].load(p.grow + (long)i * kGS, abase, xbase);
+            if (i < m) rg[s].load(p.grow + i, m, abase, xbase);
             else rg[s].clear(abase + 8u * nnzA, xbase);
             y[s] = L.ys[i];
             Z[s] = C.Z[i];
@@ -412,8 +415,8 @@ __global__ __launch_bounds__(TW, 1) void k_solve_w(KParams p, double* __restrict
 constexpr int T2 = 128;
 
 template <int K, int RS, int KPK>
-__global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restrict__ xo, double* __restrict__ yo,
-                                                    int factor_only) {
+__device__ __forceinline__ void solve_w2_body(const KParams& p, double* __restrict__ xo, double* __restrict__ yo,
+                                              int factor_only) {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int h = lane >> 5, r = lane & 31, rr = lane >> 3, ch = lane & 7;
     const int kb = w ? 1 + h : 3 * h;          // own block
@@ -526,12 +529,12 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
         const double Q = L.qv[pc];
         const unsigned abase = lds_addr(L.Acsc), wbase = lds_addr(L.w), xbase = lds_addr(L.xt);
         GatherW<K> cg;
-        cg.load(p.gcol + (long)pc * kGS, abase, wbase);
+        cg.load(p.gcol + pc, npad, abase, wbase);
         // for the inline termination check: the column's P list (addresses of Pv / X),
         // the scalings D of the column and E of the rows
         const unsigned Xbase = lds_addr(C.X);
         GatherW<KPK> pg;
-        pg.load(p.gpsym + (long)pc * kGS, lds_addr(L.Pv), Xbase);
+        pg.load(p.gpsym + pc, npad, lds_addr(L.Pv), Xbase);
         const double Dv = p.D[b * npad + pc];
         // phase-C slots (pair, j) of the lane; pair NP is the zero block
         int gslot[3], tslot[3];
@@ -557,7 +560,7 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
             ri[s] = i;
             dy[s] = 0.0;
             Ev[s] = i < m ? p.E[b * m + i] : 1.0;
-            if (i < m) rg[s].load(p.grow + (long)i * kGS, abase, xbase);
+            if (i < m) rg[s].load(p.grow + i, m, abase, xbase);
             else rg[s].clear(abase + 8u * nnzA, xbase);
             y[s] = L.ys[i];
             Z[s] = C.Z[i];
@@ -923,6 +926,57 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
 #undef PH
 #undef PHL
 #undef PHC
+}
+
+// the kernel: the solve, then (last workgroup only) the dispatch order of the next launch
+template <int K, int RS, int KPK>
+__global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restrict__ xo, double* __restrict__ yo,
+                                                    int factor_only) {
+    solve_w2_body<K, RS, KPK>(p, xo, yo, factor_only);
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    order_epilogue<T2>(p, (int*)sm);
+}
+
+// Fused setup + solve (mpcqp_setup_solve_device): the workgroup Ruiz-scales its
+// instance with the register-list setup (setup_r.h, the same arithmetic as k_setup /
+// k_setup_r), then solves it.  Everything the solve reads from the workspace was
+// written by this workgroup before the barrier, so no second kernel, no launch gap and
+// no setup kernel in front of the slowest instance.
+template <int K, int RS, int KPK, int SK, int SRS, int SAS, int SPS>
+__global__ __launch_bounds__(T2, 1) void k_setup_solve_w2(KParams p, const double* __restrict__ Px_in,
+                                                          const double* __restrict__ Ax_in,
+                                                          const double* __restrict__ q_in,
+                                                          const double* __restrict__ l_in,
+                                                          const double* __restrict__ u_in, double* __restrict__ xo,
+                                                          double* __restrict__ yo) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    setup_r_body<T2, SK, 4, SRS, SAS, SPS>(p, instance_of(p), Px_in, Ax_in, q_in, l_in, u_in, sm);
+    __syncthreads();
+    solve_w2_body<K, RS, KPK>(p, xo, yo, 0);
+    order_epilogue<T2>(p, (int*)sm);
+}
+
+// the fused kernel's instantiation for the plan, or 0: variant 10 and the 128-thread
+// register-list setup shape (one padded column per thread, two rows, four A values)
+static int setup_solve_fits(const KParams& p) {
+    return p.variant == 10 && p.npad <= T2 && p.m <= 2 * T2 && p.gk <= 6 && p.pk <= 4 && p.nnzA <= 4 * T2 &&
+           p.nnzP <= 2 * T2;
+}
+
+hipError_t launch_setup_solve(const KParams& p, long B, const double* Px, const double* Ax, const double* q,
+                              const double* l, const double* u, double* xo, double* yo, hipStream_t st) {
+    if (!setup_solve_fits(p)) {
+        hipError_t e = launch_setup(p, B, Px, Ax, q, l, u, st);
+        return e != hipSuccess ? e : launch_solve(p, B, xo, yo, 0, st);
+    }
+    const size_t lds = std::max(lds_w2_bytes(p), lds_setup_r_bytes(p.nnzP, p.nnzA, p.npad, p.m));
+    auto k = k_setup_solve_w2<6, 2, 4, 6, 2, 4, 2>;
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(T2), lds, st, p, Px, Ax, q, l, u, xo, yo);
+    e = hipGetLastError();
+    if (e != hipSuccess || !p.polish) return e;
+    return launch_polish(p, B, xo, yo, st);
 }
 
 template <int K, int RS, int KPK>

@@ -12,10 +12,10 @@ namespace mpcqp {
 template <int K>
 struct GatherW {
     unsigned e[K];
-    __device__ __forceinline__ void load(const int* list, unsigned abase, unsigned vbase) {
+    __device__ __forceinline__ void load(const int* list, int stride, unsigned abase, unsigned vbase) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const unsigned raw = (unsigned)list[k];
+            const unsigned raw = (unsigned)list[(long)k * stride];
             e[k] = (((raw >> 16) * 8u + vbase) << 16) | ((raw & 0xFFFFu) * 8u + abase);
         }
     }

@@ -124,6 +124,7 @@ def lib():
                                _P(_Settings), C.c_int32, hp]
     L.mpcqp_setup_device.argtypes = [vp, vp, vp, vp, vp, vp, vp]
     L.mpcqp_update_device.argtypes = [vp, vp, vp, vp, vp]
+    L.mpcqp_setup_solve_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.mpcqp_warm_start_device.argtypes = [vp, vp, vp, vp]
     L.mpcqp_solve_device.argtypes = [vp, vp, vp, vp, vp, vp]
     L.mpcqp_synchronize.argtypes = [vp]
@@ -441,11 +442,21 @@ class DeviceBatch:
         _check(lib().mpcqp_solve_device(self._h.ptr, self._ptr(x), self._ptr(y), self._ptr(status),
                                         self._ptr(iters), stream), "solve_device")
 
+    def setup_solve(self, Px, Ax, q, l, u, x=None, y=None, status=None, iters=None, stream=None):
+        """setup(Px, Ax, q, l, u) then solve(x, y, status, iters) -- one fused kernel where the
+        solve kernel allows it (mpcqp_setup_solve_device), identical results."""
+        _check(lib().mpcqp_setup_solve_device(self._h.ptr, self._ptr(Px), self._ptr(Ax), self._ptr(q), self._ptr(l),
+                                              self._ptr(u), self._ptr(x), self._ptr(y), self._ptr(status),
+                                              self._ptr(iters), stream), "setup_solve_device")
+
     def synchronize(self):
         _check(lib().mpcqp_synchronize(self._h.ptr), "synchronize")
 
-    def timing(self, enable=True):
-        _check(lib().mpcqp_timing(self._h.ptr, int(bool(enable))), "timing")
+    def timing(self, enable=True, setup=True):
+        """HIP-event timing of the solve launches (and of the setup launches when
+        `setup`); every recorded event is one more packet between the kernels."""
+        mask = (1 | (2 if setup else 0)) if enable else 0
+        _check(lib().mpcqp_timing(self._h.ptr, mask), "timing")
 
     def timing_read(self):
         sm = C.c_double(); so = C.c_double(); ns = C.c_int32(); no = C.c_int32()

@@ -398,3 +398,65 @@ def test_calls_on_different_streams_are_ordered():
     ref.synchronize()
     for a, c in zip(o1 + o2, r1 + r2):
         assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("cfg,B", [(2, 512), (3, 512)])
+def test_register_list_setup_is_bit_identical(monkeypatch, cfg, B):
+    """kernels.hip::k_setup_r (register-resident gather lists, one column / row per
+    thread) against the staged-index k_setup (MPCQP_SETUP_STAGED=1): the same Ruiz
+    scaling arithmetic in the same order, so the solves that follow agree bit for bit."""
+    import torch
+    from osqp_amd import DeviceBatch
+    b = mpc.make_batch(cfg, B=B, seed=77)
+    s = {k: v for k, v in b["settings"].items() if k != "verbose"}
+    dev = torch.device("cuda", 0)
+    X = [torch.from_numpy(np.ascontiguousarray(b[k])).to(dev) for k in ("Px", "Ax", "q", "l", "u")]
+
+    def run():
+        h = DeviceBatch(b["P"], b["A"], B, device=0, **s)
+        o = (torch.empty((B, b["n"]), dtype=torch.float64, device=dev),
+             torch.empty((B, b["m"]), dtype=torch.float64, device=dev),
+             torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev))
+        h.setup(*X)
+        h.solve(*o)
+        h.synchronize()
+        return o
+
+    fast = run()
+    monkeypatch.setenv("MPCQP_SETUP_STAGED", "1")
+    staged = run()
+    for a, c in zip(fast, staged):
+        assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("cfg,B", [(2, 1024), (2, 40), (3, 96)])
+def test_fused_setup_solve_is_bit_identical(cfg, B):
+    """mpcqp_setup_solve_device (one kernel for the two-wave variant: solve_wave.hip::
+    k_setup_solve_w2; setup + solve kernels otherwise) against setup_device +
+    solve_device on a second handle: identical outputs, over two consecutive batches
+    (the second dispatched in the order the first left behind)."""
+    import torch
+    from osqp_amd import DeviceBatch
+    bx, by = mpc.make_batch(cfg, B=B, seed=41), mpc.make_batch(cfg, B=B, seed=42)
+    s = {k: v for k, v in bx["settings"].items() if k != "verbose"}
+    dev = torch.device("cuda", 0)
+    n, m = bx["n"], bx["m"]
+
+    def put(b):
+        return [torch.from_numpy(np.ascontiguousarray(b[k])).to(dev) for k in ("Px", "Ax", "q", "l", "u")]
+
+    def out():
+        return (torch.empty((B, n), dtype=torch.float64, device=dev), torch.empty((B, m), dtype=torch.float64, device=dev),
+                torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev))
+
+    X, Y = put(bx), put(by)
+    fused, sep = DeviceBatch(bx["P"], bx["A"], B, device=0, **s), DeviceBatch(bx["P"], bx["A"], B, device=0, **s)
+    for D in (X, Y):
+        of, os_ = out(), out()
+        fused.setup_solve(*D, *of)
+        sep.setup(*D)
+        sep.solve(*os_)
+        torch.cuda.synchronize()
+        for a, c in zip(of, os_):
+            assert torch.equal(a, c)
+    assert (of[2] == 1).all()
