@@ -354,7 +354,7 @@ __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ 
         for (int s = 0; s < CS; ++s) {
             const int pc = tid + s * T;
             cvar[s] = pc < npad ? p.pad_var[pc] : -1;
-            if (pc < npad) cg[s].load(p.gcol + pc, npad);
+            if (pc < npad) cg[s].load(p.gcol + pc, &p.self->npad);
             else cg[s].clear(nnzA);
         }
         Gather<K> rg[RS];
@@ -362,7 +362,7 @@ __global__ __launch_bounds__(T, W) void k_solve(KParams p, double* __restrict__ 
         for (int s = 0; s < RS; ++s) {
             const int i = tid + s * T;
             if (i < m) {
-                rg[s].load(p.grow + i, m);
+                rg[s].load(p.grow + i, &p.self->m);
                 L.w[i] = rho_of(L.ct[i], rho) * Z[i] - y[s];  // w = rho z_prev - y (rho may be new)
             } else {
                 rg[s].clear(nnzA);

@@ -650,7 +650,7 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
         for (int s = 0; s < CS; ++s) {
             const int pc = tid + s * TTK;
             cvar[s] = pc < npad ? p.pad_var[pc] : -1;
-            if (pc < npad) cg[s].load(p.gcol + pc, npad);
+            if (pc < npad) cg[s].load(p.gcol + pc, &p.self->npad);
             else cg[s].clear(nnzA);
         }
         Gather<K> rg[RS];
@@ -658,7 +658,7 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
         for (int s = 0; s < RS; ++s) {
             const int i = tid + s * TTK;
             if (i < m) {
-                rg[s].load(p.grow + i, m);
+                rg[s].load(p.grow + i, &p.self->m);
                 L.w[i] = rho_of(L.ct[i], rho) * Z[i] - y[s];  // w = rho z_prev - y (rho may be new)
             } else {
                 rg[s].clear(nnzA);

@@ -84,7 +84,8 @@ __device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restri
     // column entry and the lane's half of row p are read together, so the row's LDS
     // latency overlaps the reciprocal's Newton chain; the pivot row's own lane runs the
     // FMA pass with a zero multiplier (v + (-0) * row == v exactly for finite rows).
-    // cfg 3 (256-thread kernel) Gauss-Jordan 868 k -> 787 k cycles per slowest solve.
+    // cfg 3 (256-thread kernel) Gauss-Jordan 868 k -> 767 k cycles per slowest solve (the
+    // solve time is the same with the divergent step here: measured A/B, round 2).
     auto pivot = [&](const int p, const int pj) __attribute__((always_inline)) {
         const int ph = p >> 4;
         double* rb = buf + (pj & 1) * S;
@@ -286,15 +287,23 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
 #pragma unroll 1
                     for (int o = tid; o < amax * S; o += TT) {
                         const int r = o >> 5, c = o & (S - 1);
-                        // mode 2 has amax <= 8 (variant_fits): the 8 loads of G_{k-1,j} (global,
-                        // just written) go out together; rows >= amax stay inside the tile array
-                        double gv[8];
-#pragma unroll
-                        for (int l = 0; l < 8; ++l) gv[l] = Gp[l * S + c];
                         double sacc = 0.0;
+                        if constexpr (TT == 128) {
+                            // two-wave kernel (mode 2 there has amax <= 8, variant_fits): the 8
+                            // loads of G_{k-1,j} (global, just written) go out together; rows >=
+                            // amax stay inside the tile array.  Not in the 256-thread kernels:
+                            // the unrolled loads raise factorize_nl's SGPR use, which costs the
+                            // calling solve loop SGPR spills (cfg 3 solve +6 %).
+                            double gv[8];
 #pragma unroll
-                        for (int l = 0; l < 8; ++l)
-                            if (l < amax) sacc += SP[r * S + l] * gv[l];
+                            for (int l = 0; l < 8; ++l) gv[l] = Gp[l * S + c];
+#pragma unroll
+                            for (int l = 0; l < 8; ++l)
+                                if (l < amax) sacc += SP[r * S + l] * gv[l];
+                        } else {
+#pragma unroll 1
+                            for (int l = 0; l < amax; ++l) sacc += SP[r * S + l] * Gp[l * S + c];
+                        }
                         Gk[o] = -sacc;
                     }
                 }
@@ -338,9 +347,14 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
 template <int K>
 struct Gather {
     unsigned e[K];
-    __device__ __forceinline__ void load(const int* list, int stride) {  // list[k * stride]
+    // list[k * stride].  `stride` is read through a volatile pointer (a scalar load at
+    // every run start), so the k * stride offsets cannot be hoisted out of the solve loop
+    // and held in registers for its whole length (measured: 28 more VGPR spills in the
+    // 256-thread nb = 8 kernel when they are).
+    __device__ __forceinline__ void load(const int* list, const volatile int* stride) {
+        const int st = *stride;
 #pragma unroll
-        for (int k = 0; k < K; ++k) e[k] = (unsigned)list[(long)k * stride];
+        for (int k = 0; k < K; ++k) e[k] = (unsigned)list[k * st];
     }
     __device__ __forceinline__ void clear(int zero_pos) {
 #pragma unroll

@@ -11,7 +11,8 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "python-mpc_amd"))
+_pkg = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--pkg=")]  # A/B: another build's package
+sys.path.insert(0, _pkg[0] if _pkg else os.path.join(ROOT, "python-mpc_amd"))
 os.environ.setdefault("MPCQP_PHASE_PROF", "1")
 
 import numpy as np  # noqa: E402
@@ -21,6 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--pkg", default=None, help="package directory of another build (--pkg=DIR)")
     args = ap.parse_args()
     import torch
     from osqp_amd import DeviceBatch, mpc, _drop_common_zeros
