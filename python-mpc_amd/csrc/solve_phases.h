@@ -59,13 +59,17 @@ __device__ __forceinline__ void put16(double (&v)[16], int j, double x) {
 // to sign -- M_ij = -M_ji exactly when one of i, j is already pivoted -- so row p is
 // published by the lanes that hold column p (one ds_write_b64 per lane and pivot) and the
 // 32 pivots need no workgroup barrier.  buf: 2 S doubles.  False on a non-positive pivot.
+// npiv: the tile's real rows (plan bsize); the rest are padding at the end -- identity
+// rows and columns that pivoting leaves as they are -- so the rolled loop skips their
+// pivots (cfg 3's 256-thread kernel: solve 40.1 -> 39.3 ms at B = 16384).
 //
 // Compact = false: the pivot loop is unrolled (static register indices, fastest; the
 // wave kernels can afford its ~200 VGPRs).  Compact = true: a rolled loop whose pivot
 // slot is picked with scalar switches (~90 VGPRs), for the 256-thread kernels, where
 // the unrolled form costs occupancy in every other phase.
 template <bool Compact>
-__device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restrict__ buf, double* __restrict__ Sgk) {
+__device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restrict__ buf, double* __restrict__ Sgk,
+                                        const int npiv = S) {
     const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
     double v[16];
 #pragma unroll
@@ -126,7 +130,7 @@ __device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restri
     };
     if constexpr (Compact) {
 #pragma unroll 1
-        for (int p = 0; p < S; ++p) pivot(p, __builtin_amdgcn_readfirstlane(p & 15));
+        for (int p = 0; p < npiv; ++p) pivot(p, __builtin_amdgcn_readfirstlane(p & 15));
     } else {
         // the unrolled loop keeps the divergent update: measured faster here than the
         // branch-free step (cfg 2 Gauss-Jordan 233 k vs 275 k cycles per solve of the
@@ -165,6 +169,8 @@ __device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restri
             }
             if (h == ph) v[pj] = i == p ? 1.0 : -cd;
         };
+        // all 32 pivots: an early exit at npiv breaks the unrolled schedule (measured: cfg 2
+        // Gauss-Jordan 227 k -> 297 k cycles on the slowest instance despite 19 % fewer pivots)
 #pragma unroll
         for (int p = 0; p < S; ++p) pivot_br(p, p & 15);
     }
@@ -324,7 +330,7 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
             // one wave inverts the tile (no barrier per pivot); the verdict goes through LDS
             double* okslot = Ek + 2 * S;
             if (tid < 64) {
-                const bool okw = gj_wave<(TT > 128)>(DK, Ek, Sg + (long)k * SS);
+                const bool okw = gj_wave<(TT > 128)>(DK, Ek, Sg + (long)k * SS, p.bsize[k]);
                 if (tid == 0) okslot[0] = okw ? 1.0 : 0.0;
             } else if (OVL && tid < 128 && k + 1 < nb) {
                 assemble(k + 1, SP, Eh(k + 1), tid - 64, 64, wave_sync);
