@@ -33,7 +33,8 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(ROOT, "python-mpc_amd"))
+# MPCQP_PKG: diagnostic A/B of another build of the package (tools/gpu_ab2.sh)
+sys.path.insert(0, os.environ.get("MPCQP_PKG", os.path.join(ROOT, "python-mpc_amd")))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 import numpy as np  # noqa: E402

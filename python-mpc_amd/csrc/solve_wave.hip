@@ -481,6 +481,17 @@ __device__ __forceinline__ void solve_w2_body(const KParams& p, double* __restri
 
     int status = MPCQP_UNSOLVED_, rho_updates = 0, iter = 0, info_iter = 0;
     bool can_check = false, need_factor = true;
+    // Loop-invariant per-lane data from global memory (the plan's gather lists, the
+    // scalings D and E): loaded after each factorisation (which is a call: nothing
+    // vector-valued is live across it), kept in registers across the runs and the
+    // inline termination checks in between.
+    const int pc = kb * S + r;
+    const unsigned abase = lds_addr(L.Acsc), wbase = lds_addr(L.w), xbase = lds_addr(L.xt);
+    const unsigned Xbase = lds_addr(C.X);
+    bool cv = false;
+    double Dv = 1.0, Ev[RS];
+    GatherW<K> cg, rg[RS];
+    GatherW<KPK> pg;  // the column's P list (addresses of Pv / X), for the inline check
     PH(5)
     for (;;) {
         __syncthreads();
@@ -511,6 +522,17 @@ __device__ __forceinline__ void solve_w2_body(const KParams& p, double* __restri
                 const int q = o >> 8, t = (o >> 5) & 7;
                 L.gl[o] = (q < NP && t < p.amax) ? Hg[(long)q * p.amax * S + (o & 255)] : 0.0;
             }
+            cv = p.pad_var[pc] >= 0;
+            cg.load(p.gcol + pc, npad, abase, wbase);
+            pg.load(p.gpsym + pc, npad, lds_addr(L.Pv), Xbase);
+            Dv = p.D[b * npad + pc];
+#pragma unroll
+            for (int s = 0; s < RS; ++s) {
+                const int i = min(tid + s * T2, mp - 1);
+                Ev[s] = i < m ? p.E[b * m + i] : 1.0;
+                if (i < m) rg[s].load(p.grow + i, m, abase, xbase);
+                else rg[s].clear(abase + 8u * nnzA, xbase);
+            }
             PH(0)
         }
         // ---- run state ----
@@ -523,19 +545,8 @@ __device__ __forceinline__ void solve_w2_body(const KParams& p, double* __restri
 #pragma unroll
             for (int i = 0; i < 8; i += 2) ld2(srr + i, SR[i], SR[i + 1]);
         }
-        const int pc = kb * S + r;
-        const bool cv = p.pad_var[pc] >= 0;
         double X = C.X[pc], DX = 0.0;
         const double Q = L.qv[pc];
-        const unsigned abase = lds_addr(L.Acsc), wbase = lds_addr(L.w), xbase = lds_addr(L.xt);
-        GatherW<K> cg;
-        cg.load(p.gcol + pc, npad, abase, wbase);
-        // for the inline termination check: the column's P list (addresses of Pv / X),
-        // the scalings D of the column and E of the rows
-        const unsigned Xbase = lds_addr(C.X);
-        GatherW<KPK> pg;
-        pg.load(p.gpsym + pc, npad, lds_addr(L.Pv), Xbase);
-        const double Dv = p.D[b * npad + pc];
         // phase-C slots (pair, j) of the lane; pair NP is the zero block
         int gslot[3], tslot[3];
         {
@@ -550,8 +561,7 @@ __device__ __forceinline__ void solve_w2_body(const KParams& p, double* __restri
                 tslot[s] = lds_addr(L.tv + w * 32 + jj[s] * 8);
             }
         }
-        GatherW<K> rg[RS];
-        double y[RS], Z[RS], dy[RS], rv[RS], rvi[RS], Ev[RS];
+        double y[RS], Z[RS], dy[RS], rv[RS], rvi[RS];
         int ri[RS];
         const double r_hi = RHO_EQ_OVER_RHO_INEQ * rho;
 #pragma unroll
@@ -559,9 +569,6 @@ __device__ __forceinline__ void solve_w2_body(const KParams& p, double* __restri
             const int i = min(tid + s * T2, mp - 1);  // lanes past the padded rows repeat the inert last row
             ri[s] = i;
             dy[s] = 0.0;
-            Ev[s] = i < m ? p.E[b * m + i] : 1.0;
-            if (i < m) rg[s].load(p.grow + i, m, abase, xbase);
-            else rg[s].clear(abase + 8u * nnzA, xbase);
             y[s] = L.ys[i];
             Z[s] = C.Z[i];
             const signed char cl = L.ct[i];  // OSQP rho_vec / rho_inv_vec of the row
@@ -823,33 +830,38 @@ __device__ __forceinline__ void solve_w2_body(const KParams& p, double* __restri
                     if (unscale) mxd *= cinv;
                     const bool dual_ok = R.dua < p.eps_abs + p.eps_rel * mxd;
                     bool prim_inf = false, dual_inf = false;
-                    if (!prim_ok || !dual_ok) {  // infeasibility certificates (uniform branch)
-                        __syncthreads();  // the projected delta y
+                    if (!prim_ok || !dual_ok) {  // infeasibility certificates (uniform branches)
+                        // OSQP's is_primal_infeasible / is_dual_infeasible evaluate their tests in
+                        // order and return at the first that fails: the reduced norms and sums
+                        // decide whether the gathered A'dy maximum / the A dx row test is needed
                         const double norm_dy = mx[14], norm_dx = mx[15], epi = p.eps_pinf, edi = p.eps_dinf;
-                        double na[1] = {0.0};
-                        double a = 0.0;
-#pragma unroll
-                        for (int k = 0; k < K; ++k) {
-                            const unsigned e = cg.e[k];
-                            a += lds_at(e & 0xFFFFu) * lds_at((e >> 16) - wbase + dYbase);
-                        }
-                        if (cv) na[0] = fabs(unscale ? a * (1.0 / Dv) : a);
-                        bool viol = false;
-#pragma unroll
-                        for (int s = 0; s < RS; ++s) {
-                            if (!(tid + s * T2 < m)) continue;
-                            const double ar = unscale ? adx[s] * (1.0 / Ev[s]) : adx[s];
-                            const double lo = L.lo[ri[s]], up = L.up[ri[s]];
-                            if ((up < OSQP_INFTY * MIN_SCALING && ar > edi * norm_dx) ||
-                                (lo > -OSQP_INFTY * MIN_SCALING && ar < -edi * norm_dx))
-                                viol = true;
-                        }
-                        block_max<T2, 1>(na, L.red);
-                        viol = block_any<T2>(viol, L.flag);
                         const double cs = unscale ? cval : 1.0;
-                        prim_inf = !prim_ok && m != 0 && norm_dy > epi && sm[0] < epi * norm_dy && na[0] < epi * norm_dy;
-                        dual_inf = !dual_ok && norm_dx > edi && sm[1] < cs * edi * norm_dx && mx[16] < cs * edi * norm_dx &&
-                                   !viol;
+                        if (!prim_ok && m != 0 && norm_dy > epi && sm[0] < epi * norm_dy) {
+                            __syncthreads();  // the projected delta y
+                            double na[1] = {0.0};
+                            double a = 0.0;
+#pragma unroll
+                            for (int k = 0; k < K; ++k) {
+                                const unsigned e = cg.e[k];
+                                a += lds_at(e & 0xFFFFu) * lds_at((e >> 16) - wbase + dYbase);
+                            }
+                            if (cv) na[0] = fabs(unscale ? a * (1.0 / Dv) : a);
+                            block_max<T2, 1>(na, L.red);
+                            prim_inf = na[0] < epi * norm_dy;
+                        }
+                        if (!dual_ok && norm_dx > edi && sm[1] < cs * edi * norm_dx && mx[16] < cs * edi * norm_dx) {
+                            bool viol = false;
+#pragma unroll
+                            for (int s = 0; s < RS; ++s) {
+                                if (!(tid + s * T2 < m)) continue;
+                                const double ar = unscale ? adx[s] * (1.0 / Ev[s]) : adx[s];
+                                const double lo = L.lo[ri[s]], up = L.up[ri[s]];
+                                if ((up < OSQP_INFTY * MIN_SCALING && ar > edi * norm_dx) ||
+                                    (lo > -OSQP_INFTY * MIN_SCALING && ar < -edi * norm_dx))
+                                    viol = true;
+                            }
+                            dual_inf = !block_any<T2>(viol, L.flag);
+                        }
                     }
                     if (prim_ok && dual_ok) {
                         st = MPCQP_SOLVED_;
