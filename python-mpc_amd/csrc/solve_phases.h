@@ -169,10 +169,14 @@ __device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restri
             }
             if (h == ph) v[pj] = i == p ? 1.0 : -cd;
         };
-        // all 32 pivots: an early exit at npiv breaks the unrolled schedule (measured: cfg 2
-        // Gauss-Jordan 227 k -> 297 k cycles on the slowest instance despite 19 % fewer pivots)
+        // the padding pivots (p >= npiv) are skipped by a uniform branch around each unrolled
+        // step (an early exit out of the loop broke the unrolled schedule: cfg 2
+        // Gauss-Jordan 227 k -> 297 k cycles on the slowest instance).  Skipping one leaves
+        // its identity row / column as they are, up to the sign of the zeros the step
+        // would have written (-0.0 for +0.0 in padded entries, never read as nonzero).
 #pragma unroll
-        for (int p = 0; p < S; ++p) pivot_br(p, p & 15);
+        for (int p = 0; p < S; ++p)
+            if (p < npiv) pivot_br(p, p & 15);
     }
 #pragma unroll
     for (int jj = 0; jj < 16; jj += 2) {
