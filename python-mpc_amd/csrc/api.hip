@@ -108,7 +108,7 @@ int upload_plan(const Plan& pl, Shard& s) {
     std::vector<const std::vector<int>*> parts = {
         &pl.pad_var, &pl.acsc_ptr, &pl.acsc_row, &pl.acsc_v, &pl.acsr_ptr, &pl.acsr_col, &pl.acsr_v,
         &pl.psym_ptr, &pl.psym_col, &pl.psym_v, &pl.p_r, &pl.p_c, &pl.a_r, &pl.a_c,
-        &pl.asm_blk_ptr, &pl.asm_tgt, &pl.tterm, &pl.acsr_pos, &pl.gcol, &pl.grow, &pl.gpsym, &pl.toff, &pl.bsize};
+        &pl.asm_blk_ptr, &pl.asm_tgt, &pl.tterm, &pl.acsr_pos, &pl.gcol, &pl.grow, &pl.gpsym, &pl.toff, &pl.bsize, &pl.tcnt};
     std::vector<size_t> offs;
     std::vector<int> flat;
     for (auto* v : parts) {
@@ -122,7 +122,7 @@ int upload_plan(const Plan& pl, Shard& s) {
                          &s.kp.acsr_col, &s.kp.acsr_v, &s.kp.psym_ptr, &s.kp.psym_col, &s.kp.psym_v,
                          &s.kp.p_r, &s.kp.p_c, &s.kp.a_r, &s.kp.a_c, &s.kp.asm_blk_ptr, &s.kp.asm_tgt,
                          &s.kp.tterm, &s.kp.acsr_pos,
-                         &s.kp.gcol, &s.kp.grow, &s.kp.gpsym, &s.kp.toff, &s.kp.bsize};
+                         &s.kp.gcol, &s.kp.grow, &s.kp.gpsym, &s.kp.toff, &s.kp.bsize, &s.kp.tcnt};
     for (size_t i = 0; i < parts.size(); ++i) *dst[i] = s.dplan + offs[i];
     return 0;
 }

@@ -38,6 +38,7 @@ struct KParams {
     const int *psym_ptr, *psym_col, *psym_v, *p_r, *p_c, *a_r, *a_c;
     const int *asm_blk_ptr, *asm_tgt, *tterm, *acsr_pos, *gcol, *grow, *gpsym, *toff;
     const int* bsize;  // [nb] real variables of each block (the rest of its 32 are padding, at the end)
+    const int* tcnt;   // [ntgt] assembly terms per target, descending within a block (plan.cpp)
     // workspace
     double *Px, *Ax, *q, *D, *l, *u, *E, *x, *z, *y, *scal, *F, *H, *Si, *dyc, *dxc;
     double *obj, *pri, *dua, *rho_est;

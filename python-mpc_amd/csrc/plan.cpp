@@ -222,6 +222,28 @@ std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const
         t = u;
     }
     for (int k = 0; k < pl.nb; ++k) pl.asm_blk_ptr[k + 1] += pl.asm_blk_ptr[k];
+    // within a block, targets by descending term count (stable): the kernels' assembly
+    // loops run a wave's targets for the count of its first one (tcnt), not term_max
+    // (cfg 2: 720 of 984 targets have a single term, term_max is 6).  Each target's terms
+    // keep their order, so the sums are unchanged.
+    {
+        std::vector<int> tg2, tp2{0}, ta2, tb2, tr2;
+        for (int k = 0; k < pl.nb; ++k) {
+            std::vector<int> ord;
+            for (int t = pl.asm_blk_ptr[k]; t < pl.asm_blk_ptr[k + 1]; ++t) ord.push_back(t);
+            auto cnt = [&](int t) { return pl.asm_term_ptr[t + 1] - pl.asm_term_ptr[t]; };
+            std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return cnt(x) > cnt(y); });
+            for (int t : ord) {
+                tg2.push_back(pl.asm_tgt[t]);
+                for (int u = pl.asm_term_ptr[t]; u < pl.asm_term_ptr[t + 1]; ++u) {
+                    ta2.push_back(pl.term_a[u]); tb2.push_back(pl.term_b[u]); tr2.push_back(pl.term_r[u]);
+                }
+                tp2.push_back((int)ta2.size());
+            }
+        }
+        pl.asm_tgt.swap(tg2); pl.asm_term_ptr.swap(tp2);
+        pl.term_a.swap(ta2); pl.term_b.swap(tb2); pl.term_r.swap(tr2);
+    }
     // A-pair terms address A values by their position in the padded-CSC order
     // (the order the solve kernel keeps them in LDS)
     std::vector<int> csc_pos(pl.nnzA);
@@ -233,7 +255,11 @@ std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const
     // (nnzA | nnzA << 16, 0) -- Acsc[nnzA] is the kernels' zero slot
     pl.ntgt = (int)pl.asm_tgt.size();
     pl.term_max = 0;
-    for (int t = 0; t < pl.ntgt; ++t) pl.term_max = std::max(pl.term_max, pl.asm_term_ptr[t + 1] - pl.asm_term_ptr[t]);
+    pl.tcnt.resize(pl.ntgt);
+    for (int t = 0; t < pl.ntgt; ++t) {
+        pl.tcnt[t] = pl.asm_term_ptr[t + 1] - pl.asm_term_ptr[t];
+        pl.term_max = std::max(pl.term_max, pl.tcnt[t]);
+    }
     pl.tterm.assign((size_t)2 * pl.ntgt * pl.term_max, 0);
     for (int t = 0; t < pl.ntgt; ++t)
         for (int j = 0; j < pl.term_max; ++j) {

@@ -46,6 +46,7 @@ struct Plan {
     // the same terms, padded to term_max per target, in ELL order (see plan.cpp)
     int ntgt = 0, term_max = 0;
     std::vector<int> tterm;
+    std::vector<int> tcnt;        // [ntgt] terms of each target (descending within a block)
     std::vector<int> csc_pos;     // [nnzA] user value index -> padded-CSC position
     std::vector<int> acsr_pos;    // [nnzA] CSR entry -> padded-CSC position of its value
     int max_level = 0;            // largest BFS level (diagnostic)

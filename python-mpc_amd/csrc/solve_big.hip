@@ -60,7 +60,7 @@ __device__ __forceinline__ bool factorize2(const KP& p, SLds& L, double* __restr
     constexpr int HT = TT / 2;      // threads per chain
     constexpr int NF = 16 * S / HT;  // per-thread F / G buffer (amax, bmax <= 16)
     const int tid = threadIdx.x, half = tid / HT, u = tid % HT;
-    const int nb = p.nb, amax = p.amax, bmax = p.bmax, pm = p.pmeet, ntgt = p.ntgt, tmax = p.term_max;
+    const int nb = p.nb, amax = p.amax, bmax = p.bmax, pm = p.pmeet, ntgt = p.ntgt;
     const int nst = max(pm, nb - 1 - pm);
     const int2* __restrict__ tt = (const int2*)p.tterm;
     double *SP = L.SP, *DK = L.DK, *EK = L.EK;                                   // top chain
@@ -84,8 +84,9 @@ __device__ __forceinline__ bool factorize2(const KP& p, SLds& L, double* __restr
 #pragma unroll 1
         for (int t = p.asm_blk_ptr[k] + t0; t < p.asm_blk_ptr[k + 1]; t += stride) {
             double acc = 0.0;
+            const int tn = p.tcnt[__builtin_amdgcn_readfirstlane(t)];  // the wave's largest count
 #pragma unroll 4
-            for (int j = 0; j < tmax; ++j) {
+            for (int j = 0; j < tn; ++j) {
                 const int2 w = tt[(long)j * ntgt + t];
                 const int a = w.x & 0xFFFF, bb = (int)((unsigned)w.x >> 16), r = w.y;
                 acc += r < 0 ? L.Pv[a] : rho_of(L.ct[r], rho) * L.Acsc[a] * L.Acsc[bb];

@@ -187,6 +187,214 @@ __device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restri
     return minpiv > 0.0;
 }
 
+// Gauss-Jordan of one tile in two segments, by one wave, in place (the two-wave
+// kernel's factorisation, factorize_w2).  S_k = D_k - F_k E_k' differs from the
+// assembled D_k only in the corner [0, a)^2 of its coupling rows (E_k has a nonzero
+// rows), and a pivot step changes an unpivoted entry by terms that do not involve it.
+// So SEG 1 pivots rows [a, npiv) of D_k before S_{k-1}^{-1} exists -- its unpivoted
+// corner is then the Schur complement of D_k onto the coupling rows -- and SEG 2, once
+// F_k is known, adds the correction dl (a x a, row stride 8: -F_k E_k') to that corner
+// and pivots rows [0, a); the tile then holds S_k^{-1}.  SEG 1 with a = 0 is the whole
+// inverse in gj_wave's natural order.  The step is gj_wave's divergent unrolled one; the
+// pivot order only changes which rows count as pivoted in the sign rule M_ij = -M_ji.
+// Between the segments T holds true values (sc = 1 on entry).  buf: 2 S doubles.
+template <int SEG>
+__device__ __forceinline__ bool gj_seg(double* __restrict__ T, double* __restrict__ buf, const int a, const int npiv,
+                                       const double* __restrict__ dl) {
+    const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
+    double v[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; jj += 2) {
+        const double2 t2 = *(const double2*)(T + i * S + 16 * h + jj);
+        v[jj] = t2.x;
+        v[jj + 1] = t2.y;
+    }
+    if (SEG == 2 && h == 0 && i < a) {
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj)
+            if (jj < a) v[jj] += dl[i * 8 + jj];
+    }
+    double minpiv = 1.0, sc = 1.0, iv = 1.0;
+    auto step = [&](const int p, const int pj, const bool pv) __attribute__((always_inline)) {
+        const int ph = p >> 4;
+        double* rb = buf + (pj & 1) * S;
+        if (h == ph) {
+            const double vp = sc * v[pj];
+            rb[i] = pv ? -vp : vp;  // row p = +-column p
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double rowv[16];
+#pragma unroll
+        for (int jj = 0; jj < 16; jj += 2) {
+            const double2 r2 = *(const double2*)(rb + 16 * h + jj);
+            rowv[jj] = r2.x;
+            rowv[jj + 1] = r2.y;
+        }
+        const double piv = rb[p];
+        const double mi = rb[i];
+        const double colv = pv ? -mi : mi;
+        minpiv = piv > 0.0 ? minpiv : -1.0;
+        double d = __builtin_amdgcn_rcp(piv);
+        d = __builtin_fma(d, __builtin_fma(-piv, d, 1.0), d);
+        d = __builtin_fma(d, __builtin_fma(-piv, d, 1.0), d);
+        const double cd = (colv * d) * iv;
+        if (i != p) {
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) v[jj] = __builtin_fma(-cd, rowv[jj], v[jj]);
+        } else {
+            sc = d;
+            iv = piv;
+        }
+        if (h == ph) v[pj] = i == p ? 1.0 : -cd;
+    };
+    if constexpr (SEG == 1) {
+#pragma unroll
+        for (int p = 0; p < S; ++p)
+            if (p >= a && p < npiv) step(p, p & 15, i >= a && i < p);
+    } else {
+        const bool done = i >= a && i < npiv;  // pivoted in SEG 1
+#pragma unroll
+        for (int p = 0; p < 8; ++p)
+            if (p < a) step(p, p, done || i < p);
+    }
+#pragma unroll
+    for (int jj = 0; jj < 16; jj += 2) *(double2*)(T + i * S + 16 * h + jj) = make_double2(sc * v[jj], sc * v[jj + 1]);
+    return minpiv > 0.0;
+}
+
+// Assembly of block k's D_k (sigma I + the plan's terms) and E_k (rows < amax) by the
+// threads t0, t0 + nt, ...; sync() orders the zeroing before the targets' sums.
+// POL: the polish system's row weights (factorize's comment).
+template <bool POL, class KP, class Sync>
+__device__ __forceinline__ void assemble_block(const KP& p, const SLds& L, const double rho, const int k,
+                                               double* __restrict__ D, double* __restrict__ E, const int t0,
+                                               const int nt, Sync sync) {
+    const int amax = p.amax, ntgt = p.ntgt;
+    const int2* __restrict__ tt = (const int2*)p.tterm;
+    for (int e = 2 * t0; e < SS; e += 2 * nt) *(double2*)(D + e) = make_double2(0.0, 0.0);
+    for (int e = 2 * t0; e < amax * S; e += 2 * nt) *(double2*)(E + e) = make_double2(0.0, 0.0);
+    sync();
+    if (t0 < S) D[t0 * S + t0] = p.pad_var[k * S + t0] >= 0 ? (POL ? p.delta : p.sigma) : 1.0;
+    sync();
+    // every target has one owner: its terms are summed in plan order
+#pragma unroll 1
+    for (int t = p.asm_blk_ptr[k] + t0; t < p.asm_blk_ptr[k + 1]; t += nt) {
+        double acc = 0.0;
+        // the wave's first target has the most terms (plan order); the rest pad with zeros
+        const int tn = p.tcnt[__builtin_amdgcn_readfirstlane(t)];
+#pragma unroll 4
+        for (int j = 0; j < tn; ++j) {
+            const int2 w = tt[(long)j * ntgt + t];
+            const int a = w.x & 0xFFFF, bb = (int)((unsigned)w.x >> 16), r = w.y;
+            const double wr = POL ? (double)((L.ct[r] & 1) + ((L.ct[r] >> 1) & 1)) * rho : rho_of(L.ct[r], rho);
+            acc += r < 0 ? L.Pv[a] : wr * L.Acsc[a] * L.Acsc[bb];
+        }
+        const int tg = p.asm_tgt[t];
+        if (tg < SS) D[tg] += acc;
+        else E[tg - SS] += acc;
+    }
+}
+
+// The two-wave kernel's factorisation (mode 2, nb = 4, amax <= 8; TT = 128), with the
+// Gauss-Jordan pivots that do not wait for the previous block taken off the critical
+// path (gj_seg):
+//   stage 1, the waves in parallel: wave 0 assembles D_0 and inverts it whole, then
+//     assembles D_2 and pivots its rows [amax, 32); wave 1 does the same for D_1, D_3;
+//   then for k = 1..3:  F_k = E_k S_{k-1}^{-1} (G_{k,k-1} = -F_k), the corner correction
+//     -F_k E_k' and the blocks G_kj = -F_k G_{k-1,j} (j < k-1) from LDS, then wave 0
+//     pivots rows [0, amax) of S_k (gj_seg<2>).
+// The critical path is 32 + 3 amax pivot steps instead of 4 x 32.  Outputs as mode 2 of
+// factorize: S_k^{-1} in Sg (LDS here), G_kj in Hg at pair k(k-1)/2 + j.
+template <class KP>
+__device__ __forceinline__ bool factorize_w2(const KP& p, SLds& L, const double rho, double* __restrict__ Hg,
+                                             double* __restrict__ Sg) {
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int amax = p.amax, as = amax * S;
+    const long gstride = (long)amax * S;
+    // scratch in the aliased vector region: E_0..E_3, F_1..F_3, G_20, the corner, the buffers
+    double* const V = L.SP;
+    double* const G20 = V + 7 * as;
+    double* const dl = V + 8 * as;            // amax x amax, row stride 8
+    double* const bufw = dl + 64 + w * 2 * S;  // the wave's Gauss-Jordan publish buffers
+    double* const okf = dl + 64 + 4 * S;
+    auto Ek = [&](int k) __attribute__((always_inline)) { return V + k * as; };
+    auto Fk = [&](int k) __attribute__((always_inline)) { return V + (3 + k) * as; };
+    auto wave_sync = []() __attribute__((always_inline)) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+#ifdef MPCQP_PHASE_PROF
+    long long tf = clock64();
+#define FPH(k) if (tid == 0) { const long long t_ = clock64(); L.pacc[k] += t_ - tf; tf = t_; }
+#else
+#define FPH(k)
+#endif
+    bool okw = true;
+#pragma unroll 1
+    for (int s = 0; s < 2; ++s) {
+        const int k = w + 2 * s;
+        assemble_block<false>(p, L, rho, k, Sg + (long)k * SS, Ek(k), lane, 64, wave_sync);
+        wave_sync();
+        FPH(8)
+        okw = gj_seg<1>(Sg + (long)k * SS, bufw, k ? amax : 0, p.bsize[k], nullptr) && okw;
+        FPH(10)
+    }
+    __syncthreads();
+    FPH(11)
+#pragma unroll 1
+    for (int k = 1; k < 4; ++k) {
+        const double* Sp = Sg + (long)(k - 1) * SS;
+        const double* E = Ek(k);
+        double* F = Fk(k);
+        for (int o = tid; o < as; o += 128) {
+            const int r = o >> 5, j = o & (S - 1);
+            double sacc = 0.0;
+#pragma unroll 8
+            for (int l = 0; l < S; ++l) sacc += E[r * S + l] * Sp[l * S + j];
+            F[o] = sacc;
+            Hg[(long)(k * (k - 1) / 2 + k - 1) * gstride + o] = -sacc;
+        }
+        __syncthreads();
+        if (tid < amax * amax) {  // S_k = D_k - F_k E_k' on the corner
+            const int r = tid / amax, c = tid - r * amax;
+            double sacc = 0.0;
+#pragma unroll 8
+            for (int l = 0; l < S; ++l) sacc += F[r * S + l] * E[c * S + l];
+            dl[r * 8 + c] = -sacc;
+        }
+        // G_kj = -F_k G_{k-1,j}: G_{k-1,k-2} = -F_{k-1}; G_{2,0} kept in LDS for k = 3
+#pragma unroll 1
+        for (int j = 0; j < k - 1; ++j) {
+            const bool adj = j == k - 2;
+            const double* Gp = adj ? Fk(k - 1) : G20;
+            const double sg = adj ? 1.0 : -1.0;  // G_kj = sg * F_k Gp
+            for (int o = tid; o < as; o += 128) {
+                const int r = o >> 5, c = o & (S - 1);
+                double sacc = 0.0;
+#pragma unroll
+                for (int l = 0; l < 8; ++l)
+                    if (l < amax) sacc += F[r * S + l] * Gp[l * S + c];
+                const double g = sg * sacc;
+                Hg[(long)(k * (k - 1) / 2 + j) * gstride + o] = g;
+                if (k == 2) G20[o] = g;
+            }
+        }
+        __syncthreads();
+        FPH(9)
+        if (w == 0) okw = gj_seg<2>(Sg + (long)k * SS, bufw, amax, p.bsize[k], dl) && okw;
+        __syncthreads();
+        FPH(11)
+    }
+    if (lane == 0) okf[w] = okw ? 1.0 : 0.0;
+    __syncthreads();
+    FPH(9)
+#undef FPH
+    return okf[0] > 0.5 && okf[1] > 0.5;
+}
+
 // Assemble K's tiles for the current rho and factor them (block LDL'):
 //   S_0 = D_0,  F_k = E_k S_{k-1}^{-1},  S_k = D_k - F_k E_k',  H_{k-1} = F_k'
 // E_k is nonzero only in its first amax rows (block k's first BFS level), so F_k
@@ -206,10 +414,12 @@ __device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restri
 template <int TT, class KP, bool POL = false>
 __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, double* __restrict__ Fg,
                                           double* __restrict__ Hg, double* __restrict__ Sg) {
+    if constexpr (TT == 128 && !POL) {  // the two-wave kernel (variant 10: nb = 4, amax <= 8)
+        if (p.mode == 2 && p.nb == 4 && p.amax <= 8) return factorize_w2(p, L, rho, Hg, Sg);
+    }
     const int tid = threadIdx.x;
-    const int nb = p.nb, amax = p.amax, ntgt = p.ntgt, tmax = p.term_max, mode = POL ? 1 : p.mode;
+    const int nb = p.nb, amax = p.amax, mode = POL ? 1 : p.mode;
     const long gstride = (long)amax * S;
-    const int2* __restrict__ tt = (const int2*)p.tterm;
     bool ok = true;
     double* SP = L.SP;
     double* DK = L.DK;
@@ -220,30 +430,9 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
 #else
 #define FPH(k)
 #endif
-    // Assembly of block k's D_k (sigma I + the plan's terms) and E_k (rows < amax) by the
-    // threads t0, t0 + nt, ...; sync() orders the zeroing before the targets' sums.
     auto assemble = [&](const int k, double* __restrict__ D, double* __restrict__ E, const int t0, const int nt,
                         auto sync) __attribute__((always_inline)) {
-        for (int e = 2 * t0; e < SS; e += 2 * nt) *(double2*)(D + e) = make_double2(0.0, 0.0);
-        for (int e = 2 * t0; e < amax * S; e += 2 * nt) *(double2*)(E + e) = make_double2(0.0, 0.0);
-        sync();
-        if (t0 < S) D[t0 * S + t0] = p.pad_var[k * S + t0] >= 0 ? (POL ? p.delta : p.sigma) : 1.0;
-        sync();
-        // every target has one owner: its terms are summed in plan order
-#pragma unroll 1
-        for (int t = p.asm_blk_ptr[k] + t0; t < p.asm_blk_ptr[k + 1]; t += nt) {
-            double acc = 0.0;
-#pragma unroll 4
-            for (int j = 0; j < tmax; ++j) {
-                const int2 w = tt[(long)j * ntgt + t];
-                const int a = w.x & 0xFFFF, bb = (int)((unsigned)w.x >> 16), r = w.y;
-                const double wr = POL ? (double)((L.ct[r] & 1) + ((L.ct[r] >> 1) & 1)) * rho : rho_of(L.ct[r], rho);
-                acc += r < 0 ? L.Pv[a] : wr * L.Acsc[a] * L.Acsc[bb];
-            }
-            const int tg = p.asm_tgt[t];
-            if (tg < SS) D[tg] += acc;
-            else E[tg - SS] += acc;
-        }
+        assemble_block<POL>(p, L, rho, k, D, E, t0, nt, sync);
     };
     auto block_sync = []() __attribute__((always_inline)) { __syncthreads(); };
     auto wave_sync = []() __attribute__((always_inline)) {
