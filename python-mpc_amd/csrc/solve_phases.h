@@ -267,7 +267,7 @@ __device__ __forceinline__ bool gj_seg(double* __restrict__ T, double* __restric
 // Assembly of block k's D_k (sigma I + the plan's terms) and E_k (rows < amax) by the
 // threads t0, t0 + nt, ...; sync() orders the zeroing before the targets' sums.
 // POL: the polish system's row weights (factorize's comment).
-template <bool POL, class KP, class Sync>
+template <bool POL, bool DEEP, class KP, class Sync>
 __device__ __forceinline__ void assemble_block(const KP& p, const SLds& L, const double rho, const int k,
                                                double* __restrict__ D, double* __restrict__ E, const int t0,
                                                const int nt, Sync sync) {
@@ -278,22 +278,77 @@ __device__ __forceinline__ void assemble_block(const KP& p, const SLds& L, const
     sync();
     if (t0 < S) D[t0 * S + t0] = p.pad_var[k * S + t0] >= 0 ? (POL ? p.delta : p.sigma) : 1.0;
     sync();
-    // every target has one owner: its terms are summed in plan order
-#pragma unroll 1
-    for (int t = p.asm_blk_ptr[k] + t0; t < p.asm_blk_ptr[k + 1]; t += nt) {
-        double acc = 0.0;
-        // the wave's first target has the most terms (plan order); the rest pad with zeros
-        const int tn = p.tcnt[__builtin_amdgcn_readfirstlane(t)];
-#pragma unroll 4
-        for (int j = 0; j < tn; ++j) {
-            const int2 w = tt[(long)j * ntgt + t];
-            const int a = w.x & 0xFFFF, bb = (int)((unsigned)w.x >> 16), r = w.y;
-            const double wr = POL ? (double)((L.ct[r] & 1) + ((L.ct[r] >> 1) & 1)) * rho : rho_of(L.ct[r], rho);
-            acc += r < 0 ? L.Pv[a] : wr * L.Acsc[a] * L.Acsc[bb];
-        }
-        const int tg = p.asm_tgt[t];
+    // every target has one owner: its terms are summed in plan order.  The wave's first
+    // target has the most terms (plan order); the others pad with zero terms to its count.
+    const int tb = p.asm_blk_ptr[k], te = p.asm_blk_ptr[k + 1], tmax = p.term_max;
+    if (te <= tb) return;
+    auto term = [&](const int2 w) __attribute__((always_inline)) {
+        const int a = w.x & 0xFFFF, bb = (int)((unsigned)w.x >> 16), r = w.y;
+        const double wr = POL ? (double)((L.ct[r] & 1) + ((L.ct[r] >> 1) & 1)) * rho : rho_of(L.ct[r], rho);
+        return r < 0 ? L.Pv[a] : wr * L.Acsc[a] * L.Acsc[bb];
+    };
+    auto add = [&](const int tg, const double acc) __attribute__((always_inline)) {
         if (tg < SS) D[tg] += acc;
         else E[tg - SS] += acc;
+    };
+    int t_rest = tb + t0;
+    if constexpr (DEEP) {
+        // The count, tile index and first term (the only one for most targets) of the
+        // lane's first NI targets, and the further terms of its first target (sorted
+        // first: the multi-term ones), are all loaded before any is summed, so the plan's
+        // L2 / MALL latency is paid about once per block instead of once per target
+        // (two-wave kernel; the extra registers cost the 256-thread kernels' solve loops).
+        constexpr int NI = 8, TJ = 6;
+        int tn[NI], tg[NI];
+        int2 w0[NI], wj[TJ];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int tc = min(tb + t0 + i * nt, te - 1);
+            tn[i] = p.tcnt[__builtin_amdgcn_readfirstlane(tc)];
+            tg[i] = p.asm_tgt[tc];
+            w0[i] = tt[tc];
+        }
+        const int tc0 = min(tb + t0, te - 1);
+#pragma unroll
+        for (int j = 1; j < TJ; ++j) wj[j] = tt[(long)min(j, tmax - 1) * ntgt + tc0];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int t = tb + t0 + i * nt;
+            if (t < te) {
+                double acc = 0.0;
+                acc += term(w0[i]);
+                if (i == 0) {
+#pragma unroll
+                    for (int j = 1; j < TJ; ++j)
+                        if (j < tn[0]) acc += term(wj[j]);
+#pragma unroll 1
+                    for (int j = TJ; j < tn[0]; ++j) acc += term(tt[(long)j * ntgt + t]);
+                } else {
+#pragma unroll 1
+                    for (int j = 1; j < tn[i]; ++j) acc += term(tt[(long)j * ntgt + t]);
+                }
+                add(tg[i], acc);
+            }
+        }
+        t_rest = tb + t0 + NI * nt;
+    }
+    // the (remaining) targets one at a time, the next one's plan loads in flight while
+    // the current one is summed
+    if (t_rest >= te) return;
+    int t = t_rest, tc = min(t, te - 1);
+    int tn = p.tcnt[__builtin_amdgcn_readfirstlane(tc)], tg = p.asm_tgt[tc];
+    int2 w0 = tt[tc];
+#pragma unroll 1
+    for (; t < te; t += nt) {
+        const int tcn = min(t + nt, te - 1);
+        const int tn_n = p.tcnt[__builtin_amdgcn_readfirstlane(tcn)], tg_n = p.asm_tgt[tcn];
+        const int2 w0_n = tt[tcn];
+        double acc = 0.0;
+        acc += term(w0);
+#pragma unroll 2
+        for (int j = 1; j < tn; ++j) acc += term(tt[(long)j * ntgt + t]);
+        add(tg, acc);
+        tn = tn_n; tg = tg_n; w0 = w0_n;
     }
 }
 
@@ -336,7 +391,7 @@ __device__ __forceinline__ bool factorize_w2(const KP& p, SLds& L, const double 
 #pragma unroll 1
     for (int s = 0; s < 2; ++s) {
         const int k = w + 2 * s;
-        assemble_block<false>(p, L, rho, k, Sg + (long)k * SS, Ek(k), lane, 64, wave_sync);
+        assemble_block<false, true>(p, L, rho, k, Sg + (long)k * SS, Ek(k), lane, 64, wave_sync);
         wave_sync();
         FPH(8)
         okw = gj_seg<1>(Sg + (long)k * SS, bufw, k ? amax : 0, p.bsize[k], nullptr) && okw;
@@ -349,11 +404,14 @@ __device__ __forceinline__ bool factorize_w2(const KP& p, SLds& L, const double 
         const double* Sp = Sg + (long)(k - 1) * SS;
         const double* E = Ek(k);
         double* F = Fk(k);
+        // E_k's nonzero columns are [l0, l0 + bmax) of block k-1 (plan toff / bmax): the
+        // products skip its zero columns (same sums, in the same order)
+        const int l0 = p.toff[k - 1], bmax = p.bmax;
         for (int o = tid; o < as; o += 128) {
             const int r = o >> 5, j = o & (S - 1);
             double sacc = 0.0;
-#pragma unroll 8
-            for (int l = 0; l < S; ++l) sacc += E[r * S + l] * Sp[l * S + j];
+#pragma unroll 4
+            for (int l = l0; l < l0 + bmax; ++l) sacc += E[r * S + l] * Sp[l * S + j];
             F[o] = sacc;
             Hg[(long)(k * (k - 1) / 2 + k - 1) * gstride + o] = -sacc;
         }
@@ -361,8 +419,8 @@ __device__ __forceinline__ bool factorize_w2(const KP& p, SLds& L, const double 
         if (tid < amax * amax) {  // S_k = D_k - F_k E_k' on the corner
             const int r = tid / amax, c = tid - r * amax;
             double sacc = 0.0;
-#pragma unroll 8
-            for (int l = 0; l < S; ++l) sacc += F[r * S + l] * E[c * S + l];
+#pragma unroll 4
+            for (int l = l0; l < l0 + bmax; ++l) sacc += F[r * S + l] * E[c * S + l];
             dl[r * 8 + c] = -sacc;
         }
         // G_kj = -F_k G_{k-1,j}: G_{k-1,k-2} = -F_{k-1}; G_{2,0} kept in LDS for k = 3
@@ -432,7 +490,7 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
 #endif
     auto assemble = [&](const int k, double* __restrict__ D, double* __restrict__ E, const int t0, const int nt,
                         auto sync) __attribute__((always_inline)) {
-        assemble_block<POL>(p, L, rho, k, D, E, t0, nt, sync);
+        assemble_block<POL, false>(p, L, rho, k, D, E, t0, nt, sync);
     };
     auto block_sync = []() __attribute__((always_inline)) { __syncthreads(); };
     auto wave_sync = []() __attribute__((always_inline)) {
