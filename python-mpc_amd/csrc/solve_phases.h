@@ -187,18 +187,20 @@ __device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restri
     return minpiv > 0.0;
 }
 
-// Gauss-Jordan of one tile in two segments, by one wave, in place (the two-wave
-// kernel's factorisation, factorize_w2).  S_k = D_k - F_k E_k' differs from the
+// Gauss-Jordan of one tile in two segments, by one wave, in place (the split
+// factorisations factorize_w2 / factorize_g).  S_k = D_k - F_k E_k' differs from the
 // assembled D_k only in the corner [0, a)^2 of its coupling rows (E_k has a nonzero
 // rows), and a pivot step changes an unpivoted entry by terms that do not involve it.
 // So SEG 1 pivots rows [a, npiv) of D_k before S_{k-1}^{-1} exists -- its unpivoted
 // corner is then the Schur complement of D_k onto the coupling rows -- and SEG 2, once
-// F_k is known, adds the correction dl (a x a, row stride 8: -F_k E_k') to that corner
+// F_k is known, adds the correction dl (a x a, row stride 16: -F_k E_k') to that corner
 // and pivots rows [0, a); the tile then holds S_k^{-1}.  SEG 1 with a = 0 is the whole
-// inverse in gj_wave's natural order.  The step is gj_wave's divergent unrolled one; the
+// inverse in gj_wave's natural order.  The steps are gj_wave's (Compact: the rolled,
+// branch-free one with scalar-switch register picks, for the 256-thread kernels); the
 // pivot order only changes which rows count as pivoted in the sign rule M_ij = -M_ji.
-// Between the segments T holds true values (sc = 1 on entry).  buf: 2 S doubles.
-template <int SEG>
+// T (LDS or the workspace) holds true values between the segments (sc = 1 on entry).
+// buf: 2 S doubles of LDS.  a <= 16 (a <= 8 for the unrolled SEG 2).
+template <int SEG, bool Compact = false>
 __device__ __forceinline__ bool gj_seg(double* __restrict__ T, double* __restrict__ buf, const int a, const int npiv,
                                        const double* __restrict__ dl) {
     const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
@@ -211,20 +213,22 @@ __device__ __forceinline__ bool gj_seg(double* __restrict__ T, double* __restric
     }
     if (SEG == 2 && h == 0 && i < a) {
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj)
-            if (jj < a) v[jj] += dl[i * 8 + jj];
+        for (int jj = 0; jj < 16; ++jj)
+            if (jj < a) v[jj] += dl[i * 16 + jj];
     }
     double minpiv = 1.0, sc = 1.0, iv = 1.0;
     auto step = [&](const int p, const int pj, const bool pv) __attribute__((always_inline)) {
         const int ph = p >> 4;
         double* rb = buf + (pj & 1) * S;
         if (h == ph) {
-            const double vp = sc * v[pj];
+            const double vp = sc * (Compact ? pick16(v, pj) : v[pj]);
             rb[i] = pv ? -vp : vp;  // row p = +-column p
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const double piv = rb[p];
+        const double mi = rb[i];
         double rowv[16];
 #pragma unroll
         for (int jj = 0; jj < 16; jj += 2) {
@@ -232,24 +236,41 @@ __device__ __forceinline__ bool gj_seg(double* __restrict__ T, double* __restric
             rowv[jj] = r2.x;
             rowv[jj + 1] = r2.y;
         }
-        const double piv = rb[p];
-        const double mi = rb[i];
         const double colv = pv ? -mi : mi;
         minpiv = piv > 0.0 ? minpiv : -1.0;
         double d = __builtin_amdgcn_rcp(piv);
         d = __builtin_fma(d, __builtin_fma(-piv, d, 1.0), d);
         d = __builtin_fma(d, __builtin_fma(-piv, d, 1.0), d);
-        const double cd = (colv * d) * iv;
-        if (i != p) {
+        const bool self = i == p;
+        if constexpr (Compact) {
+            const double cd = self ? 0.0 : (colv * d) * iv;
 #pragma unroll
             for (int jj = 0; jj < 16; ++jj) v[jj] = __builtin_fma(-cd, rowv[jj], v[jj]);
+            sc = self ? d : sc;
+            iv = self ? piv : iv;
+            if (h == ph) put16(v, pj, self ? 1.0 : -cd);
         } else {
-            sc = d;
-            iv = piv;
+            const double cd = (colv * d) * iv;
+            if (!self) {
+#pragma unroll
+                for (int jj = 0; jj < 16; ++jj) v[jj] = __builtin_fma(-cd, rowv[jj], v[jj]);
+            } else {
+                sc = d;
+                iv = piv;
+            }
+            if (h == ph) v[pj] = self ? 1.0 : -cd;
         }
-        if (h == ph) v[pj] = i == p ? 1.0 : -cd;
     };
-    if constexpr (SEG == 1) {
+    if constexpr (Compact) {
+        if constexpr (SEG == 1) {
+#pragma unroll 1
+            for (int p = a; p < npiv; ++p) step(p, __builtin_amdgcn_readfirstlane(p & 15), i >= a && i < p);
+        } else {
+            const bool done = i >= a && i < npiv;
+#pragma unroll 1
+            for (int p = 0; p < a; ++p) step(p, __builtin_amdgcn_readfirstlane(p & 15), done || i < p);
+        }
+    } else if constexpr (SEG == 1) {
 #pragma unroll
         for (int p = 0; p < S; ++p)
             if (p >= a && p < npiv) step(p, p & 15, i >= a && i < p);
@@ -267,17 +288,32 @@ __device__ __forceinline__ bool gj_seg(double* __restrict__ T, double* __restric
 // Assembly of block k's D_k (sigma I + the plan's terms) and E_k (rows < amax) by the
 // threads t0, t0 + nt, ...; sync() orders the zeroing before the targets' sums.
 // POL: the polish system's row weights (factorize's comment).
+template <bool POL, bool DEEP, bool STORE, class KP>
+__device__ __forceinline__ void assemble_targets(const KP& p, const SLds& L, const double rho, const int k,
+                                                 double* __restrict__ D, double* __restrict__ E, const int t0,
+                                                 const int nt);
 template <bool POL, bool DEEP, class KP, class Sync>
 __device__ __forceinline__ void assemble_block(const KP& p, const SLds& L, const double rho, const int k,
                                                double* __restrict__ D, double* __restrict__ E, const int t0,
                                                const int nt, Sync sync) {
-    const int amax = p.amax, ntgt = p.ntgt;
-    const int2* __restrict__ tt = (const int2*)p.tterm;
+    const int amax = p.amax;
     for (int e = 2 * t0; e < SS; e += 2 * nt) *(double2*)(D + e) = make_double2(0.0, 0.0);
     for (int e = 2 * t0; e < amax * S; e += 2 * nt) *(double2*)(E + e) = make_double2(0.0, 0.0);
     sync();
     if (t0 < S) D[t0 * S + t0] = p.pad_var[k * S + t0] >= 0 ? (POL ? p.delta : p.sigma) : 1.0;
     sync();
+    assemble_targets<POL, DEEP, false>(p, L, rho, k, D, E, t0, nt);
+}
+
+// The targets' sums (assemble_block).  STORE: the tiles hold zeros and the diagonal
+// (sigma, or 1 on padding rows) already, and every target is written once as that
+// base value plus its sum (no read: the workspace tiles of factorize_g).
+template <bool POL, bool DEEP, bool STORE, class KP>
+__device__ __forceinline__ void assemble_targets(const KP& p, const SLds& L, const double rho, const int k,
+                                                 double* __restrict__ D, double* __restrict__ E, const int t0,
+                                                 const int nt) {
+    const int ntgt = p.ntgt;
+    const int2* __restrict__ tt = (const int2*)p.tterm;
     // every target has one owner: its terms are summed in plan order.  The wave's first
     // target has the most terms (plan order); the others pad with zero terms to its count.
     const int tb = p.asm_blk_ptr[k], te = p.asm_blk_ptr[k + 1], tmax = p.term_max;
@@ -288,8 +324,13 @@ __device__ __forceinline__ void assemble_block(const KP& p, const SLds& L, const
         return r < 0 ? L.Pv[a] : wr * L.Acsc[a] * L.Acsc[bb];
     };
     auto add = [&](const int tg, const double acc) __attribute__((always_inline)) {
-        if (tg < SS) D[tg] += acc;
-        else E[tg - SS] += acc;
+        if constexpr (STORE) {
+            if (tg < SS) D[tg] = ((tg >> 5) == (tg & (S - 1)) ? (POL ? p.delta : p.sigma) : 0.0) + acc;
+            else E[tg - SS] = 0.0 + acc;
+        } else {
+            if (tg < SS) D[tg] += acc;
+            else E[tg - SS] += acc;
+        }
     };
     int t_rest = tb + t0;
     if constexpr (DEEP) {
@@ -371,9 +412,9 @@ __device__ __forceinline__ bool factorize_w2(const KP& p, SLds& L, const double 
     // scratch in the aliased vector region: E_0..E_3, F_1..F_3, G_20, the corner, the buffers
     double* const V = L.SP;
     double* const G20 = V + 7 * as;
-    double* const dl = V + 8 * as;            // amax x amax, row stride 8
-    double* const bufw = dl + 64 + w * 2 * S;  // the wave's Gauss-Jordan publish buffers
-    double* const okf = dl + 64 + 4 * S;
+    double* const dl = V + 8 * as;             // amax x amax, row stride 16
+    double* const bufw = dl + 256 + w * 2 * S;  // the wave's Gauss-Jordan publish buffers
+    double* const okf = dl + 256 + 4 * S;
     auto Ek = [&](int k) __attribute__((always_inline)) { return V + k * as; };
     auto Fk = [&](int k) __attribute__((always_inline)) { return V + (3 + k) * as; };
     auto wave_sync = []() __attribute__((always_inline)) {
@@ -421,7 +462,7 @@ __device__ __forceinline__ bool factorize_w2(const KP& p, SLds& L, const double 
             double sacc = 0.0;
 #pragma unroll 4
             for (int l = l0; l < l0 + bmax; ++l) sacc += F[r * S + l] * E[c * S + l];
-            dl[r * 8 + c] = -sacc;
+            dl[r * 16 + c] = -sacc;
         }
         // G_kj = -F_k G_{k-1,j}: G_{k-1,k-2} = -F_{k-1}; G_{2,0} kept in LDS for k = 3
 #pragma unroll 1
@@ -453,6 +494,98 @@ __device__ __forceinline__ bool factorize_w2(const KP& p, SLds& L, const double 
     return okf[0] > 0.5 && okf[1] > 0.5;
 }
 
+// The 256-thread register-sweep kernels' factorisation (mode 1: F_k rows < amax and
+// S_k^{-1} to the workspace; amax <= 16), split like factorize_w2 but on workspace
+// tiles, since their LDS has no room for a tile per wave:
+//   stage 1, the four waves in parallel: wave w takes blocks k = w, w + 4, ...: fills
+//     D_k (zeros, the diagonal) and E_k in the workspace (Sg[k], Fg[k] rows < amax),
+//     writes every target once, and pivots rows [a_k, 32) of D_k in place (gj_seg<1>,
+//     a_0 = 0: block 0 whole);
+//   then for k = 1..nb-1: F_k = E_k S_{k-1}^{-1} (over E_k's nonzero columns) -> LDS,
+//     the corner correction -F_k E_k', F_k -> Fg[k] (waves 1-3) while wave 0 pivots
+//     rows [0, amax) of S_k (gj_seg<2>).
+// The Gauss-Jordan critical path is 32 + (nb - 1) amax pivot steps instead of 32 nb,
+// and the assembly runs on four waves at once.  Same outputs as factorize's mode 1.
+template <class KP>
+__device__ __forceinline__ bool factorize_g(const KP& p, SLds& L, const double rho, double* __restrict__ Fg,
+                                            double* __restrict__ Sg) {
+    constexpr int TT = 256;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int nb = p.nb, amax = p.amax, as = amax * S;
+    double* const V = L.SP;                    // LDS scratch (aliases the iteration vectors)
+    double* const Fl = V;                      // F_k, amax x 32 (<= 512)
+    double* const dl = V + 512;                // corner correction, row stride 16
+    double* const bufw = V + 768 + w * 2 * S;  // the wave's Gauss-Jordan publish buffers
+    double* const okf = V + 1024;
+    auto gsync = []() __attribute__((always_inline)) {  // the wave's workspace stores before its loads
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    };
+#ifdef MPCQP_PHASE_PROF
+    long long tf = clock64();
+#define FPH(k) if (tid == 0) { const long long t_ = clock64(); L.pacc[k] += t_ - tf; tf = t_; }
+#else
+#define FPH(k)
+#endif
+    bool okw = true;
+#pragma unroll 1
+    for (int k = w; k < nb; k += 4) {
+        double* D = Sg + (long)k * SS;
+        double* E = Fg + (long)k * SS;
+        for (int e = 2 * lane; e < SS; e += 128) {
+            const int r = e >> 5, c = e & (S - 1);  // c even: the diagonal is (r, r)
+            const double dg = p.pad_var[k * S + r] >= 0 ? p.sigma : 1.0;
+            *(double2*)(D + e) = make_double2(c == r ? dg : 0.0, c + 1 == r ? dg : 0.0);
+        }
+        for (int e = 2 * lane; e < as; e += 128) *(double2*)(E + e) = make_double2(0.0, 0.0);
+        gsync();
+        assemble_targets<false, false, true>(p, L, rho, k, D, E, lane, 64);
+        gsync();
+        FPH(8)
+        okw = gj_seg<1, true>(D, bufw, k ? amax : 0, p.bsize[k], nullptr) && okw;
+        FPH(10)
+    }
+    __syncthreads();
+    FPH(11)
+    const int bmax = p.bmax;
+#pragma unroll 1
+    for (int k = 1; k < nb; ++k) {
+        const double* Sp = Sg + (long)(k - 1) * SS;
+        const double* E = Fg + (long)k * SS;
+        const int l0 = p.toff[k - 1];
+        for (int o = tid; o < as; o += TT) {
+            const int r = o >> 5, j = o & (S - 1);
+            double sacc = 0.0;
+#pragma unroll 4
+            for (int l = l0; l < l0 + bmax; ++l) sacc += E[r * S + l] * Sp[l * S + j];
+            Fl[o] = sacc;
+        }
+        __syncthreads();
+        if (tid < amax * amax) {  // S_k = D_k - F_k E_k' on the corner
+            const int r = tid / amax, c = tid - r * amax;
+            double sacc = 0.0;
+#pragma unroll 4
+            for (int l = l0; l < l0 + bmax; ++l) sacc += Fl[r * S + l] * E[c * S + l];
+            dl[r * 16 + c] = -sacc;
+        }
+        __syncthreads();
+        FPH(9)
+        if (w == 0) {
+            okw = gj_seg<2, true>(Sg + (long)k * SS, bufw, amax, p.bsize[k], dl) && okw;
+        } else {
+            for (int o = tid - 64; o < as; o += TT - 64) Fg[(long)k * SS + o] = Fl[o];
+        }
+        __syncthreads();
+        FPH(11)
+    }
+    if (lane == 0) okf[w] = okw ? 1.0 : 0.0;
+    __syncthreads();
+    FPH(9)
+#undef FPH
+    return okf[0] > 0.5 && okf[1] > 0.5 && okf[2] > 0.5 && okf[3] > 0.5;
+}
+
 // Assemble K's tiles for the current rho and factor them (block LDL'):
 //   S_0 = D_0,  F_k = E_k S_{k-1}^{-1},  S_k = D_k - F_k E_k',  H_{k-1} = F_k'
 // E_k is nonzero only in its first amax rows (block k's first BFS level), so F_k
@@ -474,6 +607,9 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
                                           double* __restrict__ Hg, double* __restrict__ Sg) {
     if constexpr (TT == 128 && !POL) {  // the two-wave kernel (variant 10: nb = 4, amax <= 8)
         if (p.mode == 2 && p.nb == 4 && p.amax <= 8) return factorize_w2(p, L, rho, Hg, Sg);
+    }
+    if constexpr (TT == 256 && !POL) {  // the register-sweep kernels (variants 1-3)
+        if (p.mode == 1 && p.amax <= 16) return factorize_g(p, L, rho, Fg, Sg);
     }
     const int tid = threadIdx.x;
     const int nb = p.nb, amax = p.amax, mode = POL ? 1 : p.mode;
