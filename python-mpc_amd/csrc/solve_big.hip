@@ -280,18 +280,19 @@ __device__ __forceinline__ double dot4c(const double (&a)[4], const double (&v)[
     return (a[0] * v[0] + a[1] * v[1]) + (a[2] * v[2] + a[3] * v[3]);
 }
 
-// xt = K^{-1} rb.  rb is read-only: the forward sweeps' low-rank updates go to
-// two dense correction arrays, corT[k][r] = (F_k w_{k-1})[r] (r < amax) and
-// corB[k][toff_k + a] = (G_k w~_{k+1})[a] (a < bmax), zero everywhere else (they
-// are cleared once per solve and the same entries are rewritten every iteration).
-// A step reads w_k - corT_k - corB_k with independent LDS loads, sums two 8-lane
-// DPP dot products side by side and writes plainly -- no read-modify-write and no
-// branch on its critical path.  Both halves run the same instruction stream with
-// per-half operands.  2 max(p, nb-1-p) + 1 barriers.
+// xt = K^{-1} rb.  The forward sweeps' low-rank updates go into rb in place (the
+// writer lane of a row reads the old value at the start of the step, off the critical
+// path), except the bottom chain's update of the middle block, which the top chain
+// updates too: it goes to corB[p][toff_p + a] (a < bmax), zero everywhere else (cleared
+// once per solve, the same entries rewritten every iteration).  A step reads only its
+// block of rb and the F / G row (8 LDS reads per lane, 16 before), sums two 8-lane DPP
+// dot products side by side.  Both halves run the same instruction stream with per-half
+// operands.  2 max(p, nb-1-p) + 1 barriers.  Same sums as the earlier read-only form
+// (w - corT - corB), which subtracted exact zeros for the other chain.
 template <int SL>
 __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KParams& p, const double* Fc,
-                                              const double* Gc, const int* toffL, const double* rb, double* xt,
-                                              double* corT, double* corB, long long* pacc) {
+                                              const double* Gc, const int* toffL, double* rb, double* xt,
+                                              double* corB, long long* pacc) {
 #ifdef MPCQP_PHASE_PROF
     long long t0s = clock64();
 #define SPH(k) if (pacc && threadIdx.x == 0) { const long long t_ = clock64(); pacc[k] += t_ - t0s; t0s = t_; }
@@ -307,31 +308,26 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
     const int nmine = half ? nbot : pm, lim = half ? bmax : amax;
     const bool writer = j0 == 0, lowrank = i < lim;
     const int ir = lowrank ? i : 0;  // F / G row this thread sums (row 0 for the rest: reads stay in range)
-    double* corW = half ? corB : corT;
-    auto load_w = [&](int k, double (&v4)[4]) {
-        const double* w = rb + k * S;
-        const double* ct = corT + k * S;
-        const double* cb = corB + k * S;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) v4[c] = (w[jg + 8 * c] - ct[jg + 8 * c]) - cb[jg + 8 * c];
-    };
-    // forward: top step s: t_{s-1} = S_{s-1}^{-1} w_{s-1}, corT_s = F_s w_{s-1};
-    //          bottom step s (k = nb-1-s): t~_{k+1} = T_{k+1}^{-1} w~_{k+1}, corB_k = G_k w~_{k+1}
+    // forward: top step s: t_{s-1} = S_{s-1}^{-1} w_{s-1}, w_s -= F_s w_{s-1};
+    //          bottom step s (k = nb-1-s): t~_{k+1} = T_{k+1}^{-1} w~_{k+1}, w~_k -= G_k w~_{k+1}
 #pragma unroll
     for (int s = 1; s < SL; ++s) {
         if (s <= nst) {
             if (s <= nmine) {
                 const int ks = half ? nb - s : s - 1, kd = half ? nb - 1 - s : s;
                 const int woff = kd * S + (half ? toffL[kd] : 0);
-                double v4[4];
-                load_w(ks, v4);
+                const bool mid = half && kd == pm;
+                double* dst = (mid ? corB : rb) + woff + i;
+                const double old = (writer && lowrank && !mid) ? *dst : 0.0;
+                const double* w = rb + ks * S;
+                const double v4[4] = {w[jg], w[jg + 8], w[jg + 16], w[jg + 24]};
                 const double* f = (half ? Gc + (kd - pm) * bmax * FGS : Fc + (s - 1) * amax * FGS) + ir * FGS;
                 const double f4[4] = {f[jg], f[jg + 8], f[jg + 16], f[jg + 24]};
                 const double t = reduce8(dot4c(R.Inv[s - 1], v4));
                 const double c = reduce8(dot4c(f4, v4));
                 if (writer) {
                     xt[ks * S + i] = t;
-                    if (lowrank) corW[woff + i] = c;
+                    if (lowrank) *dst = mid ? c : old - c;
                 }
             }
             __syncthreads();
@@ -340,8 +336,11 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
     SPH(12)
     // middle: x_p = M^{-1} w_p with both chains' corrections, by the top half
     if (half == 0) {
+        const double* w = rb + pm * S;
+        const double* cb = corB + pm * S;
         double v4[4];
-        load_w(pm, v4);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v4[c] = w[jg + 8 * c] - cb[jg + 8 * c];
 #pragma unroll
         for (int s = 0; s < SL; ++s) {
             if (s == pm) {
@@ -691,7 +690,7 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
 #else
             long long* pacc = nullptr;
 #endif
-            if constexpr (TTK == 512) twisted_solve<NS + 1>(RF, p, Fc, Gc, toffL, L.rb, L.xt, L.cor, L.tv, pacc);
+            if constexpr (TTK == 512) twisted_solve<NS + 1>(RF, p, Fc, Gc, toffL, L.rb, L.xt, L.tv, pacc);
             else wave_twisted_solve<NS>(RF, p, Fc, Gc, toffL, L.rb, L.xt, L.cor, pacc);
             PH(2)
             // z~ = A x~ ; relaxed + projected z ; y ; next w.   x update; deltas for the checks.
