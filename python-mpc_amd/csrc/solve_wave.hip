@@ -547,16 +547,19 @@ __device__ __forceinline__ void solve_w2_body(const KParams& p, double* __restri
         }
         double X = C.X[pc], DX = 0.0;
         const double Q = L.qv[pc];
-        // phase-C slots (pair, j) of the lane; pair NP is the zero block
-        int gslot[3], tslot[3];
+        // phase-C slots (pair, j) of the lane; pair NP is the zero block.  Block 0 needs
+        // three pairs and block 3 none, so wave 0's upper half (block 3's rows) takes block
+        // 0's pair (3,0) and hands its partial sum over with a half-wave swap: two slots
+        // per lane in both waves.
+        int gslot[2], tslot[2];
         {
-            int pr[3], jj[3];
-            if (w == 0 && h == 0) { pr[0] = 0; jj[0] = 1; pr[1] = 1; jj[1] = 2; pr[2] = 3; jj[2] = 3; }
-            else if (w == 0)      { pr[0] = NP; jj[0] = 3; pr[1] = NP; jj[1] = 3; pr[2] = NP; jj[2] = 3; }
-            else if (h == 0)      { pr[0] = 2; jj[0] = 2; pr[1] = 4; jj[1] = 3; pr[2] = NP; jj[2] = 3; }
-            else                  { pr[0] = 5; jj[0] = 3; pr[1] = NP; jj[1] = 3; pr[2] = NP; jj[2] = 3; }
+            int pr[2], jj[2];
+            if (w == 0 && h == 0) { pr[0] = 0; jj[0] = 1; pr[1] = 1; jj[1] = 2; }
+            else if (w == 0)      { pr[0] = 3; jj[0] = 3; pr[1] = NP; jj[1] = 3; }
+            else if (h == 0)      { pr[0] = 2; jj[0] = 2; pr[1] = 4; jj[1] = 3; }
+            else                  { pr[0] = 5; jj[0] = 3; pr[1] = NP; jj[1] = 3; }
 #pragma unroll
-            for (int s = 0; s < 3; ++s) {
+            for (int s = 0; s < 2; ++s) {
                 gslot[s] = lds_addr(L.gl + pr[s] * 8 * S + r);
                 tslot[s] = lds_addr(L.tv + w * 32 + jj[s] * 8);
             }
@@ -666,9 +669,9 @@ __device__ __forceinline__ void solve_w2_body(const KParams& p, double* __restri
             PHL(13)
             // C: x~_kb[r] = t + sum_s G_{pair_s}[q][r] t_{j_s}[q]
             {
-                double gv[3][8], tq[3][8];
+                double gv[2][8], tq[2][8];
 #pragma unroll
-                for (int s = 0; s < 3; ++s) {
+                for (int s = 0; s < 2; ++s) {
 #pragma unroll
                     for (int q = 0; q < 8; ++q) gv[s][q] = lds_at(gslot[s] + q * S * 8);
 #pragma unroll
@@ -678,13 +681,22 @@ __device__ __forceinline__ void solve_w2_body(const KParams& p, double* __restri
                 }
                 double a0 = 0.0, a1 = 0.0;
 #pragma unroll
-                for (int s = 0; s < 3; ++s)
+                for (int s = 0; s < 2; ++s)
 #pragma unroll
                     for (int q = 0; q < 8; q += 2) {
                         a0 += gv[s][q] * tq[s][q];
                         a1 += gv[s][q + 1] * tq[s][q + 1];
                     }
-                const double xn = t + (a0 + a1);
+                double d = a0 + a1;
+                if (w == 0) {  // block 0 (lower half) + its pair (3,0) from the upper half; block 3: t
+                    const unsigned lo = (unsigned)__double2loint(d), hi = (unsigned)__double2hiint(d);
+                    const auto l2 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+                    const auto h2 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+                    const double dl0 = __hiloint2double((int)h2[0], (int)l2[0]);  // lower half's partial
+                    const double dl1 = __hiloint2double((int)h2[1], (int)l2[1]);  // upper half's partial
+                    d = h ? 0.0 : dl0 + dl1;
+                }
+                const double xn = t + d;
                 L.xt[pc] = xn;
                 const double xnew = alpha * xn + (1.0 - alpha) * X;
                 DX = xnew - X;
