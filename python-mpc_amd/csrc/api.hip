@@ -220,6 +220,8 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
     k.n = pl.n; k.m = pl.m; k.nb = pl.nb; k.npad = pl.npad; k.nnzP = pl.nnzP; k.nnzA = pl.nnzA; k.amax = pl.amax;
     k.bmax = pl.bmax; k.pmeet = (pl.nb - 1) / 2;
     k.gk = pl.gather_k; k.pk = pl.p_k; k.ntgt = pl.ntgt; k.term_max = pl.term_max;
+    k.gk1 = 0;
+    for (int i = 128; i < pl.m; ++i) k.gk1 = std::max(k.gk1, pl.acsr_ptr[i + 1] - pl.acsr_ptr[i]);
     const mpcqp_settings& st = h->set;
     k.sigma = st.sigma; k.alpha = st.alpha; k.eps_abs = st.eps_abs; k.eps_rel = st.eps_rel;
     k.eps_pinf = st.eps_prim_inf; k.eps_dinf = st.eps_dual_inf; k.rho0 = st.rho;

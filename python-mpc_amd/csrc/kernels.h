@@ -30,6 +30,7 @@ enum : int {
 // workspace (instance-major arrays) + settings.  Passed by value.
 struct KParams {
     int n, m, nb, npad, nnzP, nnzA, amax, gk, pk, ntgt, term_max;
+    int gk1;          // most nonzeros in a row >= 128 (the two-wave kernel's second row slot)
     int bmax, pmeet;  // two-sided factorisation (solve_big.hip): tail width, meeting block
     int variant;  // solve-kernel instantiation (solve.hip: launch_solve)
     int mode;     // factor storage of that variant (solve.hip: factorize)

@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "setup_r.h"
 #include "solve_phases.h"
@@ -414,9 +415,10 @@ __global__ __launch_bounds__(TW, 1) void k_solve_w(KParams p, double* __restrict
 // Per-wave LDS for those: cw[w][block][8] (in cor), tw[w][block][8] (in tv).
 constexpr int T2 = 128;
 
-template <int K, int RS, int KPK>
+template <int K, int RS, int KPK, int K1>
 __device__ __forceinline__ void solve_w2_body(const KParams& p, double* __restrict__ xo, double* __restrict__ yo,
                                               int factor_only) {
+    static_assert(RS == 2, "rows i = tid and tid + 128");
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int h = lane >> 5, r = lane & 31, rr = lane >> 3, ch = lane & 7;
     const int kb = w ? 1 + h : 3 * h;          // own block
@@ -490,7 +492,11 @@ __device__ __forceinline__ void solve_w2_body(const KParams& p, double* __restri
     const unsigned Xbase = lds_addr(C.X);
     bool cv = false;
     double Dv = 1.0, Ev[RS];
-    GatherW<K> cg, rg[RS];
+    // row gather lists: slot 0 (rows < 128) K entries, slot 1 (rows >= 128) K1 <= K --
+    // the plan's row order often puts the short rows last (cfg 2: the box rows, one
+    // nonzero each, are rows 84..187), so slot 1 skips the zero-padded entries
+    GatherW<K> cg, rg0;
+    GatherW<K1> rg1;
     GatherW<KPK> pg;  // the column's P list (addresses of Pv / X), for the inline check
     PH(5)
     for (;;) {
@@ -530,8 +536,13 @@ __device__ __forceinline__ void solve_w2_body(const KParams& p, double* __restri
             for (int s = 0; s < RS; ++s) {
                 const int i = min(tid + s * T2, mp - 1);
                 Ev[s] = i < m ? p.E[b * m + i] : 1.0;
-                if (i < m) rg[s].load(p.grow + i, m, abase, xbase);
-                else rg[s].clear(abase + 8u * nnzA, xbase);
+            }
+            {
+                const int i0 = tid, i1 = min(tid + T2, mp - 1);
+                if (i0 < m) rg0.load(p.grow + i0, m, abase, xbase);
+                else rg0.clear(abase + 8u * nnzA, xbase);
+                if (i1 < m) rg1.load(p.grow + i1, m, abase, xbase);
+                else rg1.clear(abase + 8u * nnzA, xbase);
             }
             PH(0)
         }
@@ -706,22 +717,31 @@ __device__ __forceinline__ void solve_w2_body(const KParams& p, double* __restri
             PHL(14)
             // z~ = A x~ ; relaxed + projected z ; y ; next w
             {
-                double av[RS][K], xv[RS][K], lo[RS], up[RS];
+                double av0[K], xv0[K], av1[K1], xv1[K1], lo[RS], up[RS], zts[RS];
 #pragma unroll
-                for (int s = 0; s < RS; ++s) {
+                for (int k = 0; k < K; ++k) {
+                    av0[k] = lds_at(rg0.e[k] & 0xFFFFu);
+                    xv0[k] = lds_at(rg0.e[k] >> 16);
+                }
 #pragma unroll
-                    for (int k = 0; k < K; ++k) {
-                        av[s][k] = lds_at(rg[s].e[k] & 0xFFFFu);
-                        xv[s][k] = lds_at(rg[s].e[k] >> 16);
-                    }
-                    lo[s] = L.lo[ri[s]];
-                    up[s] = L.up[ri[s]];
+                for (int k = 0; k < K1; ++k) {
+                    av1[k] = lds_at(rg1.e[k] & 0xFFFFu);
+                    xv1[k] = lds_at(rg1.e[k] >> 16);
                 }
 #pragma unroll
                 for (int s = 0; s < RS; ++s) {
-                    double zt = av[s][0] * xv[s][0];
+                    lo[s] = L.lo[ri[s]];
+                    up[s] = L.up[ri[s]];
+                }
+                zts[0] = av0[0] * xv0[0];
 #pragma unroll
-                    for (int k = 1; k < K; ++k) zt += av[s][k] * xv[s][k];
+                for (int k = 1; k < K; ++k) zts[0] += av0[k] * xv0[k];
+                zts[1] = av1[0] * xv1[0];
+#pragma unroll
+                for (int k = 1; k < K1; ++k) zts[1] += av1[k] * xv1[k];
+#pragma unroll
+                for (int s = 0; s < RS; ++s) {
+                    const double zt = zts[s];
                     const double zr = alpha * zt + (1.0 - alpha) * Z[s];
                     const double zn = __builtin_fmin(__builtin_fmax(zr + rvi[s] * y[s], lo[s]), up[s]);
                     const double dd = rv[s] * (zr - zn);
@@ -760,13 +780,18 @@ __device__ __forceinline__ void solve_w2_body(const KParams& p, double* __restri
             for (int s = 0; s < RS; ++s) {  // rows: A x, z, the projected delta y, A dx
                 const bool ok = tid + s * T2 < m;
                 double ax = 0.0, ad = 0.0;
+                auto rowdots = [&](const auto& g) __attribute__((always_inline)) {
+                    constexpr int KK = std::extent_v<std::remove_reference_t<decltype(g.e)>>;
 #pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    const unsigned e = rg[s].e[k], va = e >> 16;
-                    const double a = lds_at(e & 0xFFFFu);
-                    ax += a * lds_at(va - xbase + Xbase);
-                    ad += a * lds_at(va - xbase + dxbase);
-                }
+                    for (int k = 0; k < KK; ++k) {
+                        const unsigned e = g.e[k], va = e >> 16;
+                        const double a = lds_at(e & 0xFFFFu);
+                        ax += a * lds_at(va - xbase + Xbase);
+                        ad += a * lds_at(va - xbase + dxbase);
+                    }
+                };
+                if (s == 0) rowdots(rg0);
+                else rowdots(rg1);
                 adx[s] = ad;
                 const double zi = Z[s], pr = ax - zi, ei = 1.0 / Ev[s];
                 const double lo = L.lo[ri[s]], up = L.up[ri[s]];
@@ -953,10 +978,10 @@ __device__ __forceinline__ void solve_w2_body(const KParams& p, double* __restri
 }
 
 // the kernel: the solve, then (last workgroup only) the dispatch order of the next launch
-template <int K, int RS, int KPK>
+template <int K, int RS, int KPK, int K1>
 __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restrict__ xo, double* __restrict__ yo,
                                                     int factor_only) {
-    solve_w2_body<K, RS, KPK>(p, xo, yo, factor_only);
+    solve_w2_body<K, RS, KPK, K1>(p, xo, yo, factor_only);
     extern __shared__ __attribute__((aligned(16))) double sm[];
     order_epilogue<T2>(p, (int*)sm);
 }
@@ -966,7 +991,7 @@ __global__ __launch_bounds__(T2, 1) void k_solve_w2(KParams p, double* __restric
 // k_setup_r), then solves it.  Everything the solve reads from the workspace was
 // written by this workgroup before the barrier, so no second kernel, no launch gap and
 // no setup kernel in front of the slowest instance.
-template <int K, int RS, int KPK, int SK, int SRS, int SAS, int SPS>
+template <int K, int RS, int KPK, int K1, int SK, int SRS, int SAS, int SPS>
 __global__ __launch_bounds__(T2, 1) void k_setup_solve_w2(KParams p, const double* __restrict__ Px_in,
                                                           const double* __restrict__ Ax_in,
                                                           const double* __restrict__ q_in,
@@ -976,7 +1001,7 @@ __global__ __launch_bounds__(T2, 1) void k_setup_solve_w2(KParams p, const doubl
     extern __shared__ __attribute__((aligned(16))) double sm[];
     setup_r_body<T2, SK, 4, SRS, SAS, SPS>(p, instance_of(p), Px_in, Ax_in, q_in, l_in, u_in, sm);
     __syncthreads();
-    solve_w2_body<K, RS, KPK>(p, xo, yo, 0);
+    solve_w2_body<K, RS, KPK, K1>(p, xo, yo, 0);
     order_epilogue<T2>(p, (int*)sm);
 }
 
@@ -994,7 +1019,7 @@ hipError_t launch_setup_solve(const KParams& p, long B, const double* Px, const 
         return e != hipSuccess ? e : launch_solve(p, B, xo, yo, 0, st);
     }
     const size_t lds = std::max(lds_w2_bytes(p), lds_setup_r_bytes(p.nnzP, p.nnzA, p.npad, p.m));
-    auto k = k_setup_solve_w2<6, 2, 4, 6, 2, 4, 2>;
+    auto k = p.gk1 <= 1 ? k_setup_solve_w2<6, 2, 4, 1, 6, 2, 4, 2> : k_setup_solve_w2<6, 2, 4, 6, 6, 2, 4, 2>;
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(T2), lds, st, p, Px, Ax, q, l, u, xo, yo);
@@ -1003,10 +1028,10 @@ hipError_t launch_setup_solve(const KParams& p, long B, const double* Px, const 
     return launch_polish(p, B, xo, yo, st);
 }
 
-template <int K, int RS, int KPK>
+template <int K, int RS, int KPK, int K1>
 static hipError_t go_w2(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st, size_t lds,
                         KernelRef* ref) {
-    auto k = k_solve_w2<K, RS, KPK>;
+    auto k = k_solve_w2<K, RS, KPK, K1>;
     if (ref) { *ref = {(const void*)k, T2, lds}; return hipSuccess; }
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
@@ -1037,7 +1062,9 @@ hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, i
     switch (p.variant) {
         case 8: return go_w<6, 3>(p, B, xo, yo, factor_only, st, lds, ref);
         case 9: return go_w<8, 4>(p, B, xo, yo, factor_only, st, lds, ref);
-        case 10: return go_w2<6, 2, 4>(p, B, xo, yo, factor_only, st, lds_w2_bytes(p), ref);
+        case 10:  // slot-1 rows (>= 128) with at most one nonzero (cfg 2's box rows): K1 = 1
+            return p.gk1 <= 1 ? go_w2<6, 2, 4, 1>(p, B, xo, yo, factor_only, st, lds_w2_bytes(p), ref)
+                              : go_w2<6, 2, 4, 6>(p, B, xo, yo, factor_only, st, lds_w2_bytes(p), ref);
         default: return hipErrorInvalidValue;
     }
 }
