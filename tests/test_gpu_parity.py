@@ -547,3 +547,15 @@ def test_random_banded_qps(n, m, band, seed):
         dual = np.abs(px + b["q"][k] + aty).max()
         assert prim <= (1e-3 + 1e-3 * np.abs(ax).max()) * 1.01, (k, prim)
         assert dual <= (1e-3 + 1e-3 * max(np.abs(px).max(), np.abs(aty).max(), np.abs(b["q"][k]).max())) * (1 + 1e-9), (k, dual)
+
+
+@pytest.mark.parametrize("eps", [1e-3, 1e-9])
+def test_osqp_demo_known_answer(eps):
+    """OSQP's documented demo problem (tests/test_oracle.py::osqp_demo_problem): the
+    device matches the oracle (status, iterations, x) and the closed-form optimum."""
+    from test_oracle import osqp_demo_problem
+    P, q, A, l, u, xs, ys, obj = osqp_demo_problem()
+    ro, rg = _cmp_single(P, q, A, l, u, dict(eps_abs=eps, eps_rel=eps), slice(0, 2))
+    tol = 5e-3 if eps > 1e-6 else 1e-7
+    assert np.abs(rg.x - xs).max() < tol
+    assert np.abs(rg.y - ys).max() < 10 * tol

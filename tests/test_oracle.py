@@ -178,3 +178,30 @@ def test_oracle_polish_rejected_keeps_admm_solution(golden):
         r.append(o.solve())
     assert r[1].info.status_polish == -1 and r[0].info.status_polish == 0
     assert np.array_equal(r[0].x, r[1].x)
+
+
+def osqp_demo_problem():
+    """OSQP's own documented "setup and solve" example (osqp.org docs, Python
+    interface): P = [[4, 1], [1, 2]], q = [1, 1], x1 + x2 = 1, 0 <= x <= 0.7.  Its
+    optimum is known in closed form -- x2 at its bound, x1 = 0.3, objective 1.88,
+    y = [-2.9, 0, 0.2] -- so it is a known-answer test for the OSQP 0.6 restatement
+    that does not depend on any implementation (the docs' iteration count is not
+    used: it is not reproducible across OSQP builds)."""
+    P = sp.csc_matrix(np.array([[4.0, 1.0], [0.0, 2.0]]))  # upper triangle, as osqp keeps it
+    q = np.array([1.0, 1.0])
+    A = sp.csc_matrix(np.array([[1.0, 1.0], [1.0, 0.0], [0.0, 1.0]]))
+    l = np.array([1.0, 0.0, 0.0])
+    u = np.array([1.0, 0.7, 0.7])
+    return P, q, A, l, u, np.array([0.3, 0.7]), np.array([-2.9, 0.0, 0.2]), 1.88
+
+
+@pytest.mark.parametrize("eps,tol", [(1e-3, 5e-3), (1e-9, 1e-7)])
+def test_oracle_osqp_demo_known_answer(eps, tol):
+    P, q, A, l, u, xs, ys, obj = osqp_demo_problem()
+    o = pyoracle.OSQP()
+    o.setup(P, q, A, l, u, eps_abs=eps, eps_rel=eps, verbose=False)
+    r = o.solve()
+    assert r.info.status == "solved"
+    assert np.abs(r.x - xs).max() < tol
+    assert np.abs(r.y - ys).max() < 10 * tol
+    assert abs(r.info.obj_val - obj) < 10 * tol
