@@ -20,6 +20,10 @@ own batch (weak scaling, no data-path collective); timing = barrier +
 synchronize on both sides, max over ranks.  --config 3/5 select the slack /
 incremental-dynamic workloads (not the headline line); cfg 5 is warm-started as
 SURVEY.md §8d D2 prescribes (cold solve, one-stage shift, timed warm re-solve).
+--config 4 is BASELINE.json configs[3] (B = 262144 slack QPs split over 8 GPUs):
+32768 per rank, each rank generating its own shard (seed 4000 + rank) -- the
+same distribution as one seeded batch cut into contiguous shards, without
+every rank building all 262144 instances on the host.
 
 rank 0 prints ONE JSON line with "roofline" (k_solve, HBM-bound by the
 algorithmic-bytes model of SURVEY.md §8d D3, HIP-event kernel times from the
@@ -58,7 +62,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 5])
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
     ap.add_argument("--batch", type=int, default=None, help="instances per GPU (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
