@@ -273,8 +273,12 @@ __device__ __forceinline__ void block_max_sum_tr(double (&v)[K], double (&sm)[KS
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
         double r = rs[k];
+        if constexpr (NW == 4) {  // block_sum's order for four waves
+            r = (rs[k] + rs[KS + k]) + (rs[2 * KS + k] + rs[3 * KS + k]);
+        } else {
 #pragma unroll
-        for (int w = 1; w < NW; ++w) r += rs[w * KS + k];
+            for (int w = 1; w < NW; ++w) r += rs[w * KS + k];
+        }
         sm[k] = r;
     }
     __syncthreads();

@@ -671,7 +671,7 @@ size_t lds_solve_bytes(const KParams& p) { return lds_base_bytes(p); }
 
 size_t lds_kernel_bytes(const KParams& p) {
     if (p.variant == 16) return lds_dense_bytes(p);
-    if (p.variant == 10) return lds_w2_bytes(p);
+    if (p.variant == 10 || p.variant == 17) return lds_w2_bytes(p);
     return p.variant >= 11 && p.variant <= 14 ? lds_solve_bytes_big(p) : lds_solve_bytes(p);
 }
 
@@ -715,6 +715,9 @@ bool variant_fits(const KParams& p, int v) {
         case 14:
             return p.nb > 4 && p.nb <= 8 && p.amax <= 16 && p.bmax <= 16 && p.gk <= 8 && p.npad <= 256 &&
                    p.m <= 256 && lds_solve_bytes_big(p) <= 160 * 1024;
+        case 17:  // four waves, two workgroups per CU (two waves per SIMD): up to 80 KB of LDS each
+            return p.nb == 4 && p.amax <= 8 && p.gk <= 6 && p.pk <= 4 && p.m <= 256 && p.npad <= 128 &&
+                   p.nnzA <= 512 && p.nnzP <= 256 && lds_w2_bytes(p) <= 80 * 1024;
         case 16:  // dense inverse: one variable per lane pair of a 256-thread workgroup, packed LDS addresses
             return p.n <= kDenseR && p.npad <= 128 && p.gk <= 6 && p.pk <= 4 && p.m <= 2 * 128 &&
                    lds_dense_bytes(p) < 65536;
@@ -736,13 +739,14 @@ int solve_threads(int variant) {
         case 11: case 12: case 13: return kThreadsBig;
         case 14: return 128;
         case 16: return 256;
+        case 17: return 256;
         default: return T;
     }
 }
 
 int solve_mode(int variant) {  // what factorize stores for the variant (KParams::mode)
     switch (variant) {
-        case 0: case 8: case 9: case 10: return 2;
+        case 0: case 8: case 9: case 10: case 17: return 2;
         case 1: case 2: case 3: case 7: case 16: return 1;  // (16: no factor stored; dx aliases rb)
         case 11: case 12: case 13: case 14: return 3;  // two-sided factor (solve_big.hip)
         default: return 0;
@@ -761,7 +765,7 @@ static hipError_t launch_solve_only(const KParams& p, long B, double* xo, double
         case 5: return go<0, 32, 8, 4, 4, 2>(p, B, xo, yo, factor_only, st, lds, ref);
         case 6: return go<0, 32, 16, 8, 8, 1>(p, B, xo, yo, factor_only, st, lds, ref);
         case 7: return go<4, 8, 6, 1, 1, 4, false>(p, B, xo, yo, factor_only, st, lds, ref);
-        case 8: case 9: case 10: return launch_solve_wave(p, B, xo, yo, factor_only, st, ref);
+        case 8: case 9: case 10: case 17: return launch_solve_wave(p, B, xo, yo, factor_only, st, ref);
         case 16: return launch_solve_dense(p, B, xo, yo, factor_only, st, ref);
         case 11: case 12: case 13: case 14: return launch_solve_big(p, B, xo, yo, factor_only, st, ref);
         default: return hipErrorInvalidValue;

@@ -494,6 +494,93 @@ __device__ __forceinline__ bool factorize_w2(const KP& p, SLds& L, const double 
     return okf[0] > 0.5 && okf[1] > 0.5;
 }
 
+// The four-wave kernel's factorisation (solve_wave.hip::k_solve_w4, variant 17: mode 2,
+// nb = 4, amax <= 8; TT = 256): factorize_w2 with one wave per block in stage 1 -- wave
+// k assembles D_k and pre-pivots it (block 0: the whole inverse), all four at once --
+// then the same k = 1..3 chain (F_k, the corner, the G blocks, wave 0's corner pivots).
+// The critical path of stage 1 is one block's pivots instead of two.  Same outputs.
+template <class KP>
+__device__ __forceinline__ bool factorize_w4(const KP& p, SLds& L, const double rho, double* __restrict__ Hg,
+                                             double* __restrict__ Sg) {
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int amax = p.amax, as = amax * S;
+    const long gstride = (long)amax * S;
+    double* const V = L.SP;
+    double* const G20 = V + 7 * as;
+    double* const dl = V + 8 * as;              // amax x amax, row stride 16
+    double* const bufw = dl + 256 + w * 2 * S;  // the wave's Gauss-Jordan publish buffers
+    double* const okf = dl + 256 + 8 * S;
+    auto Ek = [&](int k) __attribute__((always_inline)) { return V + k * as; };
+    auto Fk = [&](int k) __attribute__((always_inline)) { return V + (3 + k) * as; };
+    auto wave_sync = []() __attribute__((always_inline)) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+#ifdef MPCQP_PHASE_PROF
+    long long tf = clock64();
+#define FPH(k) if (tid == 0) { const long long t_ = clock64(); L.pacc[k] += t_ - tf; tf = t_; }
+#else
+#define FPH(k)
+#endif
+    assemble_block<false, true>(p, L, rho, w, Sg + (long)w * SS, Ek(w), lane, 64, wave_sync);
+    wave_sync();
+    FPH(8)
+    bool okw = gj_seg<1>(Sg + (long)w * SS, bufw, w ? amax : 0, p.bsize[w], nullptr);
+    FPH(10)
+    __syncthreads();
+    FPH(11)
+#pragma unroll 1
+    for (int k = 1; k < 4; ++k) {
+        const double* Sp = Sg + (long)(k - 1) * SS;
+        const double* E = Ek(k);
+        double* F = Fk(k);
+        const int l0 = p.toff[k - 1], bmax = p.bmax;
+        for (int o = tid; o < as; o += 256) {
+            const int r = o >> 5, j = o & (S - 1);
+            double sacc = 0.0;
+#pragma unroll 4
+            for (int l = l0; l < l0 + bmax; ++l) sacc += E[r * S + l] * Sp[l * S + j];
+            F[o] = sacc;
+            Hg[(long)(k * (k - 1) / 2 + k - 1) * gstride + o] = -sacc;
+        }
+        __syncthreads();
+        if (tid < amax * amax) {  // S_k = D_k - F_k E_k' on the corner
+            const int r = tid / amax, c = tid - r * amax;
+            double sacc = 0.0;
+#pragma unroll 4
+            for (int l = l0; l < l0 + bmax; ++l) sacc += F[r * S + l] * E[c * S + l];
+            dl[r * 16 + c] = -sacc;
+        }
+#pragma unroll 1
+        for (int j = 0; j < k - 1; ++j) {
+            const bool adj = j == k - 2;
+            const double* Gp = adj ? Fk(k - 1) : G20;
+            const double sg = adj ? 1.0 : -1.0;
+            for (int o = tid; o < as; o += 256) {
+                const int r = o >> 5, c = o & (S - 1);
+                double sacc = 0.0;
+#pragma unroll
+                for (int l = 0; l < 8; ++l)
+                    if (l < amax) sacc += F[r * S + l] * Gp[l * S + c];
+                const double g = sg * sacc;
+                Hg[(long)(k * (k - 1) / 2 + j) * gstride + o] = g;
+                if (k == 2) G20[o] = g;
+            }
+        }
+        __syncthreads();
+        FPH(9)
+        if (w == 0) okw = gj_seg<2>(Sg + (long)k * SS, bufw, amax, p.bsize[k], dl) && okw;
+        __syncthreads();
+        FPH(11)
+    }
+    if (lane == 0) okf[w] = okw ? 1.0 : 0.0;
+    __syncthreads();
+    FPH(9)
+#undef FPH
+    return okf[0] > 0.5 && okf[1] > 0.5 && okf[2] > 0.5 && okf[3] > 0.5;
+}
+
 // The 256-thread register-sweep kernels' factorisation (mode 1: F_k rows < amax and
 // S_k^{-1} to the workspace; amax <= 16), split like factorize_w2 but on workspace
 // tiles, since their LDS has no room for a tile per wave:
@@ -608,8 +695,9 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
     if constexpr (TT == 128 && !POL) {  // the two-wave kernel (variant 10: nb = 4, amax <= 8)
         if (p.mode == 2 && p.nb == 4 && p.amax <= 8) return factorize_w2(p, L, rho, Hg, Sg);
     }
-    if constexpr (TT == 256 && !POL) {  // the register-sweep kernels (variants 1-3)
+    if constexpr (TT == 256 && !POL) {  // the register-sweep kernels (variants 1-3), the four-wave kernel (17)
         if (p.mode == 1 && p.amax <= 16) return factorize_g(p, L, rho, Fg, Sg);
+        if (p.variant == 17 && p.mode == 2 && p.nb == 4 && p.amax <= 8) return factorize_w4(p, L, rho, Hg, Sg);
     }
     const int tid = threadIdx.x;
     const int nb = p.nb, amax = p.amax, mode = POL ? 1 : p.mode;

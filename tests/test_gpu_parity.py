@@ -250,12 +250,14 @@ def test_polish_batch_cfg2():
     assert np.all(du[same] < 1e-6), du.max()
 
 
-@pytest.mark.parametrize("variant,cfg,B", [(11, 3, 256), (14, 3, 256), (12, 5, 64), (8, 2, 256), (16, 2, 256)])
+@pytest.mark.parametrize("variant,cfg,B", [(11, 3, 256), (14, 3, 256), (12, 5, 64), (8, 2, 256), (16, 2, 256),
+                                             (17, 2, 1024)])
 def test_alternative_kernel_variants(monkeypatch, variant, cfg, B):
     """Kernel instantiations that are not the default choice for a plan stay exact:
     the 512-thread two-sided kernel on the slack layout (variant 11), the two-wave
     two-sided kernel (14), the long-horizon kernel on cfg 5 (12), the one-wave
-    kernel on cfg 2 (8) and the dense-inverse kernel on cfg 2 (16), selected with the MPCQP_VARIANT override."""
+    kernel on cfg 2 (8), the dense-inverse kernel on cfg 2 (16) and the four-wave kernel on
+    cfg 2 (17), selected with the MPCQP_VARIANT override."""
     monkeypatch.setenv("MPCQP_VARIANT", str(variant))
     b = mpc.make_batch(cfg, B=B)
     settings = dict(warm_start=True) if cfg == 3 else dict(polish=False, warm_start=False)
