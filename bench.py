@@ -119,11 +119,15 @@ def bound_sequence(b, count, seed, to_dev):
 
 
 def solve_kernel_name(info, fused):
-    """The kernel the roofline times: the fused setup+solve kernel where the two-wave
-    variant runs it (solve_wave.hip::k_setup_solve_w2), else the solve kernel."""
-    if info["threads_per_qp"] == 128 and fused:
-        return "mpcqp::k_setup_solve_w2"
-    return {64: "mpcqp::k_solve_w", 128: "mpcqp::k_solve_w2"}.get(info["threads_per_qp"], "mpcqp::k_solve")
+    """The kernel the roofline times: the fused setup+solve kernel where the four- or
+    two-wave variant runs it (solve_wave.hip::k_setup_solve_w4 / _w2), else the solve
+    kernel."""
+    v = info["variant"]
+    if v in (10, 17) and fused:
+        return "mpcqp::k_setup_solve_w4" if v == 17 else "mpcqp::k_setup_solve_w2"
+    return {8: "mpcqp::k_solve_w", 9: "mpcqp::k_solve_w", 10: "mpcqp::k_solve_w2", 17: "mpcqp::k_solve_w4",
+            11: "mpcqp::k_solve_b", 12: "mpcqp::k_solve_b", 13: "mpcqp::k_solve_b", 14: "mpcqp::k_solve_b",
+            16: "mpcqp::k_solve_d"}.get(v, "mpcqp::k_solve")
 
 
 def pmc_traffic(workload, batch, kernel):

@@ -726,7 +726,7 @@ bool variant_fits(const KParams& p, int v) {
 }
 
 int solve_variant(const KParams& p) {
-    static const int order[] = {10, 8, 9, 0, 1, 2, 3, 11, 12, 13, 4, 5, 6};  // 14, 16: MPCQP_VARIANT only
+    static const int order[] = {17, 10, 8, 9, 0, 1, 2, 3, 11, 12, 13, 4, 5, 6};  // 14, 16: MPCQP_VARIANT only
     for (int v : order)
         if (variant_fits(p, v)) return v;
     return -1;

@@ -251,13 +251,14 @@ def test_polish_batch_cfg2():
 
 
 @pytest.mark.parametrize("variant,cfg,B", [(11, 3, 256), (14, 3, 256), (12, 5, 64), (8, 2, 256), (16, 2, 256),
-                                             (17, 2, 1024)])
+                                             (10, 2, 1024), (17, 2, 1024)])
 def test_alternative_kernel_variants(monkeypatch, variant, cfg, B):
     """Kernel instantiations that are not the default choice for a plan stay exact:
     the 512-thread two-sided kernel on the slack layout (variant 11), the two-wave
     two-sided kernel (14), the long-horizon kernel on cfg 5 (12), the one-wave
-    kernel on cfg 2 (8), the dense-inverse kernel on cfg 2 (16) and the four-wave kernel on
-    cfg 2 (17), selected with the MPCQP_VARIANT override."""
+    kernel on cfg 2 (8), the dense-inverse kernel on cfg 2 (16), the two-wave kernel (10,
+    the default before the four-wave one) and the four-wave kernel (17) on cfg 2, selected
+    with the MPCQP_VARIANT override."""
     monkeypatch.setenv("MPCQP_VARIANT", str(variant))
     b = mpc.make_batch(cfg, B=B)
     settings = dict(warm_start=True) if cfg == 3 else dict(polish=False, warm_start=False)
@@ -433,8 +434,8 @@ def test_register_list_setup_is_bit_identical(monkeypatch, cfg, B):
 
 @pytest.mark.parametrize("cfg,B", [(2, 1024), (2, 40), (3, 96)])
 def test_fused_setup_solve_is_bit_identical(cfg, B):
-    """mpcqp_setup_solve_device (one kernel for the two-wave variant: solve_wave.hip::
-    k_setup_solve_w2; setup + solve kernels otherwise) against setup_device +
+    """mpcqp_setup_solve_device (one kernel for the four- and two-wave variants:
+    solve_wave.hip::k_setup_solve_w4 / _w2; setup + solve kernels otherwise) against setup_device +
     solve_device on a second handle: identical outputs, over two consecutive batches
     (the second dispatched in the order the first left behind)."""
     import torch
