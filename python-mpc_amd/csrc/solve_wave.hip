@@ -1020,7 +1020,7 @@ __global__ __launch_bounds__(T2, 1) void k_setup_solve_w2(KParams p, const doubl
 // (solve_phases.h::factorize_w4).  MPCQP_VARIANT=17 (A/B against variant 10).
 constexpr int T4 = 256;
 
-template <int K, int KPK>
+template <int K, int KPK, int QR>
 __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restrict__ xo, double* __restrict__ yo) {
     const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int h = lane >> 5, r = lane & 31, rr = lane >> 3, ch = lane & 7;
@@ -1209,6 +1209,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            PH(12)
             // B: t_w[r] = S_w^{-1}[r] (b_w + c_w): half-row sums, permlane32 swap
             double t;
             {
@@ -1232,24 +1233,26 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 if (low && r < 8) L.tv[w * 8 + r] = t;
             }
             __syncthreads();
-            PH(2)
-            // C: x~_w[r] = t + sum_s G_{pair_s}[q][r] t_{j_s}[q]  (slots split over the halves)
+            PH(13)
+            // C: x~_w[r] = t + sum_s G_{pair_s}[q][r] t_{j_s}[q]  (slots split over the halves;
+            // rows q < QR: the G blocks are zero from row amax on)
             {
-                double gv[2][8], tq[2][8];
+                constexpr int QE = (QR + 1) & ~1;  // t rows read in pairs
+                double gv[2][QE], tq[2][QE];
 #pragma unroll
                 for (int s = 0; s < 2; ++s) {
 #pragma unroll
-                    for (int q = 0; q < 8; ++q) gv[s][q] = lds_at(gslot[s] + q * S * 8);
+                    for (int q = 0; q < QE; ++q) gv[s][q] = q < QR ? lds_at(gslot[s] + q * S * 8) : 0.0;
 #pragma unroll
-                    for (int q = 0; q < 8; q += 2) lds_at2(tslot[s] + q * 8, tq[s][q], tq[s][q + 1]);
+                    for (int q = 0; q < QE; q += 2) lds_at2(tslot[s] + q * 8, tq[s][q], tq[s][q + 1]);
                 }
                 double a0 = 0.0, a1 = 0.0;
 #pragma unroll
                 for (int s = 0; s < 2; ++s)
 #pragma unroll
-                    for (int q = 0; q < 8; q += 2) {
+                    for (int q = 0; q < QR; q += 2) {
                         a0 += gv[s][q] * tq[s][q];
-                        a1 += gv[s][q + 1] * tq[s][q + 1];
+                        if (q + 1 < QR) a1 += gv[s][q + 1] * tq[s][q + 1];
                     }
                 const double d = a0 + a1;
                 const unsigned lo = (unsigned)__double2loint(d), hi = (unsigned)__double2hiint(d);
@@ -1264,7 +1267,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 X = xnew;
             }
             __syncthreads();
-            PH(2)
+            PH(14)
             // rows: z~ = A x~ ; relaxed + projected z ; y ; next w
             {
                 double av[K], xv[K];
@@ -1477,6 +1480,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
             for (int k = 0; k < 6; ++k) p.prof[b * kProfSlots + k] = L.pacc[k];
 #pragma unroll
             for (int k = 8; k < 15; ++k) p.prof[b * kProfSlots + k] = L.pacc[k];
+            p.prof[b * kProfSlots + 2] = L.pacc[12] + L.pacc[13] + L.pacc[14];
             p.prof[b * kProfSlots + 6] = clock64() - t0c;
             p.prof[b * kProfSlots + 7] = wall_clock64() - t0w;
             p.prof[b * kProfSlots + 15] = t0w;
@@ -1486,16 +1490,16 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
 #undef PH
 }
 
-template <int K, int KPK>
+template <int K, int KPK, int QR>
 __global__ __launch_bounds__(T4, 2) void k_solve_w4(KParams p, double* __restrict__ xo, double* __restrict__ yo,
                                                     int factor_only) {
-    solve_w4_body<K, KPK>(p, xo, yo);
+    solve_w4_body<K, KPK, QR>(p, xo, yo);
     extern __shared__ __attribute__((aligned(16))) double sm[];
     order_epilogue<T4>(p, (int*)sm);
 }
 
 // setup (setup_r.h with 256 threads: one column and one row per thread) + solve
-template <int K, int KPK, int SK, int SAS>
+template <int K, int KPK, int QR, int SK, int SAS>
 __global__ __launch_bounds__(T4, 2) void k_setup_solve_w4(KParams p, const double* __restrict__ Px_in,
                                                           const double* __restrict__ Ax_in,
                                                           const double* __restrict__ q_in,
@@ -1505,7 +1509,7 @@ __global__ __launch_bounds__(T4, 2) void k_setup_solve_w4(KParams p, const doubl
     extern __shared__ __attribute__((aligned(16))) double sm[];
     setup_r_body<T4, SK, 4, 1, SAS, 1>(p, instance_of(p), Px_in, Ax_in, q_in, l_in, u_in, sm);
     __syncthreads();
-    solve_w4_body<K, KPK>(p, xo, yo);
+    solve_w4_body<K, KPK, QR>(p, xo, yo);
     order_epilogue<T4>(p, (int*)sm);
 }
 
@@ -1525,7 +1529,8 @@ hipError_t launch_setup_solve(const KParams& p, long B, const double* Px, const 
     }
     const size_t lds = std::max(lds_w2_bytes(p), lds_setup_r_bytes(p.nnzP, p.nnzA, p.npad, p.m));
     if (p.variant == 17) {
-        auto k4 = k_setup_solve_w4<6, 4, 6, 2>;
+        // QR: rows of the G blocks phase C sums (the nonzero ones: amax)
+        auto k4 = p.amax <= 5 ? k_setup_solve_w4<6, 4, 5, 6, 2> : k_setup_solve_w4<6, 4, 8, 6, 2>;
         hipError_t e = hipFuncSetAttribute((const void*)k4, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k4, dim3((unsigned)B), dim3(T4), lds, st, p, Px, Ax, q, l, u, xo, yo);
@@ -1577,7 +1582,7 @@ hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, i
         case 8: return go_w<6, 3>(p, B, xo, yo, factor_only, st, lds, ref);
         case 9: return go_w<8, 4>(p, B, xo, yo, factor_only, st, lds, ref);
         case 17: {
-            auto k = k_solve_w4<6, 4>;
+            auto k = p.amax <= 5 ? k_solve_w4<6, 4, 5> : k_solve_w4<6, 4, 8>;
             const size_t lds = lds_w2_bytes(p);
             if (ref) { *ref = {(const void*)k, T4, lds}; return hipSuccess; }
             hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
