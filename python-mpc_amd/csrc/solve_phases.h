@@ -545,32 +545,38 @@ __device__ __forceinline__ bool factorize_w4(const KP& p, SLds& L, const double 
             Hg[(long)(k * (k - 1) / 2 + k - 1) * gstride + o] = -sacc;
         }
         __syncthreads();
-        if (tid < amax * amax) {  // S_k = D_k - F_k E_k' on the corner
-            const int r = tid / amax, c = tid - r * amax;
-            double sacc = 0.0;
-#pragma unroll 4
-            for (int l = l0; l < l0 + bmax; ++l) sacc += F[r * S + l] * E[c * S + l];
-            dl[r * 16 + c] = -sacc;
-        }
-#pragma unroll 1
-        for (int j = 0; j < k - 1; ++j) {
-            const bool adj = j == k - 2;
-            const double* Gp = adj ? Fk(k - 1) : G20;
-            const double sg = adj ? 1.0 : -1.0;
-            for (int o = tid; o < as; o += 256) {
-                const int r = o >> 5, c = o & (S - 1);
+        FPH(9)
+        if (w == 0) {
+            // wave 0: the corner S_k = D_k - F_k E_k' and its pivots right away (one wave:
+            // a wave sync orders the corner before gj_seg reads it)
+            if (lane < amax * amax) {
+                const int r = lane / amax, c = lane - r * amax;
                 double sacc = 0.0;
+#pragma unroll 4
+                for (int l = l0; l < l0 + bmax; ++l) sacc += F[r * S + l] * E[c * S + l];
+                dl[r * 16 + c] = -sacc;
+            }
+            wave_sync();
+            okw = gj_seg<2>(Sg + (long)k * SS, bufw, amax, p.bsize[k], dl) && okw;
+        } else {
+            // waves 1-3 meanwhile: G_kj = -F_k G_{k-1,j} (j < k-1), off the chain's path
+#pragma unroll 1
+            for (int j = 0; j < k - 1; ++j) {
+                const bool adj = j == k - 2;
+                const double* Gp = adj ? Fk(k - 1) : G20;
+                const double sg = adj ? 1.0 : -1.0;
+                for (int o = tid - 64; o < as; o += 192) {
+                    const int r = o >> 5, c = o & (S - 1);
+                    double sacc = 0.0;
 #pragma unroll
-                for (int l = 0; l < 8; ++l)
-                    if (l < amax) sacc += F[r * S + l] * Gp[l * S + c];
-                const double g = sg * sacc;
-                Hg[(long)(k * (k - 1) / 2 + j) * gstride + o] = g;
-                if (k == 2) G20[o] = g;
+                    for (int l = 0; l < 8; ++l)
+                        if (l < amax) sacc += F[r * S + l] * Gp[l * S + c];
+                    const double g = sg * sacc;
+                    Hg[(long)(k * (k - 1) / 2 + j) * gstride + o] = g;
+                    if (k == 2) G20[o] = g;
+                }
             }
         }
-        __syncthreads();
-        FPH(9)
-        if (w == 0) okw = gj_seg<2>(Sg + (long)k * SS, bufw, amax, p.bsize[k], dl) && okw;
         __syncthreads();
         FPH(11)
     }
