@@ -1213,13 +1213,14 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
             // B: t_w[r] = S_w^{-1}[r] (b_w + c_w): half-row sums, permlane32 swap
             double t;
             {
-                double v[16], cc[8];
+                constexpr int QE = (QR + 1) & ~1;  // c_w's nonzero rows (< amax), read in pairs
+                double v[16], cc[QE];
 #pragma unroll
                 for (int c = 0; c < 16; c += 2) ld2(L.rb + w * S + 16 * h + c, v[c], v[c + 1]);
 #pragma unroll
-                for (int c = 0; c < 8; c += 2) ld2(cwh + c, cc[c], cc[c + 1]);
+                for (int c = 0; c < QE; c += 2) ld2(cwh + c, cc[c], cc[c + 1]);
 #pragma unroll
-                for (int c = 0; c < 8; ++c) v[c] += cc[c];
+                for (int c = 0; c < QR; ++c) v[c] += cc[c];
                 double a[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
                 for (int c = 0; c < 16; ++c) a[c & 3] += SB[c] * v[c];
