@@ -504,8 +504,10 @@ __device__ __forceinline__ void solve_w2_body(const KParams& p, double* __restri
         if (need_factor) {  // start, and after a rho change
             need_factor = false;
             // the factorisation scratch aliases ys: y waits in the workspace's y array
-            if (iter > 0)
+            if (iter > 0) {
                 for (int i = tid; i < m; i += T2) p.y[b * m + i] = L.ys[i];
+                __syncthreads();  // every ys read is done before factorize_w2's scratch overwrites it
+            }
             const bool ok = factorize_nl<T2>(p.self, b, rho, Sg);
             if (!ok) {
                 if (iter == 0) {
@@ -1089,8 +1091,10 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
         __syncthreads();
         if (need_factor) {
             need_factor = false;
-            if (iter > 0)
+            if (iter > 0) {
                 for (int i = tid; i < m; i += T4) p.y[b * m + i] = L.ys[i];
+                __syncthreads();  // every ys read is done before factorize_w4's E tiles overwrite it
+            }
             const bool ok = factorize_nl<T4>(p.self, b, rho, Sg);
             if (!ok) {
                 if (iter == 0) {

@@ -562,3 +562,21 @@ def test_osqp_demo_known_answer(eps):
     tol = 5e-3 if eps > 1e-6 else 1e-7
     assert np.abs(rg.x - xs).max() < tol
     assert np.abs(rg.y - ys).max() < 10 * tol
+
+
+@pytest.mark.parametrize("cfg,B", [(2, 1024), (3, 512)])
+def test_repeat_solves_are_bitwise_identical(cfg, B):
+    """The same batch solved on three fresh handles gives bitwise identical outputs: no
+    result may depend on the timing of the waves inside a workgroup.  (A missing barrier
+    between the y park and the factorisation's scratch made one instance in ~4 runs of
+    cfg 2 drift by 1e-5 in the four-wave kernel before it was fixed.)"""
+    b = mpc.make_batch(cfg, B=B)
+    s = dict(warm_start=True)
+    outs = []
+    for _ in range(3):
+        bg = OSQPBatch()
+        bg.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
+        outs.append(bg.solve())
+    for r in outs[1:]:
+        assert np.array_equal(r.x, outs[0].x) and np.array_equal(r.y, outs[0].y)
+        assert np.array_equal(r.iter, outs[0].iter)
