@@ -286,11 +286,47 @@ def test_settings_paths_match_oracle(settings):
     _batch_parity(b, s)
 
 
-@pytest.mark.parametrize("B", [1, 3])
-def test_tiny_batches(B):
-    """Batches smaller than a wave of instances (one and three QPs)."""
-    b = mpc.make_batch(3, B=B, seed=11)
+@pytest.mark.parametrize("cfg,B", [(3, 1), (3, 3), (2, 1), (2, 3)])
+def test_tiny_batches(cfg, B):
+    """Batches smaller than a wave of instances (one and three QPs), for the slack
+    layout's register-sweep kernel and the vanilla layout's four-wave kernel."""
+    b = mpc.make_batch(cfg, B=B, seed=11)
     _batch_parity(b, dict(warm_start=True), min_match=1.0)
+
+
+def test_cfg2_warm_resolves_after_updates():
+    """The four-wave kernel's warm path: the batch solved, then update(l, u) with the
+    initial states moved (a receding-horizon step) and solved again from the previous
+    x, z, y -- three times, each against the oracle doing the same."""
+    b = mpc.make_batch(2, B=64, seed=5)
+    s = dict(warm_start=True)
+    P, A = b["P"], b["A"]
+    dev = OSQPBatch()
+    dev.setup(P, b["q"], A, b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
+    orc = []
+    for k in range(b["Px"].shape[0]):
+        o = pyoracle.OSQP()
+        Pk, Ak = P.copy(), A.copy()
+        Pk.data, Ak.data = b["Px"][k].copy(), b["Ax"][k].copy()
+        o.setup(Pk, b["q"][k], Ak, b["l"][k], b["u"][k], **s)
+        orc.append(o)
+    rng = np.random.default_rng(7)
+    l, u = b["l"].copy(), b["u"].copy()
+    for step in range(3):
+        if step:
+            x0 = -l[:, :4] + rng.uniform(-0.02, 0.02, (l.shape[0], 4))
+            l[:, :4] = -x0
+            u[:, :4] = -x0
+            dev.update(l=l, u=u)
+            for k, o in enumerate(orc):
+                o.update(l=l[k], u=u[k])
+        rd = dev.solve()
+        ro = [o.solve() for o in orc]
+        it = np.array([r.info.iter for r in ro])
+        assert np.mean(rd.iter == it) >= 0.99
+        same = rd.iter == it
+        du = np.array([np.abs(rd.x[k, b["u_block"]] - ro[k].x[b["u_block"]]).max() for k in range(len(ro))])
+        assert np.all(du[same] < U_TOL), du.max()
 
 
 @pytest.mark.parametrize("cfg,B", [(2, 1024), (3, 1024), (5, 320)])
