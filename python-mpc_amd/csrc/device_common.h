@@ -261,14 +261,31 @@ __device__ __forceinline__ void block_max_sum_tr(double (&v)[K], double (&sm)[KS
         for (int k = 0; k < KS; ++k) rs[wid * KS + k] = s[k];
     }
     __syncthreads();
+    if constexpr (NW > 4) {
+        // eight waves: thread k < K folds value k over the waves first (every thread
+        // loading all K x NW partials would hold them all in registers at once)
+        double* const fin = rs + NW * KS;
+        if ((int)threadIdx.x < K) {
+            const int k = threadIdx.x, b0 = k >= K1, r1 = k - K1 * b0, b1 = r1 >= K2, j = r1 - K2 * b1;
+            const double* src = red + ((b0 + 2 * b1) * K2 + j) * NW;
+            double r = src[0];
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const int b0 = k >= K1, r1 = k - K1 * b0, b1 = r1 >= K2, j = r1 - K2 * b1;
-        const double* src = red + ((b0 + 2 * b1) * K2 + j) * NW;
-        double r = src[0];
+            for (int w = 1; w < NW; ++w) r = vmax(r, src[w]);
+            fin[k] = r;
+        }
+        __syncthreads();
 #pragma unroll
-        for (int w = 1; w < NW; ++w) r = vmax(r, src[w]);
-        v[k] = r;
+        for (int k = 0; k < K; ++k) v[k] = fin[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int b0 = k >= K1, r1 = k - K1 * b0, b1 = r1 >= K2, j = r1 - K2 * b1;
+            const double* src = red + ((b0 + 2 * b1) * K2 + j) * NW;
+            double r = src[0];
+#pragma unroll
+            for (int w = 1; w < NW; ++w) r = vmax(r, src[w]);
+            v[k] = r;
+        }
     }
 #pragma unroll
     for (int k = 0; k < KS; ++k) {

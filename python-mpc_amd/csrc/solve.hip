@@ -718,6 +718,13 @@ bool variant_fits(const KParams& p, int v) {
         case 17:  // four waves, two workgroups per CU (two waves per SIMD): up to 80 KB of LDS each
             return p.nb == 4 && p.amax <= 8 && p.gk <= 6 && p.pk <= 4 && p.m <= 256 && p.npad <= 128 &&
                    p.nnzA <= 512 && p.nnzP <= 256 && lds_w2_bytes(p) <= 80 * 1024;
+        case 18: {  // eight waves, one workgroup per CU; the gather lists pack 16-bit LDS addresses
+            KParams q2 = p;
+            q2.mode = 2;  // the LDS carve of mode 2 (fits may run before KParams::mode is set)
+            const long mp = solve_mpad(p.m), packed = 8L * (al2(p.nnzA + 1) + al2(p.nnzP + 1) + 4 * mp + 4L * p.npad);
+            return p.nb == 8 && p.amax <= 12 && p.gk <= 8 && p.pk <= 8 && p.m <= 512 && p.npad <= 256 &&
+                   packed < 65536 && lds_solve_bytes(q2) <= 160 * 1024;
+        }
         case 16:  // dense inverse: one variable per lane pair of a 256-thread workgroup, packed LDS addresses
             return p.n <= kDenseR && p.npad <= 128 && p.gk <= 6 && p.pk <= 4 && p.m <= 2 * 128 &&
                    lds_dense_bytes(p) < 65536;
@@ -726,7 +733,7 @@ bool variant_fits(const KParams& p, int v) {
 }
 
 int solve_variant(const KParams& p) {
-    static const int order[] = {17, 10, 8, 9, 0, 1, 2, 3, 11, 12, 13, 4, 5, 6};  // 14, 16: MPCQP_VARIANT only
+    static const int order[] = {17, 10, 8, 9, 0, 1, 2, 3, 11, 12, 13, 4, 5, 6};  // 14, 16, 18: MPCQP_VARIANT only
     for (int v : order)
         if (variant_fits(p, v)) return v;
     return -1;
@@ -740,13 +747,14 @@ int solve_threads(int variant) {
         case 14: return 128;
         case 16: return 256;
         case 17: return 256;
+        case 18: return 512;
         default: return T;
     }
 }
 
 int solve_mode(int variant) {  // what factorize stores for the variant (KParams::mode)
     switch (variant) {
-        case 0: case 8: case 9: case 10: case 17: return 2;
+        case 0: case 8: case 9: case 10: case 17: case 18: return 2;
         case 1: case 2: case 3: case 7: case 16: return 1;  // (16: no factor stored; dx aliases rb)
         case 11: case 12: case 13: case 14: return 3;  // two-sided factor (solve_big.hip)
         default: return 0;
@@ -765,7 +773,7 @@ static hipError_t launch_solve_only(const KParams& p, long B, double* xo, double
         case 5: return go<0, 32, 8, 4, 4, 2>(p, B, xo, yo, factor_only, st, lds, ref);
         case 6: return go<0, 32, 16, 8, 8, 1>(p, B, xo, yo, factor_only, st, lds, ref);
         case 7: return go<4, 8, 6, 1, 1, 4, false>(p, B, xo, yo, factor_only, st, lds, ref);
-        case 8: case 9: case 10: case 17: return launch_solve_wave(p, B, xo, yo, factor_only, st, ref);
+        case 8: case 9: case 10: case 17: case 18: return launch_solve_wave(p, B, xo, yo, factor_only, st, ref);
         case 16: return launch_solve_dense(p, B, xo, yo, factor_only, st, ref);
         case 11: case 12: case 13: case 14: return launch_solve_big(p, B, xo, yo, factor_only, st, ref);
         default: return hipErrorInvalidValue;

@@ -587,6 +587,100 @@ __device__ __forceinline__ bool factorize_w4(const KP& p, SLds& L, const double 
     return okf[0] > 0.5 && okf[1] > 0.5 && okf[2] > 0.5 && okf[3] > 0.5;
 }
 
+__host__ __device__ inline double* w8_gpair(double* Fg, double* Hg, int amax, int q);  // (below)
+
+// The eight-wave kernel's factorisation (solve_wave.hip::k_solve_w8, variant 18: mode 2,
+// nb = 8, amax <= 12; TT = 512): factorize_w4 with eight blocks -- stage 1 pre-pivots all
+// eight at once (wave k: block k), then the k = 1..7 chain: F_k = E_k S_{k-1}^{-1}
+// (G_{k,k-1} = -F_k), wave 0 forms the corner and pivots it (gj_seg<2>, rolled: amax may
+// exceed 8) while waves 1-7 form G_kj = -F_k G_{k-1,j}, j < k-1, reading G_{k-1,j} back
+// from Hg (written by this workgroup one step earlier).  Outputs as factorize's mode 2;
+// the tiles Sg lie in V past the scratch (w8_toff).
+template <class KP>
+__device__ __forceinline__ bool factorize_w8(const KP& p, SLds& L, const double rho, double* __restrict__ Fg,
+                                             double* __restrict__ Hg, double* __restrict__ Sg) {
+    constexpr int NB = 8, TT = 512;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int amax = p.amax, as = amax * S;
+    double* const V = L.SP;
+    double* const dl = V + (2 * NB - 1) * as;   // amax x amax, row stride 16
+    double* const bufw = dl + 256 + w * 2 * S;  // the wave's Gauss-Jordan publish buffers
+    double* const okf = dl + 256 + NB * 2 * S;
+    auto Ek = [&](int k) __attribute__((always_inline)) { return V + k * as; };
+    auto Fk = [&](int k) __attribute__((always_inline)) { return V + (NB - 1 + k) * as; };
+    auto G = [&](int q) __attribute__((always_inline)) { return w8_gpair(Fg, Hg, amax, q); };
+    auto wave_sync = []() __attribute__((always_inline)) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+#ifdef MPCQP_PHASE_PROF
+    long long tf = clock64();
+#define FPH(k) if (tid == 0) { const long long t_ = clock64(); L.pacc[k] += t_ - tf; tf = t_; }
+#else
+#define FPH(k)
+#endif
+    assemble_block<false, true>(p, L, rho, w, Sg + (long)w * SS, Ek(w), lane, 64, wave_sync);
+    wave_sync();
+    FPH(8)
+    bool okw = gj_seg<1>(Sg + (long)w * SS, bufw, w ? amax : 0, p.bsize[w], nullptr);
+    FPH(10)
+    __syncthreads();
+    FPH(11)
+#pragma unroll 1
+    for (int k = 1; k < NB; ++k) {
+        const double* Sp = Sg + (long)(k - 1) * SS;
+        const double* E = Ek(k);
+        double* F = Fk(k);
+        const int l0 = p.toff[k - 1], bmax = p.bmax;
+        for (int o = tid; o < as; o += TT) {
+            const int r = o >> 5, j = o & (S - 1);
+            double sacc = 0.0;
+#pragma unroll 4
+            for (int l = l0; l < l0 + bmax; ++l) sacc += E[r * S + l] * Sp[l * S + j];
+            F[o] = sacc;
+            G(k * (k - 1) / 2 + k - 1)[o] = -sacc;
+        }
+        __syncthreads();
+        FPH(9)
+        if (w == 0) {
+            for (int o = lane; o < amax * amax; o += 64) {  // S_k = D_k - F_k E_k' on the corner
+                const int r = o / amax, c = o - r * amax;
+                double sacc = 0.0;
+#pragma unroll 4
+                for (int l = l0; l < l0 + bmax; ++l) sacc += F[r * S + l] * E[c * S + l];
+                dl[r * 16 + c] = -sacc;
+            }
+            wave_sync();
+            okw = gj_seg<2, true>(Sg + (long)k * SS, bufw, amax, p.bsize[k], dl) && okw;
+        } else {
+#pragma unroll 1
+            for (int j = 0; j < k - 1; ++j) {
+                const bool adj = j == k - 2;
+                const double* Gp = adj ? Fk(k - 1) : G((k - 1) * (k - 2) / 2 + j);
+                const double sg = adj ? 1.0 : -1.0;
+                for (int o = tid - 64; o < as; o += TT - 64) {
+                    const int r = o >> 5, c = o & (S - 1);
+                    double sacc = 0.0;
+#pragma unroll 4
+                    for (int l = 0; l < amax; ++l) sacc += F[r * S + l] * Gp[l * S + c];
+                    G(k * (k - 1) / 2 + j)[o] = sg * sacc;
+                }
+            }
+        }
+        __syncthreads();
+        FPH(11)
+    }
+    if (lane == 0) okf[w] = okw ? 1.0 : 0.0;
+    __syncthreads();
+    FPH(9)
+#undef FPH
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < NB; ++k) ok = ok && okf[k] > 0.5;
+    return ok;
+}
+
 // The 256-thread register-sweep kernels' factorisation (mode 1: F_k rows < amax and
 // S_k^{-1} to the workspace; amax <= 16), split like factorize_w2 but on workspace
 // tiles, since their LDS has no room for a tile per wave:
@@ -704,6 +798,9 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
     if constexpr (TT == 256 && !POL) {  // the register-sweep kernels (variants 1-3), the four-wave kernel (17)
         if (p.mode == 1 && p.amax <= 16) return factorize_g(p, L, rho, Fg, Sg);
         if (p.variant == 17 && p.mode == 2 && p.nb == 4 && p.amax <= 8) return factorize_w4(p, L, rho, Hg, Sg);
+    }
+    if constexpr (TT == 512 && !POL) {  // the eight-wave kernel (18)
+        if (p.variant == 18 && p.mode == 2 && p.nb == 8 && p.amax <= 12) return factorize_w8(p, L, rho, Fg, Hg, Sg);
     }
     const int tid = threadIdx.x;
     const int nb = p.nb, amax = p.amax, mode = POL ? 1 : p.mode;
@@ -889,13 +986,33 @@ struct Res {  // update_info results
 // V holds the per-iteration vectors, then (mode 2) an LDS copy of the G blocks for
 // the wave kernel; the factorisation's three scratch tiles alias all of it.
 __host__ __device__ inline long solve_glen(int nb, int amax, int mode) {
-    return mode == 2 ? ((long)nb * (nb - 1) / 2 + 1) * (amax > 8 ? amax : 8) * S : 0;  // rows padded to >= 8, + a zero pair
+    // rows padded to >= 8 (nb = 4) or to 12 (nb = 8, the eight-wave kernel), + a zero pair
+    return mode == 2 ? ((long)nb * (nb - 1) / 2 + 1) * (nb > 4 ? 12 : (amax > 8 ? amax : 8)) * S : 0;
+}
+// The eight-wave kernel (variant 18: mode 2, nb = 8, amax <= 12) keeps everything in V:
+// its factorisation scratch at [0, w8_toff), the S_k^{-1} tiles after it, and its
+// reduction buffer (256) at w8_roff.  The G copy (at 3 mp + 2 npad) overlaps the tiles:
+// it is filled once the tiles are in registers (solve_wave.hip::solve_w8_body).
+__host__ __device__ inline long w8_toff(int amax) { return (15L * amax * S + 256 + 16 * S + 64 + 63) & ~63L; }
+// pair q's G block (amax x 32) of one instance: the 28 pairs outgrow the instance's
+// H tiles (nb SS doubles) for amax > 9 and continue in its F tiles (unused in mode 2)
+__host__ __device__ inline double* w8_gpair(double* Fg, double* Hg, int amax, int q) {
+    const int gs = amax * S, nqh = 8 * SS / gs;
+    return q < nqh ? Hg + (long)q * gs : Fg + (long)(q - nqh) * gs;
+}
+__host__ __device__ inline long w8_roff(int m, int npad, int amax) {
+    const long t = w8_toff(amax) + 8L * SS, g = 3L * ((m + 63) & ~63) + 2L * npad + solve_glen(8, amax, 2);
+    return t > g ? t : g;
 }
 // row arrays are padded to whole waves (the wave kernel's rows i = lane + 64 s are
 // then all in range; padded rows are inert: l = u = 0, empty gather list)
 __host__ __device__ inline int solve_mpad(int m) { return (m + 63) & ~63; }
 __host__ __device__ inline long solve_vlen(int m, int npad, int nb, int amax, int mode) {
     const long a = 3L * solve_mpad(m) + 2L * npad + solve_glen(nb, amax, mode), b = 3L * SS;
+    if (mode == 2 && nb > 4) {
+        const long c = w8_roff(m, npad, amax) + 256;
+        return c > a ? c : a;
+    }
     return a > b ? a : b;
 }
 
@@ -1037,7 +1154,7 @@ __device__ __forceinline__ void update_info_ph(const KParams* gp, long b, double
         v[12] = cmax(v[12], fabs(aty));
         v[13] = cmax(v[13], fabs(px));
     }
-    double* r = c.L.red + 64;
+    double* r = c.L.red + (TT / 64 * 14 <= 64 ? 64 : 112);  // after the per-wave maxima
     block_max_to<TT>(v, c.L.red, r);
     if (tid == 0) {
         Res R;

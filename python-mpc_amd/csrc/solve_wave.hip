@@ -1518,6 +1518,500 @@ __global__ __launch_bounds__(T4, 2) void k_setup_solve_w4(KParams p, const doubl
     order_epilogue<T4>(p, (int*)sm);
 }
 
+
+// ---------------------------------------------------------------------------
+// Eight-wave variant (variant 18, k_solve_w8): the four-wave kernel's iteration for nb = 8
+// plans (the slack-variable MPC, SURVEY.md configs[2]/[3]): one 512-thread workgroup per
+// QP, wave k owns block k (lane (h, r): row r of S_k^{-1}, columns [16 h, 16 h + 16)), one
+// workgroup per CU.  The 28 G blocks (rows < 12) and the eight S_k^{-1} tiles do not fit
+// in LDS together, so the tiles live only during the factorisation: S^{-1} stays in
+// registers for the whole solve and the G copy reuses the tiles' LDS (solve_phases.h::
+// w8_toff).  Phase A: 16 rows x 4 lanes of 8 columns per wave; phase C: up to four pairs
+// per half.  MPCQP_VARIANT=18.
+constexpr int T8 = 512;
+
+template <int K, int KPK>
+__device__ __forceinline__ void solve_w8_body(const KParams& p, double* __restrict__ xo, double* __restrict__ yo) {
+    const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int h = lane >> 5, r = lane & 31, rr = lane >> 2, ch = lane & 3;
+    constexpr int NB = 8, NP = NB * (NB - 1) / 2;  // exactly eight blocks (solve.hip::variant_fits)
+    constexpr int QR = 12, GR = 12;                 // G rows summed (amax <= 12) / per pair in gl
+    static_assert(K % 2 == 0, "the rhs splits the column list over the half-waves");
+    constexpr int KH = K / 2;                       // column-list entries per half in the rhs
+    const long b = instance_of(p);
+    const int n = p.n, m = p.m, npad = p.npad, nnzP = p.nnzP, nnzA = p.nnzA;
+    SL2 C = carve(p);
+    SLds& L = C.L;
+    double* const Hg = p.H + b * (long)p.nb * SS;
+    double* const Fg = p.F + b * (long)p.nb * SS;  // the G pairs past H's room (w8_gpair)
+    double* const Sg = L.SP + w8_toff(p.amax);                    // S_k^{-1} tiles (in V, past the factor scratch)
+    double* const red8 = L.SP + w8_roff(p.m, p.npad, p.amax);     // the inline check's reduction buffer
+
+    if (p.err[b]) {
+        for (int j = tid; j < n; j += T8) if (xo) xo[b * n + j] = __builtin_nan("");
+        for (int i = tid; i < m; i += T8) if (yo) yo[b * m + i] = __builtin_nan("");
+        if (tid == 0) fail_status(p, b);
+        return;
+    }
+#ifdef MPCQP_PHASE_PROF
+    long long tph = 0, t0c = 0, t0w = 0;
+    const bool prof = p.prof != nullptr;
+    if (prof) { t0w = wall_clock64(); t0c = tph = clock64(); if (tid < 16) L.pacc[tid] = 0; }
+#define PH(k) if (prof && tid == 0) { const long long t_ = clock64(); L.pacc[k] += t_ - tph; tph = t_; }
+#else
+#define PH(k)
+#endif
+    const double cval = p.scal[b * 4 + 0], cinv = p.scal[b * 4 + 1];
+    double rho = p.scal[b * 4 + 2];
+    const double sigma = p.sigma, alpha = p.alpha;
+    const bool warm = p.warm_start != 0;
+    for (int e = tid; e < nnzA; e += T8) L.Acsc[e] = p.Ax[b * nnzA + e];
+    if (tid == 0) L.Acsc[nnzA] = 0.0;
+    for (int v = tid; v < nnzP; v += T8) L.Pv[v] = p.Px[b * nnzP + v];
+    if (tid == 0) L.Pv[nnzP] = 0.0;
+    const int mp = solve_mpad(m);
+    for (int i = tid; i < mp; i += T8) {
+        const bool in = i < m;
+        L.lo[i] = in ? p.l[b * m + i] : 0.0;
+        L.up[i] = in ? p.u[b * m + i] : 0.0;
+        L.ct[i] = in ? p.ct[b * m + i] : 0;
+        C.Z[i] = (in && warm) ? p.z[b * m + i] : 0.0;
+    }
+    for (int pc = tid; pc < npad; pc += T8) {
+        L.qv[pc] = p.q[b * npad + pc];
+        C.X[pc] = warm ? p.x[b * npad + pc] : 0.0;
+    }
+    if (tid < 16) L.cor[tid] = 0.0;        // c_0 = 0 (block 0 has no correction)
+    if (tid < 16) L.cor[128 + tid] = 0.0;  // the upper half's zero correction row (phase B)
+    if (tid < 16) L.res[tid] = 0.0;
+    if (tid < 4) L.flag[tid] = 0;
+
+    int status = MPCQP_UNSOLVED_, rho_updates = 0, iter = 0, info_iter = 0;
+    bool can_check = false, need_factor = true;
+    const int pc = w * S + r;  // the lane's column (both halves; the lower half stores)
+    const bool low = h == 0;
+    const unsigned abase = lds_addr(L.Acsc), wbase = lds_addr(L.w), xbase = lds_addr(L.xt);
+    const unsigned Xbase = lds_addr(C.X);
+    bool cv = false;
+    double Dv = 1.0, Ev = 1.0;
+    GatherW<K> cg, rg;
+    GatherW<KPK> pg;
+    const int ri = min(tid, mp - 1);  // lanes past the padded rows repeat the inert last row
+    double SB[16];                    // row r of S_w^{-1}, columns [16 h, 16 h + 16): kept across runs
+#pragma unroll
+    for (int c = 0; c < 16; ++c) SB[c] = 0.0;
+    PH(5)
+    for (;;) {
+        __syncthreads();
+        if (need_factor) {
+            need_factor = false;
+            if (iter > 0) {
+                for (int i = tid; i < m; i += T8) p.y[b * m + i] = L.ys[i];
+                __syncthreads();  // every ys read is done before factorize_w4's E tiles overwrite it
+            }
+            const bool ok = factorize_nl<T8>(p.self, b, rho, Sg);
+            if (!ok) {
+                if (iter == 0) {
+                    for (int j = tid; j < n; j += T8) if (xo) xo[b * n + j] = __builtin_nan("");
+                    for (int i = tid; i < m; i += T8) if (yo) yo[b * m + i] = __builtin_nan("");
+                    if (tid == 0) fail_status(p, b);
+                    return;
+                }
+                status = MPCQP_NON_CVX_;
+                can_check = true;
+                break;
+            }
+            __syncthreads();
+            {
+                const double* src = Sg + (long)w * SS + r * S + 16 * h;
+#pragma unroll
+                for (int c = 0; c < 16; c += 2) ld2(src + c, SB[c], SB[c + 1]);
+            }
+            __syncthreads();  // the tiles are in registers: the G copy overwrites them
+            const bool have_y = iter > 0 || warm;
+            for (int i = tid; i < mp; i += T8) L.ys[i] = (have_y && i < m) ? p.y[b * m + i] : 0.0;
+            for (int o = tid; o < (NP + 1) * GR * S; o += T8) {
+                const int q = o / (GR * S), t = (o >> 5) - q * GR;
+                L.gl[o] = (q < NP && t < p.amax) ? w8_gpair(Fg, Hg, p.amax, q)[t * S + (o & 31)] : 0.0;
+            }
+            cv = low && p.pad_var[pc] >= 0;
+            cg.load(p.gcol + pc, npad, abase, wbase);
+            pg.load(p.gpsym + pc, npad, lds_addr(L.Pv), Xbase);
+            Dv = p.D[b * npad + pc];
+            Ev = ri < m ? p.E[b * m + ri] : 1.0;
+            if (ri < m) rg.load(p.grow + ri, m, abase, xbase);  // by ri: duplicate lanes repeat its row
+            else rg.clear(abase + 8u * nnzA, xbase);
+            PH(0)
+        }
+        // ---- run state ----
+        double X = C.X[pc], DX = 0.0;
+        const double Q = L.qv[pc];
+        // phase-C slots: the pairs (j, w), j > w, alternate over the halves (the i-th to half
+        // i & 1); the wave runs NSW(w) slots, a half without a pair there reads the zero pair
+        constexpr int NS = (NB - 1 + 1) / 2;
+        const int nsw = (NB - w) >> 1;  // ceil((NB - 1 - w) / 2)
+        unsigned gslot[NS], tslot[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const int j = w + 1 + 2 * s + h;
+            const bool v = j < NB;
+            gslot[s] = lds_addr(L.gl + (v ? j * (j - 1) / 2 + w : NP) * GR * S + r);
+            tslot[s] = lds_addr(L.tv + (v ? j : 0) * 16);
+        }
+        // the half's share of the column list (KH entries; the list is zero-padded to K)
+        GatherW<KH> ch2;
+#pragma unroll
+        for (int k = 0; k < KH; ++k) ch2.e[k] = h ? cg.e[k + KH] : cg.e[k];
+        const double r_hi = RHO_EQ_OVER_RHO_INEQ * rho;
+        double y = L.ys[ri], Z = C.Z[ri], dy = 0.0;
+        const signed char cl = L.ct[ri];
+        const double rv = cl < 0 ? RHO_MIN : (cl > 0 ? r_hi : rho);
+        const double rvi = cl < 0 ? 1.0 / RHO_MIN : (cl > 0 ? 1.0 / r_hi : 1.0 / rho);
+        __syncthreads();
+        L.w[ri] = rv * Z - y;
+        int stop_at = p.max_iter;
+        if (p.check_term) stop_at = min(stop_at, (iter / p.check_term + 1) * p.check_term);
+        if (p.adaptive_rho && p.rho_interval) stop_at = min(stop_at, (iter / p.rho_interval + 1) * p.rho_interval);
+        __syncthreads();
+        PH(5)
+        double* const cw = L.cor + w * 16;                  // c_w rows < QR
+        const double* const cwh = L.cor + (h ? 128 : w * 16);  // the half's correction (upper half: zeros)
+        while (iter < stop_at) {
+            ++iter;
+            // rhs = sigma x_prev - q + A' (rho z_prev - y), column pc: the lower half sums
+            // the list's first KH entries, the upper half the rest, one permlane32 swap
+            {
+                double av[KH], wv[KH];
+#pragma unroll
+                for (int k = 0; k < KH; ++k) {
+                    av[k] = lds_at(ch2.e[k] & 0xFFFFu);
+                    wv[k] = lds_at(ch2.e[k] >> 16);
+                }
+                double v = low ? sigma * X - Q : 0.0;
+#pragma unroll
+                for (int k = 0; k < KH; ++k) v += av[k] * wv[k];
+                const unsigned vlo = (unsigned)__double2loint(v), vhi = (unsigned)__double2hiint(v);
+                const auto l2 = __builtin_amdgcn_permlane32_swap(vlo, vlo, false, false);
+                const auto h2 = __builtin_amdgcn_permlane32_swap(vhi, vhi, false, false);
+                const double v0 = __hiloint2double((int)h2[0], (int)l2[0]);
+                const double v1 = __hiloint2double((int)h2[1], (int)l2[1]);
+                if (low) L.rb[pc] = cv ? v0 + v1 : 0.0;
+            }
+            __syncthreads();
+            PH(1)
+            // A: c_w = sum_{j<w} G_wj b_j (rows rr < QR: 16 rows x 4 lanes of 8 columns), wave w only
+            if (w > 0) {
+                const double* gq = L.gl + (w * (w - 1) / 2) * GR * S + min(rr, GR - 1) * S + 8 * ch;
+                double acc = 0.0;
+#pragma unroll
+                for (int j = 0; j < NB - 1; ++j) {
+                    if (j < w) {
+                        double bj[8], ga[8];
+#pragma unroll
+                        for (int e = 0; e < 8; e += 2) {
+                            ld2(L.rb + j * S + 8 * ch + e, bj[e], bj[e + 1]);
+                            ld2(gq + j * GR * S + e, ga[e], ga[e + 1]);
+                        }
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) acc += ga[e] * bj[e];
+                    }
+                }
+                acc += dpp<0xB1>(acc);
+                acc += dpp<0x4E>(acc);
+                if (ch == 0 && rr < QR) cw[rr] = acc;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            PH(12)
+            // B: t_w[r] = S_w^{-1}[r] (b_w + c_w): half-row sums, permlane32 swap
+            double t;
+            {
+                constexpr int QE = (QR + 1) & ~1;  // c_w's nonzero rows (< amax), read in pairs
+                double v[16], cc[QE];
+#pragma unroll
+                for (int c = 0; c < 16; c += 2) ld2(L.rb + w * S + 16 * h + c, v[c], v[c + 1]);
+#pragma unroll
+                for (int c = 0; c < QE; c += 2) ld2(cwh + c, cc[c], cc[c + 1]);
+#pragma unroll
+                for (int c = 0; c < QR; ++c) v[c] += cc[c];
+                double a[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int c = 0; c < 16; ++c) a[c & 3] += SB[c] * v[c];
+                const double th = (a[0] + a[1]) + (a[2] + a[3]);
+                const unsigned lo = (unsigned)__double2loint(th), hi = (unsigned)__double2hiint(th);
+                const auto l2 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+                const auto h2 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+                const double t0 = __hiloint2double((int)h2[0], (int)l2[0]);  // lower half's
+                const double t1 = __hiloint2double((int)h2[1], (int)l2[1]);  // upper half's
+                t = t0 + t1;
+                if (low && r < QR) L.tv[w * 16 + r] = t;
+            }
+            __syncthreads();
+            PH(13)
+            // C: x~_w[r] = t + sum_s G_{pair_s}[q][r] t_{j_s}[q]  (slots split over the halves;
+            // rows q < QR: the G blocks are zero from row amax on)
+            {
+                double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+                for (int s = 0; s < NS; ++s) {
+                    if (s < nsw) {
+                        double gv[QR], tq[QR];
+#pragma unroll
+                        for (int q = 0; q < QR; ++q) gv[q] = lds_at(gslot[s] + q * S * 8);
+#pragma unroll
+                        for (int q = 0; q < QR; q += 2) lds_at2(tslot[s] + q * 8, tq[q], tq[q + 1]);
+#pragma unroll
+                        for (int q = 0; q < QR; q += 2) {
+                            a0 += gv[q] * tq[q];
+                            a1 += gv[q + 1] * tq[q + 1];
+                        }
+                    }
+                }
+                const double d = a0 + a1;
+                const unsigned lo = (unsigned)__double2loint(d), hi = (unsigned)__double2hiint(d);
+                const auto l2 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+                const auto h2 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+                const double d0 = __hiloint2double((int)h2[0], (int)l2[0]);
+                const double d1 = __hiloint2double((int)h2[1], (int)l2[1]);
+                const double xn = t + (d0 + d1);
+                if (low) L.xt[pc] = xn;
+                const double xnew = alpha * xn + (1.0 - alpha) * X;
+                DX = xnew - X;
+                X = xnew;
+            }
+            __syncthreads();
+            PH(14)
+            // rows: z~ = A x~ ; relaxed + projected z ; y ; next w
+            {
+                double av[K], xv[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    av[k] = lds_at(rg.e[k] & 0xFFFFu);
+                    xv[k] = lds_at(rg.e[k] >> 16);
+                }
+                const double lo = L.lo[ri], up = L.up[ri];
+                double zt = av[0] * xv[0];
+#pragma unroll
+                for (int k = 1; k < K; ++k) zt += av[k] * xv[k];
+                const double zr = alpha * zt + (1.0 - alpha) * Z;
+                const double zn = __builtin_fmin(__builtin_fmax(zr + rvi * y, lo), up);
+                const double dd = rv * (zr - zn);
+                Z = zn;
+                dy = dd;
+                y += dd;
+                L.w[ri] = rv * zn - y;
+            }
+            __syncthreads();
+            PH(3)
+        }
+        // run state back to LDS
+        if (low) { C.X[pc] = X; L.dx[pc] = DX; }
+        L.ys[ri] = y; C.Z[ri] = Z; C.dY[ri] = dy;
+        __syncthreads();
+        can_check = p.check_term && (iter % p.check_term == 0);
+        const bool do_rho = p.adaptive_rho && p.rho_interval && (iter % p.rho_interval == 0);
+        if (!can_check && !do_rho) break;
+        info_iter = iter;
+        bool stop = false;
+        {
+            // inline update_info + check_termination (as solve_w2_body's), one row per thread
+            const bool unscale = p.scaling && !p.scaled_term;
+            const unsigned ysbase = lds_addr(L.ys), dYbase = lds_addr(C.dY), dxbase = lds_addr(L.dx);
+            double mx[17], sm[2] = {0.0, 0.0}, adx = 0.0;
+#pragma unroll
+            for (int k = 0; k < 17; ++k) mx[k] = 0.0;
+            {
+                const bool ok = tid < m;
+                double ax = 0.0, ad = 0.0;
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const unsigned e = rg.e[k], va = e >> 16;
+                    const double a = lds_at(e & 0xFFFFu);
+                    ax += a * lds_at(va - xbase + Xbase);
+                    ad += a * lds_at(va - xbase + dxbase);
+                }
+                adx = ad;
+                const double zi = Z, pr = ax - zi, ei = 1.0 / Ev;
+                const double lo = L.lo[ri], up = L.up[ri];
+                double d = dy;
+                if (up > OSQP_INFTY * MIN_SCALING) d = (lo < -OSQP_INFTY * MIN_SCALING) ? 0.0 : cmin(d, 0.0);
+                else if (lo < -OSQP_INFTY * MIN_SCALING) d = cmax(d, 0.0);
+                if (ok) {
+                    mx[0] = fabs(ei * pr);
+                    mx[2] = fabs(ei * zi);
+                    mx[3] = fabs(ei * ax);
+                    mx[7] = fabs(pr);
+                    mx[9] = fabs(zi);
+                    mx[10] = fabs(ax);
+                    mx[14] = fabs(unscale ? Ev * d : d);
+                    sm[0] = up * cmax(d, 0.0) + lo * cmin(d, 0.0);
+                    C.dY[ri] = d;
+                }
+            }
+            {  // the lane's column (lower half): P x, A' y, P dx, and the delta x norm
+                double px = 0.0, pdx = 0.0, aty = 0.0;
+#pragma unroll
+                for (int k = 0; k < KPK; ++k) {
+                    const unsigned e = pg.e[k], va = e >> 16;
+                    const double pv = lds_at(e & 0xFFFFu);
+                    px += pv * lds_at(va);
+                    pdx += pv * lds_at(va - Xbase + dxbase);
+                }
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const unsigned e = cg.e[k];
+                    aty += lds_at(e & 0xFFFFu) * lds_at((e >> 16) - wbase + ysbase);
+                }
+                if (cv) {
+                    const double d = (Q + px) + aty, di = 1.0 / Dv;
+                    mx[1] = fabs(di * d);
+                    mx[4] = fabs(di * Q);
+                    mx[5] = fabs(di * aty);
+                    mx[6] = fabs(di * px);
+                    mx[8] = fabs(d);
+                    mx[11] = fabs(Q);
+                    mx[12] = fabs(aty);
+                    mx[13] = fabs(px);
+                    mx[15] = fabs(unscale ? Dv * DX : DX);
+                    mx[16] = fabs(unscale ? pdx * di : pdx);
+                }
+            }
+            if (tid < npad && p.pad_var[tid] >= 0) sm[1] = L.qv[tid] * L.dx[tid];
+            block_max_sum_tr<T8, 17, 2>(mx, sm, red8);
+            Res R;
+            if (unscale) {
+                R.pri = mx[0]; R.dua = cinv * mx[1];
+                R.nz = mx[2]; R.nax = mx[3]; R.nq = mx[4]; R.naty = mx[5]; R.npx = mx[6];
+            } else {
+                R.pri = mx[7]; R.dua = mx[8];
+                R.nz = mx[9]; R.nax = mx[10]; R.nq = mx[11]; R.naty = mx[12]; R.npx = mx[13];
+            }
+            R.rpri = mx[7]; R.rdua = mx[8]; R.rz = mx[9]; R.rax = mx[10]; R.rq = mx[11]; R.raty = mx[12]; R.rpx = mx[13];
+            if (m == 0) R.pri = 0.0;
+            if (tid == 0) R.save(L.res);
+            if (can_check) {
+                int st = MPCQP_UNSOLVED_;
+                double obj = 0.0;
+                bool done = false;
+                if (R.pri > OSQP_INFTY || R.dua > OSQP_INFTY) {
+                    st = MPCQP_NON_CVX_;
+                    obj = __builtin_nan("");
+                    done = true;
+                } else {
+                    const bool prim_ok = m == 0 || R.pri < p.eps_abs + p.eps_rel * cmax(R.nz, R.nax);
+                    double mxd = cmax(cmax(R.nq, R.naty), R.npx);
+                    if (unscale) mxd *= cinv;
+                    const bool dual_ok = R.dua < p.eps_abs + p.eps_rel * mxd;
+                    bool prim_inf = false, dual_inf = false;
+                    if (!prim_ok || !dual_ok) {
+                        const double norm_dy = mx[14], norm_dx = mx[15], epi = p.eps_pinf, edi = p.eps_dinf;
+                        const double cs = unscale ? cval : 1.0;
+                        if (!prim_ok && m != 0 && norm_dy > epi && sm[0] < epi * norm_dy) {
+                            __syncthreads();
+                            double na[1] = {0.0};
+                            double a = 0.0;
+#pragma unroll
+                            for (int k = 0; k < K; ++k) {
+                                const unsigned e = cg.e[k];
+                                a += lds_at(e & 0xFFFFu) * lds_at((e >> 16) - wbase + dYbase);
+                            }
+                            if (cv) na[0] = fabs(unscale ? a * (1.0 / Dv) : a);
+                            block_max<T8, 1>(na, L.red);
+                            prim_inf = na[0] < epi * norm_dy;
+                        }
+                        if (!dual_ok && norm_dx > edi && sm[1] < cs * edi * norm_dx && mx[16] < cs * edi * norm_dx) {
+                            bool viol = false;
+                            if (tid < m) {
+                                const double ar = unscale ? adx * (1.0 / Ev) : adx;
+                                const double lo = L.lo[ri], up = L.up[ri];
+                                if ((up < OSQP_INFTY * MIN_SCALING && ar > edi * norm_dx) ||
+                                    (lo > -OSQP_INFTY * MIN_SCALING && ar < -edi * norm_dx))
+                                    viol = true;
+                            }
+                            dual_inf = !block_any<T8>(viol, L.flag);
+                        }
+                    }
+                    if (prim_ok && dual_ok) {
+                        st = MPCQP_SOLVED_;
+                        done = true;
+                    } else if (prim_inf) {
+                        st = MPCQP_PRIMAL_INFEASIBLE_;
+                        obj = OSQP_INFTY;
+                        if (tid == 0) L.flag[3] = unscale;
+                        done = true;
+                    } else if (dual_inf) {
+                        st = MPCQP_DUAL_INFEASIBLE_;
+                        obj = -OSQP_INFTY;
+                        if (tid == 0) L.flag[2] = unscale;
+                        done = true;
+                    }
+                }
+                __syncthreads();
+                if (done && tid == 0) { L.flag[1] = st; L.res[14] = obj; }
+                __syncthreads();
+                status = done ? st : MPCQP_UNSOLVED_;
+                stop = done;
+            }
+        }
+        if (!stop && do_rho) {
+            Res R;
+            R.restore(L.res);
+            const double pr = R.rpri / (cmax(R.rz, R.rax) + DIVISION_TOL);
+            const double du = R.rdua / (cmax(cmax(R.rq, R.raty), R.rpx) + DIVISION_TOL);
+            double rn = rho * sqrt(pr / (du + DIVISION_TOL));
+            rn = cmin(cmax(rn, RHO_MIN), RHO_MAX);
+            if (rn > rho * p.rho_tol || rn < rho / p.rho_tol) {
+                rho = cmin(cmax(rn, RHO_MIN), RHO_MAX);
+                rho_updates++;
+                need_factor = true;
+            }
+        }
+        __syncthreads();
+        PH(4)
+        if (stop || iter >= p.max_iter) break;
+    }
+    if (!can_check && status == MPCQP_UNSOLVED_) {
+        update_info_nl<T8>(p.self, b, cinv);
+        info_iter = iter;
+        status = check_termination_nl<T8>(p.self, b, cval, cinv, 0);
+    }
+    const bool has_sol = !(status == MPCQP_PRIMAL_INFEASIBLE_ || status == MPCQP_PRIMAL_INFEASIBLE_INACCURATE_ ||
+                           status == MPCQP_DUAL_INFEASIBLE_ || status == MPCQP_DUAL_INFEASIBLE_INACCURATE_ ||
+                           status == MPCQP_NON_CVX_);
+    if (has_sol) objective_nl<T8>(p.self, cinv);
+    if (status == MPCQP_UNSOLVED_) {
+        status = check_termination_nl<T8>(p.self, b, cval, cinv, 1);
+        if (status == MPCQP_UNSOLVED_) status = MPCQP_MAX_ITER_REACHED_;
+    }
+    finalize_nl<T8>(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates, p.ostat, p.oiter);
+#ifdef MPCQP_PHASE_PROF
+    if (prof) {
+        __syncthreads();
+        PH(5)
+        if (tid == 0) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) p.prof[b * kProfSlots + k] = L.pacc[k];
+#pragma unroll
+            for (int k = 8; k < 15; ++k) p.prof[b * kProfSlots + k] = L.pacc[k];
+            p.prof[b * kProfSlots + 2] = L.pacc[12] + L.pacc[13] + L.pacc[14];
+            p.prof[b * kProfSlots + 6] = clock64() - t0c;
+            p.prof[b * kProfSlots + 7] = wall_clock64() - t0w;
+            p.prof[b * kProfSlots + 15] = t0w;
+        }
+    }
+#endif
+#undef PH
+}
+
+template <int K, int KPK>
+__global__ __launch_bounds__(T8, 1) void k_solve_w8(KParams p, double* __restrict__ xo, double* __restrict__ yo,
+                                                    int factor_only) {
+    solve_w8_body<K, KPK>(p, xo, yo);
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    order_epilogue<T8>(p, (int*)sm);
+}
+
 // the fused kernel's instantiation for the plan, or 0: variant 10 and the 128-thread
 // register-list setup shape (one padded column per thread, two rows, four A values)
 static int setup_solve_fits(const KParams& p) {
@@ -1593,6 +2087,14 @@ hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, i
             hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
             hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(T4), lds, st, p, xo, yo, factor_only);
+            return hipGetLastError();
+        }
+        case 18: {
+            auto k = k_solve_w8<8, 8>;
+            if (ref) { *ref = {(const void*)k, T8, lds}; return hipSuccess; }
+            hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(T8), lds, st, p, xo, yo, factor_only);
             return hipGetLastError();
         }
         case 10:  // slot-1 rows (>= 128) with at most one nonzero (cfg 2's box rows): K1 = 1

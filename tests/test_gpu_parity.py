@@ -251,13 +251,14 @@ def test_polish_batch_cfg2():
 
 
 @pytest.mark.parametrize("variant,cfg,B", [(11, 3, 256), (14, 3, 256), (12, 5, 64), (8, 2, 256), (16, 2, 256),
-                                             (10, 2, 1024), (17, 2, 1024)])
+                                             (10, 2, 1024), (17, 2, 1024), (18, 3, 256)])
 def test_alternative_kernel_variants(monkeypatch, variant, cfg, B):
     """Kernel instantiations that are not the default choice for a plan stay exact:
     the 512-thread two-sided kernel on the slack layout (variant 11), the two-wave
     two-sided kernel (14), the long-horizon kernel on cfg 5 (12), the one-wave
     kernel on cfg 2 (8), the dense-inverse kernel on cfg 2 (16), the two-wave kernel (10,
-    the default before the four-wave one) and the four-wave kernel (17) on cfg 2, selected
+    the default before the four-wave one) and the four-wave kernel (17) on cfg 2, the
+    eight-wave kernel (18) on the slack layout, selected
     with the MPCQP_VARIANT override."""
     monkeypatch.setenv("MPCQP_VARIANT", str(variant))
     b = mpc.make_batch(cfg, B=B)
