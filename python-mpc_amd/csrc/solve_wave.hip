@@ -1086,6 +1086,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
     GatherW<K> cg, rg;
     GatherW<KPK> pg;
     const int ri = min(tid, mp - 1);  // lanes past the padded rows repeat the inert last row
+    const bool rows_wave = w * 64 < mp;  // wave-uniform
     PH(5)
     for (;;) {
         __syncthreads();
@@ -1243,13 +1244,22 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
             // rows q < QR: the G blocks are zero from row amax on)
             {
                 constexpr int QE = (QR + 1) & ~1;  // t rows read in pairs
+                // the wave's slot count (wave 0: 2, waves 1-2: 1, wave 3: 0): slots no half
+                // of the wave has a pair for are skipped, not read as the zero pair (LDS
+                // return bandwidth is shared with the CU's other workgroup)
+                const int nsw = (NB - w) >> 1;
                 double gv[2][QE], tq[2][QE];
 #pragma unroll
                 for (int s = 0; s < 2; ++s) {
+                    if (s < nsw) {
 #pragma unroll
-                    for (int q = 0; q < QE; ++q) gv[s][q] = q < QR ? lds_at(gslot[s] + q * S * 8) : 0.0;
+                        for (int q = 0; q < QE; ++q) gv[s][q] = q < QR ? lds_at(gslot[s] + q * S * 8) : 0.0;
 #pragma unroll
-                    for (int q = 0; q < QE; q += 2) lds_at2(tslot[s] + q * 8, tq[s][q], tq[s][q + 1]);
+                        for (int q = 0; q < QE; q += 2) lds_at2(tslot[s] + q * 8, tq[s][q], tq[s][q + 1]);
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < QE; ++q) gv[s][q] = tq[s][q] = 0.0;
+                    }
                 }
                 double a0 = 0.0, a1 = 0.0;
 #pragma unroll
@@ -1273,8 +1283,9 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
             }
             __syncthreads();
             PH(14)
-            // rows: z~ = A x~ ; relaxed + projected z ; y ; next w
-            {
+            // rows: z~ = A x~ ; relaxed + projected z ; y ; next w (waves wholly past the
+            // padded rows skip it: their lanes would only repeat the inert last row)
+            if (rows_wave) {
                 double av[K], xv[K];
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
@@ -1298,7 +1309,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
         }
         // run state back to LDS
         if (low) { C.X[pc] = X; L.dx[pc] = DX; }
-        L.ys[ri] = y; C.Z[ri] = Z; C.dY[ri] = dy;
+        if (rows_wave) { L.ys[ri] = y; C.Z[ri] = Z; C.dY[ri] = dy; }
         __syncthreads();
         can_check = p.check_term && (iter % p.check_term == 0);
         const bool do_rho = p.adaptive_rho && p.rho_interval && (iter % p.rho_interval == 0);
