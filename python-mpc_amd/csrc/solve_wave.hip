@@ -1156,8 +1156,17 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
         GatherW<KH> ch2;
 #pragma unroll
         for (int k = 0; k < KH; ++k) ch2.e[k] = h ? cg.e[k + KH] : cg.e[k];
+        double ca[KH];  // the half's A values of the column (registers for the run)
+#pragma unroll
+        for (int k = 0; k < KH; ++k) ca[k] = lds_at(ch2.e[k] & 0xFFFFu);
         const double r_hi = RHO_EQ_OVER_RHO_INEQ * rho;
         double y = L.ys[ri], Z = C.Z[ri], dy = 0.0;
+        // the row's A values and bounds stay in registers for the run (fewer LDS returns
+        // per iteration; the CU's other workgroup shares them)
+        double av[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) av[k] = lds_at(rg.e[k] & 0xFFFFu);
+        const double rlo = L.lo[ri], rup = L.up[ri];
         const signed char cl = L.ct[ri];
         const double rv = cl < 0 ? RHO_MIN : (cl > 0 ? r_hi : rho);
         const double rvi = cl < 0 ? 1.0 / RHO_MIN : (cl > 0 ? 1.0 / r_hi : 1.0 / rho);
@@ -1175,15 +1184,12 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
             // rhs = sigma x_prev - q + A' (rho z_prev - y), column pc: the lower half sums
             // the list's first KH entries, the upper half the rest, one permlane32 swap
             {
-                double av[KH], wv[KH];
+                double wv[KH];
 #pragma unroll
-                for (int k = 0; k < KH; ++k) {
-                    av[k] = lds_at(ch2.e[k] & 0xFFFFu);
-                    wv[k] = lds_at(ch2.e[k] >> 16);
-                }
+                for (int k = 0; k < KH; ++k) wv[k] = lds_at(ch2.e[k] >> 16);
                 double v = low ? sigma * X - Q : 0.0;
 #pragma unroll
-                for (int k = 0; k < KH; ++k) v += av[k] * wv[k];
+                for (int k = 0; k < KH; ++k) v += ca[k] * wv[k];
                 const unsigned vlo = (unsigned)__double2loint(v), vhi = (unsigned)__double2hiint(v);
                 const auto l2 = __builtin_amdgcn_permlane32_swap(vlo, vlo, false, false);
                 const auto h2 = __builtin_amdgcn_permlane32_swap(vhi, vhi, false, false);
@@ -1286,13 +1292,10 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
             // rows: z~ = A x~ ; relaxed + projected z ; y ; next w (waves wholly past the
             // padded rows skip it: their lanes would only repeat the inert last row)
             if (rows_wave) {
-                double av[K], xv[K];
+                double xv[K];
 #pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    av[k] = lds_at(rg.e[k] & 0xFFFFu);
-                    xv[k] = lds_at(rg.e[k] >> 16);
-                }
-                const double lo = L.lo[ri], up = L.up[ri];
+                for (int k = 0; k < K; ++k) xv[k] = lds_at(rg.e[k] >> 16);
+                const double lo = rlo, up = rup;
                 double zt = av[0] * xv[0];
 #pragma unroll
                 for (int k = 1; k < K; ++k) zt += av[k] * xv[k];
