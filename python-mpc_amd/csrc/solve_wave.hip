@@ -1152,6 +1152,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 tslot[s] = lds_addr(L.tv + jj[s] * 8);
             }
         }
+        const int nsw = (NB - w) >> 1;  // phase-C slots of the wave (wave 0: 2, waves 1-2: 1, wave 3: 0)
         // the half's share of the column list (KH entries; the list is zero-padded to K)
         GatherW<KH> ch2;
 #pragma unroll
@@ -1170,8 +1171,28 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
         const signed char cl = L.ct[ri];
         const double rv = cl < 0 ? RHO_MIN : (cl > 0 ? r_hi : rho);
         const double rvi = cl < 0 ? 1.0 / RHO_MIN : (cl > 0 ? 1.0 / r_hi : 1.0 / rho);
-        __syncthreads();
-        L.w[ri] = rv * Z - y;
+        __syncthreads();  // (the G copy of a refactorisation is complete)
+        // phase A's G values (rows rr < 8 of G_wj, columns [4 ch, 4 ch + 4), j < w) in registers for the run
+        double ga[NB - 1][4];
+        {
+            const double* gq = L.gl + (w * (w - 1) / 2) * 8 * S + rr * S + 4 * ch;
+#pragma unroll
+            for (int j = 0; j < NB - 1; ++j) {
+                if (j < w) {
+                    ld2(gq + j * 8 * S, ga[j][0], ga[j][1]);
+                    ld2(gq + j * 8 * S + 2, ga[j][2], ga[j][3]);
+                } else {
+                    ga[j][0] = ga[j][1] = ga[j][2] = ga[j][3] = 0.0;
+                }
+            }
+        }
+        // phase C's G values (column r of the slots' pairs, rows < QR) in registers for the run
+        double gc[2][QR];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int q = 0; q < QR; ++q) gc[s][q] = s < nsw ? lds_at(gslot[s] + q * S * 8) : 0.0;
+        if (rows_wave) L.w[ri] = rv * Z - y;  // (lanes past the padded rows may hold a stale y)
         int stop_at = p.max_iter;
         if (p.check_term) stop_at = min(stop_at, (iter / p.check_term + 1) * p.check_term);
         if (p.adaptive_rho && p.rho_interval) stop_at = min(stop_at, (iter / p.rho_interval + 1) * p.rho_interval);
@@ -1201,18 +1222,15 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
             PH(1)
             // A: c_w = sum_{j<w} G_wj b_j (rows < 8), wave w only
             if (w > 0) {
-                const double* gq = L.gl + (w * (w - 1) / 2) * 8 * S + rr * S + 4 * ch;
                 double acc = 0.0;
 #pragma unroll
                 for (int j = 0; j < NB - 1; ++j) {
                     if (j < w) {
-                        double bj[4], ga[4];
+                        double bj[4];
                         ld2(L.rb + j * S + 4 * ch, bj[0], bj[1]);
                         ld2(L.rb + j * S + 4 * ch + 2, bj[2], bj[3]);
-                        ld2(gq + j * 8 * S, ga[0], ga[1]);
-                        ld2(gq + j * 8 * S + 2, ga[2], ga[3]);
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) acc += ga[e] * bj[e];
+                        for (int e = 0; e < 4; ++e) acc += ga[j][e] * bj[e];
                     }
                 }
                 cw[rr] = reduce8(acc);
@@ -1253,13 +1271,12 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 // the wave's slot count (wave 0: 2, waves 1-2: 1, wave 3: 0): slots no half
                 // of the wave has a pair for are skipped, not read as the zero pair (LDS
                 // return bandwidth is shared with the CU's other workgroup)
-                const int nsw = (NB - w) >> 1;
                 double gv[2][QE], tq[2][QE];
 #pragma unroll
                 for (int s = 0; s < 2; ++s) {
                     if (s < nsw) {
 #pragma unroll
-                        for (int q = 0; q < QE; ++q) gv[s][q] = q < QR ? lds_at(gslot[s] + q * S * 8) : 0.0;
+                        for (int q = 0; q < QE; ++q) gv[s][q] = q < QR ? gc[s][q] : 0.0;
 #pragma unroll
                         for (int q = 0; q < QE; q += 2) lds_at2(tslot[s] + q * 8, tq[s][q], tq[s][q + 1]);
                     } else {
@@ -1611,6 +1628,7 @@ __device__ __forceinline__ void solve_w8_body(const KParams& p, double* __restri
     GatherW<K> cg, rg;
     GatherW<KPK> pg;
     const int ri = min(tid, mp - 1);  // lanes past the padded rows repeat the inert last row
+    const bool rows_wave = w * 64 < mp;  // wave-uniform: waves wholly past the padded rows skip the rows
     double SB[16];                    // row r of S_w^{-1}, columns [16 h, 16 h + 16): kept across runs
 #pragma unroll
     for (int c = 0; c < 16; ++c) SB[c] = 0.0;
@@ -1682,7 +1700,7 @@ __device__ __forceinline__ void solve_w8_body(const KParams& p, double* __restri
         const double rv = cl < 0 ? RHO_MIN : (cl > 0 ? r_hi : rho);
         const double rvi = cl < 0 ? 1.0 / RHO_MIN : (cl > 0 ? 1.0 / r_hi : 1.0 / rho);
         __syncthreads();
-        L.w[ri] = rv * Z - y;
+        if (rows_wave) L.w[ri] = rv * Z - y;  // (lanes past the padded rows may hold a stale y)
         int stop_at = p.max_iter;
         if (p.check_term) stop_at = min(stop_at, (iter / p.check_term + 1) * p.check_term);
         if (p.adaptive_rho && p.rho_interval) stop_at = min(stop_at, (iter / p.rho_interval + 1) * p.rho_interval);
@@ -1797,7 +1815,7 @@ __device__ __forceinline__ void solve_w8_body(const KParams& p, double* __restri
             __syncthreads();
             PH(14)
             // rows: z~ = A x~ ; relaxed + projected z ; y ; next w
-            {
+            if (rows_wave) {
                 double av[K], xv[K];
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
@@ -1821,7 +1839,7 @@ __device__ __forceinline__ void solve_w8_body(const KParams& p, double* __restri
         }
         // run state back to LDS
         if (low) { C.X[pc] = X; L.dx[pc] = DX; }
-        L.ys[ri] = y; C.Z[ri] = Z; C.dY[ri] = dy;
+        if (rows_wave) { L.ys[ri] = y; C.Z[ri] = Z; C.dY[ri] = dy; }
         __syncthreads();
         can_check = p.check_term && (iter % p.check_term == 0);
         const bool do_rho = p.adaptive_rho && p.rho_interval && (iter % p.rho_interval == 0);
