@@ -1019,7 +1019,10 @@ __global__ __launch_bounds__(T2, 1) void k_setup_solve_w2(KParams p, const doubl
 //   rows  z~ = A x~ (one row per lane), relaxation, projection, y, w      -> barrier
 // Four barriers instead of three, but each wave issues about 60 % of a two-wave wave's
 // instructions, and the factorisation pre-pivots the four blocks at once
-// (solve_phases.h::factorize_w4).  MPCQP_VARIANT=17 (A/B against variant 10).
+// (solve_phases.h::factorize_w4).  Operands that do not change within a run (the row's
+// and half-column's A values, the row bounds, phase A's and phase C's G values) are
+// loaded into registers at the run start: the two workgroups sharing a CU share its LDS
+// return path.  MPCQP_VARIANT=17 (A/B against variant 10).
 constexpr int T4 = 256;
 
 template <int K, int KPK, int QR>
