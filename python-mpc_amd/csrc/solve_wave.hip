@@ -1021,8 +1021,8 @@ __global__ __launch_bounds__(T2, 1) void k_setup_solve_w2(KParams p, const doubl
 // instructions, and the factorisation pre-pivots the four blocks at once
 // (solve_phases.h::factorize_w4).  Operands that do not change within a run (the row's
 // and half-column's A values, the row bounds, phase A's and phase C's G values) are
-// loaded into registers at the run start: the two workgroups sharing a CU share its LDS
-// return path.  MPCQP_VARIANT=17 (A/B against variant 10).
+// loaded into registers at the run start: fewer LDS reads (and waits) per iteration on
+// every wave's path.  MPCQP_VARIANT=17 (A/B against variant 10).
 constexpr int T4 = 256;
 
 template <int K, int KPK, int QR>
@@ -1165,8 +1165,8 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
         for (int k = 0; k < KH; ++k) ca[k] = lds_at(ch2.e[k] & 0xFFFFu);
         const double r_hi = RHO_EQ_OVER_RHO_INEQ * rho;
         double y = L.ys[ri], Z = C.Z[ri], dy = 0.0;
-        // the row's A values and bounds stay in registers for the run (fewer LDS returns
-        // per iteration; the CU's other workgroup shares them)
+        // the row's A values and bounds stay in registers for the run (fewer LDS reads per
+        // iteration)
         double av[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) av[k] = lds_at(rg.e[k] & 0xFFFFu);
