@@ -15,15 +15,19 @@ reference's closed loops), so the solver's longest-previous-solve-first
 dispatch (kernels.hip::k_order) predicts each step from the previous, different
 QP -- never from a repeat of the same one.
 
-Multi-GPU: one process per GPU (torch.distributed.run); every rank solves its
-own batch (weak scaling, no data-path collective); timing = barrier +
-synchronize on both sides, max over ranks.  --config 3/5 select the slack /
-incremental-dynamic workloads (not the headline line); cfg 5 is warm-started as
-SURVEY.md §8d D2 prescribes (cold solve, one-stage shift, timed warm re-solve).
---config 4 is BASELINE.json configs[3] (B = 262144 slack QPs split over 8 GPUs):
-32768 per rank, each rank generating its own shard (seed 4000 + rank) -- the
-same distribution as one seeded batch cut into contiguous shards, without
-every rank building all 262144 instances on the host.
+Multi-GPU: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set)
+each process is one rank; `python bench.py --gpus N` without it spawns the N
+rank processes itself (bench.launch: fresh interpreters, 127.0.0.1 rendezvous,
+the parent never touches a GPU) and exits with their status.  Every rank solves
+its own shard (no data-path collective); timing = barrier + synchronize on both
+sides, max over ranks.  --config 3/5 select the slack / incremental-dynamic
+workloads (not the headline line); cfg 5 is warm-started as SURVEY.md §8d D2
+prescribes (cold solve, one-stage shift, timed warm re-solve).  --config 4 is
+BASELINE.json configs[3]: ONE batch of 262144 slack QPs split into contiguous
+shards over the N ranks (262144 / N per rank, strong scaling).  The batch is
+built from 64 seeded chunks of 4096 instances (seed 4000 + chunk), so the union
+of the shards is the same 262144 instances at every N and each rank builds only
+its own chunks.
 
 rank 0 prints ONE JSON line with "roofline" (k_solve, HBM-bound by the
 algorithmic-bytes model of SURVEY.md §8d D3, HIP-event kernel times from the
@@ -57,13 +61,18 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6  # MI355X fp64 vector peak (spec) -- diagnostic only
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
-    ap.add_argument("--batch", type=int, default=None, help="instances per GPU (default: the config's)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="instances per GPU (default: the config's; cfg 4: the GLOBAL batch, split over the ranks)")
+    ap.add_argument("--jitter", type=float, default=JITTER,
+                    help="per-step jitter of the initial states, fraction of the D2 half-range")
+    ap.add_argument("--independent", action="store_true",
+                    help="every step's initial states drawn afresh from the D2 ranges (no correlation between steps)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--separate-setup", action="store_true",
@@ -72,7 +81,7 @@ def parse():
                     help="diagnostic: no HIP events in the timed region (roofline kernel_ms from the untimed pass)")
     ap.add_argument("--no-dispatch-ab", action="store_true",
                     help="skip the identity-dispatch diagnostic (rocprof passes: one handle's launches only)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def dist_env():
@@ -86,6 +95,81 @@ def instance_seed(config, rank):
     return 1000 * config + rank
 
 
+CHUNK = 4096  # cfg 4: instances per seeded chunk of the global batch
+
+
+def make_shard(config, B, world, rank):
+    """The rank's instances.  cfg 4 (strong scaling): contiguous chunks [r C / N, (r + 1) C / N)
+    of the one global batch of B instances, chunk c generated with seed 4000 + c, so the
+    shards of any world size tile the same global batch.  Other configs (weak scaling): B
+    instances of the rank's own seed."""
+    from osqp_amd import mpc
+    if config != 4:
+        return mpc.make_batch(config, B=B, seed=instance_seed(config, rank))
+    if B % CHUNK or (B // CHUNK) % world:
+        raise SystemExit(f"cfg 4: the global batch {B} must be a multiple of {CHUNK} * world ({world})")
+    nc = B // CHUNK
+    parts = [mpc.make_batch(4, B=CHUNK, seed=instance_seed(4, c))
+             for c in range(rank * nc // world, (rank + 1) * nc // world)]
+    b = dict(parts[0])
+    for k in ("Px", "Ax", "q", "l", "u"):
+        b[k] = np.ascontiguousarray(np.concatenate([p[k] for p in parts]))
+    b["B"] = B // world
+    return b
+
+
+def launch(n, cmd, timeout=None, stdout=None):
+    """Run `cmd` as n rank processes of one job (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*
+    as torch.distributed.run sets them, rendezvous on 127.0.0.1).  Fresh interpreters are
+    started as children; the caller must not have touched a GPU.  Returns the first
+    non-zero exit status (the remaining ranks are stopped then), else 0."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=env, stdout=stdout))
+    t0 = time.monotonic()
+    rc = 0
+    while procs:
+        for p in list(procs):
+            c = p.poll()
+            if c is None:
+                continue
+            procs.remove(p)
+            if c and not rc:
+                rc = c
+                for q in procs:
+                    q.terminate()
+        if timeout is not None and time.monotonic() - t0 > timeout and procs:
+            rc = rc or 124
+            for q in procs:
+                q.kill()
+        time.sleep(0.05)
+    return rc
+
+
+def cpu_share():
+    """(cores this process may run on, where the count comes from): the affinity mask,
+    capped by a cgroup v2 CPU quota when one is set (a GPU lease's share of the host)."""
+    n = len(os.sched_getaffinity(0))
+    src = f"sched_getaffinity ({n})"
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()
+        if quota != "max":
+            q = max(1, int(-(-int(quota) // int(period))))
+            if q < n:
+                n, src = q, f"cgroup cpu.max quota {quota}/{period} (affinity {src})"
+    except (OSError, ValueError):
+        pass
+    return n, src
+
+
 def max_over_ranks(x, world):
     """Max of a host float over all ranks (gloo; no data-path collective)."""
     if world <= 1:
@@ -97,11 +181,12 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
-def bound_sequence(b, count, seed, to_dev):
-    from osqp_amd import mpc
+def bound_sequence(b, count, seed, to_dev, jitter=JITTER, independent=False):
     """`count` distinct (l, u) device pairs of batch `b`: the first unchanged, each later
-    one with the initial-state rows (l = u = -x0) jittered (JITTER, clipped to the D2
-    ranges).  Everything else of the QP (P, A, q, the other bounds) is shared."""
+    one with the initial-state rows (l = u = -x0) jittered (`jitter`, clipped to the D2
+    ranges) or, `independent`, drawn afresh from the D2 ranges.  Everything else of the
+    QP (P, A, q, the other bounds) is shared."""
+    from osqp_amd import mpc
     rng = np.random.default_rng(seed + 7919)
     lo, hi = (np.array(v) for v in zip(*X0_RANGES[mpc.CONFIGS[b["cfg"]]["layout"]]))
     nx0 = lo.size
@@ -109,7 +194,10 @@ def bound_sequence(b, count, seed, to_dev):
     dl0, du0 = to_dev(b["l"]), to_dev(b["u"])
     seq = [(dl0, du0)]
     for _ in range(count - 1):
-        xt = np.clip(x0 + JITTER * 0.5 * (hi - lo) * rng.uniform(-1, 1, x0.shape), lo, hi)
+        if independent:
+            xt = lo + (hi - lo) * rng.uniform(0, 1, x0.shape)
+        else:
+            xt = np.clip(x0 + jitter * 0.5 * (hi - lo) * rng.uniform(-1, 1, x0.shape), lo, hi)
         dxt = to_dev(-xt)
         dl, du = dl0.clone(), du0.clone()
         dl[:, :nx0] = dxt
@@ -143,22 +231,44 @@ def pmc_traffic(workload, batch, kernel):
     return t if t.get("kernel") == kernel else {}  # measured on another kernel: not this one's traffic
 
 
-def main():
-    args = parse()
+def main(argv=None, solver_cls=None, device=None):
+    """argv: the command line (default sys.argv[1:]).  solver_cls / device: a stand-in for
+    osqp_amd.DeviceBatch and its torch device -- only tests/test_multiproc.py passes them,
+    to rehearse the rank logic on CPU (the stand-in is defined in tests/, never here)."""
+    args = parse(argv)
+    world, rank, local = dist_env()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU: spawn the ranks (this process stays off the GPU) and exit
+        # with their status; rank 0 prints the JSON line
+        cmd = [sys.executable, os.path.abspath(__file__)] + (sys.argv[1:] if argv is None else list(argv))
+        raise SystemExit(launch(args.gpus, cmd))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were started")
     import torch
     import torch.distributed as dist
     from osqp_amd import DeviceBatch, _drop_common_zeros
 
-    world, rank, local = dist_env()
     if world > 1:
         dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if device is None:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device(device)
+    on_gpu = dev.type == "cuda"
+    dsync = torch.cuda.synchronize if on_gpu else (lambda: None)
+    Solver = solver_cls or DeviceBatch
 
     from osqp_amd import mpc
     spec = mpc.CONFIGS[args.config]
-    B = args.batch or (spec["B"] if args.config != 4 else spec["B"] // 8)
-    b = mpc.make_batch(args.config, B=B, seed=instance_seed(args.config, rank))
+    strong = args.config == 4  # one global batch split over the ranks
+    if strong:
+        B_global = args.batch or spec["B"]
+        B = B_global // world
+    else:
+        B = args.batch or spec["B"]
+        B_global = world * B
+    b = make_shard(args.config, B_global if strong else B, world, rank)
     P, Px = _drop_common_zeros(b["P"], b["Px"])
     A, Ax = _drop_common_zeros(b["A"], b["Ax"])
     settings = {k: v for k, v in b["settings"].items() if k != "verbose"}
@@ -169,14 +279,15 @@ def main():
 
     dPx, dAx, dq = (to_dev(a) for a in (Px, Ax, b["q"]))
     # the base batch, then one distinct batch per warmup and timed step
-    seq = bound_sequence(b, 1 + args.warmup + args.steps, instance_seed(args.config, rank), to_dev)
+    seq = bound_sequence(b, 1 + args.warmup + args.steps, instance_seed(args.config, rank), to_dev,
+                         jitter=args.jitter, independent=args.independent)
     dl, du = seq[0]
     dx = torch.empty((B, n), dtype=torch.float64, device=dev)
     dy = torch.empty((B, m), dtype=torch.float64, device=dev)
     dst = torch.empty(B, dtype=torch.int32, device=dev)
     dit = torch.empty(B, dtype=torch.int32, device=dev)
-    torch.cuda.synchronize()
-    solver = DeviceBatch(P, A, B, device=local, **settings)
+    dsync()
+    solver = Solver(P, A, B, device=local, **settings)
     warm = args.config == 5
     xs = ys = None
     if warm:
@@ -188,7 +299,7 @@ def main():
         solver.solve(dx, dy, dst, dit)
         solver.synchronize()
         xs, ys = warm_shift(b["N"], 8, 2, dx, dy)
-        torch.cuda.synchronize()
+        dsync()
 
     def step(t, sv=solver, fused=not args.separate_setup):
         sl, su = seq[t]
@@ -215,7 +326,7 @@ def main():
             dist.barrier()
 
     barrier()
-    torch.cuda.synchronize()
+    dsync()
     solver.synchronize()
     fused = not (warm or args.separate_setup)
     if not args.no_kernel_timing:  # one event pair per launch, on the solver's stream
@@ -224,7 +335,7 @@ def main():
     for t in range(1 + args.warmup, 1 + args.warmup + args.steps):
         step(t)
     solver.synchronize()
-    torch.cuda.synchronize()
+    dsync()
     t1 = time.perf_counter()
     barrier()
     kt = solver.timing_read() if not args.no_kernel_timing else None
@@ -245,7 +356,7 @@ def main():
     value_identity = None
     if not args.no_dispatch_ab:
         os.environ["MPCQP_DISPATCH"] = "identity"
-        ident = DeviceBatch(P, A, B, device=local, **settings)
+        ident = Solver(P, A, B, device=local, **settings)
         del os.environ["MPCQP_DISPATCH"]
         for t in range(1 + args.warmup):
             step(t, ident)
@@ -257,9 +368,14 @@ def main():
         value_identity = B * args.steps / (time.perf_counter() - ta)
         del ident
 
-    value = world * B * args.steps / dt
+    value = B_global * args.steps / dt
     nnzP, nnzA = P.nnz, A.nnz
-    bytes_per_solve = 8 * (nnzP + nnzA + n + 2 * m) + 8 * (n + m) + (8 * (n + m) if warm else 0)
+    # SURVEY.md §8d D3 counts the nonzeros of one instance's matrices: cfg 5's stored
+    # pattern is the union over the batch (2666 entries), of which an instance has about
+    # 2016 nonzero -- the algorithmic bytes count the instance's own (mean over the batch)
+    nnzP_alg = float(np.count_nonzero(Px) / B)
+    nnzA_alg = float(np.count_nonzero(Ax) / B)
+    bytes_per_solve = 8 * (nnzP_alg + nnzA_alg + n + 2 * m) + 8 * (n + m) + (8 * (n + m) if warm else 0)
     solve_ms = kt["solve_ms"] / max(1, kt["n_solve"])
     setup_ms = kt["setup_ms"] / kt["n_setup"] if kt["n_setup"] else None  # None: setup runs inside the fused kernel
     achieved = bytes_per_solve * B / (solve_ms * 1e-3) / 1e9
@@ -275,10 +391,10 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         import pyoracle
-        threads = int(os.environ.get("OMP_NUM_THREADS") or min(16, os.cpu_count() or 1))
+        threads, threads_src = cpu_share()
         # bounded sample: passes over the same instances until ~cpu_seconds of wall time
         nc = min(B, max(threads * 8, 64))
-        done, tc, passes = 0, 0.0, 0
+        done, tc, passes, t_setup, t_solve = 0, 0.0, 0, 0.0, 0.0
         ws = {}
         if warm:
             ws = dict(x0=xs[:nc].cpu().numpy(), y0=ys[:nc].cpu().numpy())
@@ -287,18 +403,26 @@ def main():
             rc = pyoracle.solve_batch(P, A, Px[:nc], b["q"][:nc], Ax[:nc], b["l"][:nc], b["u"][:nc],
                                       nthreads=threads, **ws, **settings)
             tc += time.perf_counter() - t
+            t_setup += rc.t_setup
+            t_solve += rc.t_solve
             done += nc
             passes += 1
         cpu = {"value": done / tc, "unit": "QP solves/s", "cores": threads, "kind": "port",
+               "cores_source": threads_src, "host_cpus": os.cpu_count(),
                "sample": f"{passes} passes over the first {nc} of the {B} instances ({done} solves), "
                          f"fresh setup(){'+warm_start(shifted x, y)' if warm else ''}+solve() each, "
                          f"{threads} POSIX threads, oracle/osqp_oracle.c "
                          f"(OSQP 0.6 restatement; osqp itself is not installed on the box)",
                "seconds": round(tc, 3),
+               # thread-seconds of the two phases (orc_setup: scaling, KKT ordering and
+               # LDL' factorisation; orc_solve: ADMM) and the solve-only rate they imply
+               "setup_thread_s": round(t_setup, 3), "solve_thread_s": round(t_solve, 3),
+               "value_solve_only": done / tc * (t_setup + t_solve) / t_solve if t_solve > 0 else None,
                "status_match_gpu": float(np.mean(rc.status_val == status[:nc])),
                "iter_match_gpu": float(np.mean(rc.iter == iters[:nc]))}
 
     if rank == 0:
+        kname = solve_kernel_name(info, fused=fused)
         line = {
             "metric": "QP solves/sec (batch) at N=20 nx=4 nu=1" if args.config == 2 else
                       f"QP solves/sec (batch), {spec['name']}",
@@ -309,31 +433,34 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (seeded lane-tracking initial states, SURVEY.md §8d D2, jittered per step)",
+            "data": "synthetic (seeded lane-tracking initial states, SURVEY.md §8d D2, " +
+                    ("drawn afresh every step)" if args.independent else f"jittered +-{args.jitter:.0%} per step)"),
             "config": {"workload": spec["name"], "config_index": args.config, "batch_per_gpu": B,
-                       "global_batch": world * B, "horizon_N": b["N"], "n": n, "m": m,
-                       "nnz_triuP": nnzP, "nnz_A": nnzA, "eps_abs": 1e-3, "eps_rel": 1e-3,
+                       "global_batch": B_global, "horizon_N": b["N"], "n": n, "m": m,
+                       "nnz_triuP": nnzP, "nnz_A": nnzA, "nnz_A_per_instance": nnzA_alg,
+                       "eps_abs": 1e-3, "eps_rel": 1e-3,
                        "step": ("setup()+warm_start(base solution shifted one stage)+solve()" if warm else
                                 "setup()+solve()" + ("" if args.separate_setup else
-                                                     " (mpcqp_setup_solve_device: one call; one kernel for "
-                                                     "the two-wave variant)"))
-                               + " per instance, inputs resident in HBM; a distinct batch per "
-                                f"step (initial states jittered +-{JITTER:.0%} of the D2 ranges)",
+                                                     f" (mpcqp_setup_solve_device: one call; kernel {kname})"))
+                               + " per instance, inputs resident in HBM; a distinct batch per step (" +
+                               ("initial states drawn afresh)" if args.independent else
+                                f"initial states jittered +-{args.jitter:.0%} of the D2 ranges)"),
                        "parallelism": f"batch-shard x{world}",
                        "dispatch": "longest previous solve first (kernels.hip::k_order), predicted from the "
                                    "previous step's different batch",
                        "value_identity_dispatch_rank0": value_identity,
                        "iters_mean": float(iters.mean()), "iters_max": int(iters.max()),
                        "solved_frac": float(np.mean(status == 1)),
-                       "plan": {"nb": info["nb"], "block": S, "amax": info["amax"], "lds_bytes": info["lds_bytes_solve"],
+                       "plan": {"nb": info["nb"], "block": S, "amax": info["amax"], "npad": info["npad"],
+                                "lds_bytes": info["lds_bytes_solve"],
                                 "kernel_variant": info["variant"], "threads_per_qp": info["threads_per_qp"]}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic.get("bytes_per_launch"),
                          "traffic_source": traffic.get("source"),
-                         "kernel": solve_kernel_name(info, fused=fused),
+                         "kernel": kname,
                          "kernel_ms": solve_ms, "setup_kernel_ms": setup_ms,
                          "bytes_per_solve": bytes_per_solve, "launch_instances": B,
                          "fp64_tflops_model": fp64_tflops, "fp64_peak_tflops": FP64_PEAK_TFLOPS},

@@ -104,7 +104,10 @@ void mpcqp_default_settings(mpcqp_settings *s);
 
 /* Symbolic analysis + allocation + per-instance setup (scaling, rho classes).
  * device_mask: bit d selects HIP device d; 0 = device 0.  The batch is split
- * into contiguous shards across the selected devices (no collectives). */
+ * into contiguous shards across the selected devices (no collectives): every
+ * shard's kernels are enqueued (one stream per shard) before the host gathers
+ * the results, so the devices run concurrently.  MPCQP_SPLIT=k in the
+ * environment (diagnostic) cuts k shards per selected device. */
 int mpcqp_setup_batch(int32_t n, int32_t m,
                       const int32_t *Pp, const int32_t *Pi,
                       const int32_t *Ap, const int32_t *Ai,
@@ -144,14 +147,18 @@ int mpcqp_solve_device(mpcqp_handle *h, double *dx, double *dy, int32_t *dstatus
                        void *stream);
 /* setup + solve of the same inputs in one call: mpcqp_setup_device(dPx..du) followed by
  * mpcqp_solve_device(dx, dy, dstatus, diters), with identical results.  Where the
- * solve kernel allows it (the two-wave kernel of the N=20 lateral layouts) both run as
- * ONE kernel: each workgroup scales its instance and solves it, so no setup kernel and
- * no launch gap stand in front of the slowest instance.  The reference's per-call
+ * solve kernel allows it -- the four-wave kernel k_setup_solve_w4 (the N=20 lateral
+ * layouts: vanilla, and slack once its slack columns are eliminated) or the two-wave
+ * kernel k_setup_solve_w2 -- both run as ONE kernel: each workgroup scales its instance
+ * and solves it, so no setup kernel and no launch gap stand in front of the slowest
+ * instance; the last workgroup also sorts the next dispatch order.  The reference's per-call
  * pattern prob.setup(...); prob.solve() (Control/MPC/mpc_kinematics.py:194-198,
  * mpc_dynamics.py:392-396) maps onto it one-to-one. */
 int mpcqp_setup_solve_device(mpcqp_handle *h, const double *dPx, const double *dAx, const double *dq,
                              const double *dl, const double *du, double *dx, double *dy, int32_t *dstatus,
                              int32_t *diters, void *stream);
+/* Blocks until every call enqueued on the handle so far has finished, on the handle's
+ * own stream(s) and on the caller stream the last *_device call used. */
 int mpcqp_synchronize(mpcqp_handle *h);
 /* hipEvent-bracketed timing of the ADMM kernel launches of the last *_device
  * solve on the handle's stream: milliseconds, or -1 when unavailable. */

@@ -20,6 +20,7 @@
 
 #include <math.h>
 #include <pthread.h>
+#include <time.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -1064,13 +1065,21 @@ typedef struct {
     double *x_out, *y_out;
     int *status, *iters;
     int err;
+    double t_setup, t_solve; /* thread-seconds in orc_setup (+ warm start) and in orc_solve */
 } batch_job;
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
 
 static void *batch_worker(void *arg) {
     batch_job *j = (batch_job *)arg;
     int nnzP = j->Pp[j->n], nnzA = j->Ap[j->n];
     for (int b = j->b0; b < j->b1; ++b) {
         orc_work *w = NULL;
+        const double t0 = now_s();
         int e = orc_setup(&w, j->n, j->m, j->Pp, j->Pi, j->Px_b + (size_t)b * nnzP,
                           j->q_b + (size_t)b * j->n, j->Ap, j->Ai, j->Ax_b + (size_t)b * nnzA,
                           j->l_b + (size_t)b * j->m, j->u_b + (size_t)b * j->m, j->s);
@@ -1080,7 +1089,10 @@ static void *batch_worker(void *arg) {
             continue;
         }
         if (j->x0_b && j->y0_b) orc_warm_start(w, j->x0_b + (size_t)b * j->n, j->y0_b + (size_t)b * j->m);
+        const double t1 = now_s();
         orc_solve(w);
+        j->t_setup += t1 - t0;
+        j->t_solve += now_s() - t1;
         orc_get_solution(w, j->x_out ? j->x_out + (size_t)b * j->n : NULL,
                          j->y_out ? j->y_out + (size_t)b * j->m : NULL, NULL, NULL);
         if (j->status) j->status[b] = w->info.status_val;
@@ -1103,6 +1115,15 @@ int orc_solve_batch_warm(int B, int n, int m, const int *Pp, const int *Pi, cons
                          const double *l_b, const double *u_b, const double *x0_b, const double *y0_b,
                          const orc_settings *s, double *x_out, double *y_out, int *status, int *iters,
                          int nthreads) {
+    return orc_solve_batch_timed(B, n, m, Pp, Pi, Px_b, q_b, Ap, Ai, Ax_b, l_b, u_b, x0_b, y0_b, s, x_out, y_out,
+                                 status, iters, nthreads, NULL);
+}
+
+int orc_solve_batch_timed(int B, int n, int m, const int *Pp, const int *Pi, const double *Px_b,
+                          const double *q_b, const int *Ap, const int *Ai, const double *Ax_b,
+                          const double *l_b, const double *u_b, const double *x0_b, const double *y0_b,
+                          const orc_settings *s, double *x_out, double *y_out, int *status, int *iters,
+                          int nthreads, double *phase_s) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > B) nthreads = B > 0 ? B : 1;
     batch_job *jobs = (batch_job *)calloc(nthreads, sizeof(batch_job));
@@ -1123,8 +1144,11 @@ int orc_solve_batch_warm(int B, int n, int m, const int *Pp, const int *Pi, cons
         for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
     }
     int err = 0;
-    for (int t = 0; t < nthreads; ++t)
+    if (phase_s) phase_s[0] = phase_s[1] = 0.0;
+    for (int t = 0; t < nthreads; ++t) {
         if (jobs[t].err && !err) err = jobs[t].err;
+        if (phase_s) { phase_s[0] += jobs[t].t_setup; phase_s[1] += jobs[t].t_solve; }
+    }
     free(jobs); free(th);
     return err;
 }

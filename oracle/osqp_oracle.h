@@ -115,6 +115,15 @@ int orc_solve_batch_warm(int B, int n, int m,
                          const orc_settings *s, double *x_out, double *y_out, int *status, int *iters,
                          int nthreads);
 
+/* Same, and phase_s[0] / phase_s[1] (may be NULL) receive the thread-seconds spent in
+ * setup (+ warm start) and in solve, summed over the threads (bench.py's CPU baseline). */
+int orc_solve_batch_timed(int B, int n, int m,
+                          const int *Pp, const int *Pi, const double *Px_b, const double *q_b,
+                          const int *Ap, const int *Ai, const double *Ax_b,
+                          const double *l_b, const double *u_b, const double *x0_b, const double *y0_b,
+                          const orc_settings *s, double *x_out, double *y_out, int *status, int *iters,
+                          int nthreads, double *phase_s);
+
 #ifdef __cplusplus
 }
 #endif

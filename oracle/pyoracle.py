@@ -99,6 +99,7 @@ def lib():
                                            P(C.c_double), P(C.c_double), P(C.c_double), P(C.c_double),
                                            P(_Settings), P(C.c_double), P(C.c_double), P(C.c_int), P(C.c_int),
                                            C.c_int]
+        L.orc_solve_batch_timed.argtypes = L.orc_solve_batch_warm.argtypes + [P(C.c_double)]
         _lib = L
     return _lib
 
@@ -223,7 +224,9 @@ def solve_batch(P, A, Px_b, q_b, Ax_b, l_b, u_b, nthreads=1, x0=None, y0=None, *
         raise ValueError("x0 and y0 go together")
     if x0 is not None:
         x0 = np.ascontiguousarray(x0, np.float64); y0 = np.ascontiguousarray(y0, np.float64)
-    e = lib().orc_solve_batch_warm(B, n, m, _ip(Pp), _ip(Pi), _dp(Px_b), _dp(q_b), _ip(Ap), _ip(Ai),
-                                   _dp(Ax_b), _dp(l_b), _dp(u_b), _dp(x0), _dp(y0), C.byref(s), _dp(x),
-                                   _dp(y), _ip(st), _ip(it), int(nthreads))
-    return SimpleNamespace(x=x, y=y, status_val=st, iter=it, err=e)
+    ph = np.zeros(2)
+    e = lib().orc_solve_batch_timed(B, n, m, _ip(Pp), _ip(Pi), _dp(Px_b), _dp(q_b), _ip(Ap), _ip(Ai),
+                                    _dp(Ax_b), _dp(l_b), _dp(u_b), _dp(x0), _dp(y0), C.byref(s), _dp(x),
+                                    _dp(y), _ip(st), _ip(it), int(nthreads), _dp(ph))
+    # t_setup / t_solve: thread-seconds in setup (+ warm start) and in solve
+    return SimpleNamespace(x=x, y=y, status_val=st, iter=it, err=e, t_setup=float(ph[0]), t_solve=float(ph[1]))

@@ -294,7 +294,7 @@ int make_handle(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi, cons
     const long nd = (long)devs.size();
     for (long i = 0; i < nd; ++i) {
         Shard s;
-        s.dev = devs[i];
+        s.dev = devs[i];  // devs may repeat a device (MPCQP_SPLIT): several shards on it, one stream each
         s.b0 = B * i / nd;
         s.B = B * (i + 1) / nd - s.b0;
         if (s.B <= 0) continue;
@@ -318,10 +318,13 @@ int check_bounds_host(const mpcqp_handle* h, const double* l, const double* u, l
     return 0;
 }
 
+// waits for the handle's own streams and for the last call's work wherever it was
+// enqueued (a caller stream of the *_device entry points: last_ev)
 int sync_all(mpcqp_handle* h) {
     for (auto& s : h->shards) {
         HIPCHK(hipSetDevice(s.dev));
         HIPCHK(hipStreamSynchronize(s.stream));
+        if (s.last_st) HIPCHK(hipEventSynchronize(s.last_ev));
     }
     return 0;
 }
@@ -330,21 +333,15 @@ int sync_all(mpcqp_handle* h) {
 // to another stream is waited for first.  The handle's workspace -- including the
 // dispatch order each solve rewrites for the next (kernels.hip::k_order) -- is then
 // never read by one stream while another writes it, whatever streams the caller uses.
-// The event is recorded only on a change of stream (at that moment it covers everything
-// enqueued on the old stream), so a single-stream caller adds no packets between its
-// kernels.  A record that fails (the old stream was destroyed) falls back to a device
-// synchronisation.
+// stream_leave records last_ev on the call's own stream once its work is enqueued, so
+// stream_enter never touches a stream of an earlier call (which the caller may have
+// destroyed since): on a change of stream it only makes the new stream wait for last_ev.
 int stream_enter(Shard& s, hipStream_t st) {
-    if (!s.last_st || s.last_st == st) return 0;
-    if (hipEventRecord(s.last_ev, s.last_st) == hipSuccess) {
-        HIPCHK(hipStreamWaitEvent(st, s.last_ev, 0));
-    } else {
-        (void)hipGetLastError();
-        HIPCHK(hipDeviceSynchronize());
-    }
+    if (s.last_st && s.last_st != st) HIPCHK(hipStreamWaitEvent(st, s.last_ev, 0));
     return 0;
 }
 int stream_leave(Shard& s, hipStream_t st) {
+    HIPCHK(hipEventRecord(s.last_ev, st));
     s.last_st = st;
     return 0;
 }
@@ -396,6 +393,16 @@ int mpcqp_setup_batch(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi
     for (int d = 0; d < 32; ++d)
         if (device_mask & (1u << d)) devs.push_back(d);
     if (devs.empty()) devs.push_back(0);
+    // MPCQP_SPLIT=k (diagnostic): k contiguous shards per selected device, each with its own
+    // stream, workspace and dispatch order -- the multi-device shard / gather code (b0
+    // offsets, launch-all-then-gather) exercised on a one-GPU box
+    if (const char* ev = getenv("MPCQP_SPLIT"); ev && atoi(ev) > 1) {
+        const int k = std::min(atoi(ev), 64);
+        std::vector<int> rep;
+        for (int d : devs)
+            for (int i = 0; i < k; ++i) rep.push_back(d);
+        devs.swap(rep);
+    }
     mpcqp_handle* h = nullptr;
     if (int e = make_handle(n, m, Pp, Pi, Ap, Ai, B, settings, devs, true, &h)) return e;
     if (int e = check_bounds_host(h, l, u, B)) { mpcqp_free(h); return e; }
@@ -457,6 +464,9 @@ int mpcqp_warm_start_batch(mpcqp_handle* h, const double* x, const double* y) {
 int mpcqp_solve_batch(mpcqp_handle* h, double* x, double* y, int32_t* status, int32_t* iters) {
     if (!h) return fail(MPCQP_EINVAL, "NULL handle");
     const long n = h->n, m = h->m;
+    // every shard's kernels are enqueued before any result is copied back: a copy into the
+    // caller's (pageable) memory blocks the host until its shard is done, so copying inside
+    // the launch loop would start shard d+1 only after shard d had finished
     for (auto& s : h->shards) {
         HIPCHK(hipSetDevice(s.dev));
         if (int e = stream_enter(s, s.stream)) return e;
@@ -464,11 +474,15 @@ int mpcqp_solve_batch(mpcqp_handle* h, double* x, double* y, int32_t* status, in
         HIPCHK(launch_solve(s.kp, s.B, s.out_x, s.out_y, 0, s.stream));
         HIPCHK(hipEventRecord(s.ev1, s.stream));
         HIPCHK(launch_order(s.kp, s.B, s.stream));
+        if (int e = stream_leave(s, s.stream)) return e;
+    }
+    // the host-side gather: each shard's slice of the caller's buffers, in shard order
+    for (auto& s : h->shards) {
+        HIPCHK(hipSetDevice(s.dev));
         if (x) HIPCHK(hipMemcpyAsync(x + s.b0 * n, s.out_x, sizeof(double) * s.B * n, hipMemcpyDeviceToHost, s.stream));
         if (y) HIPCHK(hipMemcpyAsync(y + s.b0 * m, s.out_y, sizeof(double) * s.B * m, hipMemcpyDeviceToHost, s.stream));
         if (status) HIPCHK(hipMemcpyAsync(status + s.b0, s.kp.status, sizeof(int) * s.B, hipMemcpyDeviceToHost, s.stream));
         if (iters) HIPCHK(hipMemcpyAsync(iters + s.b0, s.kp.iter, sizeof(int) * s.B, hipMemcpyDeviceToHost, s.stream));
-        if (int e = stream_leave(s, s.stream)) return e;
     }
     if (int e = sync_all(h)) return e;
     float ms = 0.f;
@@ -524,8 +538,10 @@ int mpcqp_create(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi, con
 
 static hipStream_t pick(Shard& s, void* stream) { return stream ? (hipStream_t)stream : s.stream; }
 
-static int ev_begin(mpcqp_handle* h, std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, hipStream_t st) {
-    if (!h->collect) return 0;
+// on: the record this launch kind goes to is enabled (collect: solve launches,
+// collect_setup: setup launches)
+static int ev_begin(bool on, std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, hipStream_t st) {
+    if (!on) return 0;
     hipEvent_t a, b;
     HIPCHK(hipEventCreate(&a));
     HIPCHK(hipEventCreate(&b));
@@ -533,8 +549,8 @@ static int ev_begin(mpcqp_handle* h, std::vector<std::pair<hipEvent_t, hipEvent_
     v.push_back({a, b});
     return 0;
 }
-static int ev_end(mpcqp_handle* h, std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, hipStream_t st) {
-    if (!h->collect || v.empty()) return 0;
+static int ev_end(bool on, std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, hipStream_t st) {
+    if (!on || v.empty()) return 0;
     HIPCHK(hipEventRecord(v.back().second, st));
     return 0;
 }
@@ -547,10 +563,10 @@ int mpcqp_setup_device(mpcqp_handle* h, const double* dPx, const double* dAx, co
     HIPCHK(hipSetDevice(s.dev));
     if (int e = stream_enter(s, st)) return e;
     if (h->collect_setup)
-        if (int e = ev_begin(h, h->ev_setup, st)) return e;
+        if (int e = ev_begin(h->collect_setup, h->ev_setup, st)) return e;
     HIPCHK(launch_setup(s.kp, s.B, dPx, dAx, dq, dl, du, st));
     if (h->collect_setup)
-        if (int e = ev_end(h, h->ev_setup, st)) return e;
+        if (int e = ev_end(h->collect_setup, h->ev_setup, st)) return e;
     return stream_leave(s, st);
 }
 
@@ -585,7 +601,7 @@ int mpcqp_solve_device(mpcqp_handle* h, double* dx, double* dy, int32_t* dstatus
     // one event pair around the launch: the timing record's while timing is on, else
     // the handle's own (mpcqp_last_kernel_ms)
     if (h->collect) {
-        if (int e = ev_begin(h, h->ev_solve, st)) return e;
+        if (int e = ev_begin(h->collect, h->ev_solve, st)) return e;
     } else {
         HIPCHK(hipEventRecord(s.ev0, st));
     }
@@ -594,7 +610,7 @@ int mpcqp_solve_device(mpcqp_handle* h, double* dx, double* dy, int32_t* dstatus
     k.oiter = diters;
     HIPCHK(launch_solve(k, s.B, dx, dy, 0, st));
     if (h->collect) {
-        if (int e = ev_end(h, h->ev_solve, st)) return e;
+        if (int e = ev_end(h->collect, h->ev_solve, st)) return e;
         h->last_pair = h->ev_solve.back();
     } else {
         HIPCHK(hipEventRecord(s.ev1, st));
@@ -614,7 +630,7 @@ int mpcqp_setup_solve_device(mpcqp_handle* h, const double* dPx, const double* d
     HIPCHK(hipSetDevice(s.dev));
     if (int e = stream_enter(s, st)) return e;
     if (h->collect) {
-        if (int e = ev_begin(h, h->ev_solve, st)) return e;
+        if (int e = ev_begin(h->collect, h->ev_solve, st)) return e;
     } else {
         HIPCHK(hipEventRecord(s.ev0, st));
     }
@@ -623,7 +639,7 @@ int mpcqp_setup_solve_device(mpcqp_handle* h, const double* dPx, const double* d
     k.oiter = diters;
     HIPCHK(launch_setup_solve(k, s.B, dPx, dAx, dq, dl, du, dx, dy, st));
     if (h->collect) {
-        if (int e = ev_end(h, h->ev_solve, st)) return e;
+        if (int e = ev_end(h->collect, h->ev_solve, st)) return e;
         h->last_pair = h->ev_solve.back();
     } else {
         HIPCHK(hipEventRecord(s.ev1, st));

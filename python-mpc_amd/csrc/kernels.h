@@ -57,7 +57,8 @@ struct KParams {
     // Rewritten after every solve by launch_order (longest previous solve first).
     const int* order;
     long slots;  // workgroups of the solve kernel resident at once on the device (CUs x occupancy)
-    // k_solve_w2 sorts the order itself in its last workgroup (device_common.h::order_epilogue)
+    // the four- and two-wave kernels (k_solve_w4 / k_setup_solve_w4, k_solve_w2 /
+    // k_setup_solve_w2) sort the order themselves in their last workgroup (device_common.h::order_epilogue)
     // when the batch is at most kOrderFuseMax: arrival counter (zero between launches), or null
     int* done;
 };
