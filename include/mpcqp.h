@@ -94,6 +94,8 @@ typedef struct {
     int32_t gather_k;           /* max nonzeros per row / column of A */
     int32_t variant;            /* solve-kernel instantiation in use */
     int32_t threads_per_qp;     /* workgroup size of that kernel */
+    int32_t n_eliminated;       /* variables taken out of the block system by a scalar Schur
+                                   complement (degree <= 1 vertices of K: slack columns) */
 } mpcqp_plan_info;
 
 typedef struct mpcqp_handle mpcqp_handle;
@@ -190,6 +192,12 @@ const char *mpcqp_last_error(void);
 int mpcqp_analyze(int32_t n, int32_t m, const int32_t *Pp, const int32_t *Pi,
                   const int32_t *Ap, const int32_t *Ai, int32_t *nb, int32_t *block,
                   int32_t *var_pad, int32_t *bsize);
+/* Same, with `eliminate`: the plan a handle uses for the four-wave kernel -- degree <= 1
+ * vertices of K's graph (slack columns) taken out of the blocks (padded indices from
+ * nb * block on), blocks packed greedily; n_eliminated (may be NULL) receives their count. */
+int mpcqp_analyze_ex(int32_t n, int32_t m, const int32_t *Pp, const int32_t *Pi,
+                     const int32_t *Ap, const int32_t *Ai, int32_t eliminate, int32_t *nb,
+                     int32_t *block, int32_t *var_pad, int32_t *bsize, int32_t *n_eliminated);
 
 /* ======================================================================
  * The MPC data path around the solver, on the device.

@@ -104,11 +104,23 @@ size_t carve(size_t& off, size_t count) {
     return o;
 }
 
+// the plan-shape fields of KParams (what variant_fits reads)
+void shape_params(const Plan& pl, KParams& k) {
+    k.n = pl.n; k.m = pl.m; k.nb = pl.nb; k.npad = pl.npad; k.nnzP = pl.nnzP; k.nnzA = pl.nnzA; k.amax = pl.amax;
+    k.bmax = pl.bmax; k.pmeet = (pl.nb - 1) / 2;
+    k.gk = pl.gather_k; k.pk = pl.p_k; k.ntgt = pl.ntgt; k.term_max = pl.term_max;
+    k.gk1 = 0;
+    for (int i = 128; i < pl.m; ++i) k.gk1 = std::max(k.gk1, pl.acsr_ptr[i + 1] - pl.acsr_ptr[i]);
+    k.ne = pl.ne; k.ecnt = pl.ecnt; k.eterm_max = pl.eterm_max;
+    k.gkr = pl.max_row_nnz; k.gkc = pl.max_col_nnz;
+}
+
 int upload_plan(const Plan& pl, Shard& s) {
     std::vector<const std::vector<int>*> parts = {
         &pl.pad_var, &pl.acsc_ptr, &pl.acsc_row, &pl.acsc_v, &pl.acsr_ptr, &pl.acsr_col, &pl.acsr_v,
         &pl.psym_ptr, &pl.psym_col, &pl.psym_v, &pl.p_r, &pl.p_c, &pl.a_r, &pl.a_c,
-        &pl.asm_blk_ptr, &pl.asm_tgt, &pl.tterm, &pl.acsr_pos, &pl.gcol, &pl.grow, &pl.gpsym, &pl.toff, &pl.bsize, &pl.tcnt};
+        &pl.asm_blk_ptr, &pl.asm_tgt, &pl.tterm, &pl.acsr_pos, &pl.gcol, &pl.grow, &pl.gpsym, &pl.toff, &pl.bsize, &pl.tcnt,
+        &pl.eown, &pl.etterm};
     std::vector<size_t> offs;
     std::vector<int> flat;
     for (auto* v : parts) {
@@ -122,7 +134,8 @@ int upload_plan(const Plan& pl, Shard& s) {
                          &s.kp.acsr_col, &s.kp.acsr_v, &s.kp.psym_ptr, &s.kp.psym_col, &s.kp.psym_v,
                          &s.kp.p_r, &s.kp.p_c, &s.kp.a_r, &s.kp.a_c, &s.kp.asm_blk_ptr, &s.kp.asm_tgt,
                          &s.kp.tterm, &s.kp.acsr_pos,
-                         &s.kp.gcol, &s.kp.grow, &s.kp.gpsym, &s.kp.toff, &s.kp.bsize, &s.kp.tcnt};
+                         &s.kp.gcol, &s.kp.grow, &s.kp.gpsym, &s.kp.toff, &s.kp.bsize, &s.kp.tcnt,
+                         &s.kp.eown, &s.kp.etterm};
     for (size_t i = 0; i < parts.size(); ++i) *dst[i] = s.dplan + offs[i];
     return 0;
 }
@@ -217,11 +230,7 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
         s.out_x = (double*)(base + carve<double>(off, B * n));
         s.out_y = (double*)(base + carve<double>(off, B * m));
     }
-    k.n = pl.n; k.m = pl.m; k.nb = pl.nb; k.npad = pl.npad; k.nnzP = pl.nnzP; k.nnzA = pl.nnzA; k.amax = pl.amax;
-    k.bmax = pl.bmax; k.pmeet = (pl.nb - 1) / 2;
-    k.gk = pl.gather_k; k.pk = pl.p_k; k.ntgt = pl.ntgt; k.term_max = pl.term_max;
-    k.gk1 = 0;
-    for (int i = 128; i < pl.m; ++i) k.gk1 = std::max(k.gk1, pl.acsr_ptr[i + 1] - pl.acsr_ptr[i]);
+    shape_params(pl, k);
     const mpcqp_settings& st = h->set;
     k.sigma = st.sigma; k.alpha = st.alpha; k.eps_abs = st.eps_abs; k.eps_rel = st.eps_rel;
     k.eps_pinf = st.eps_prim_inf; k.eps_dinf = st.eps_dual_inf; k.rho0 = st.rho;
@@ -259,6 +268,28 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
     return 0;
 }
 
+// The plan of a handle: with the degree <= 1 vertices of K eliminated (plan.h) when the
+// four-wave kernel then runs the reduced system -- the slack layouts (SURVEY.md §8
+// configs 1, 3, 4: 230 variables, 8 blocks -> 125 in 4) -- else the plain plan.  Polish
+// factors the full system (factorize<POL>), so it keeps the plain plan; MPCQP_ELIM=0 (A/B)
+// and an MPCQP_VARIANT override other than 17 do too.
+std::string choose_plan(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
+                        const int32_t* Ai, const mpcqp_settings& st, Plan& pl) {
+    const char* ev = getenv("MPCQP_ELIM");
+    const char* vv = getenv("MPCQP_VARIANT");
+    if (!st.polish && !(ev && ev[0] == '0') && !(vv && *vv && atoi(vv) != 17)) {
+        std::string err = build_plan(n, m, Pp, Pi, Ap, Ai, pl, true);
+        if (err.empty() && pl.ne == 0) return err;  // nothing to eliminate: the plain plan
+        if (err.empty()) {
+            KParams k{};
+            shape_params(pl, k);
+            k.mode = 2;
+            if (variant_fits(k, 17)) return err;
+        }
+    }
+    return build_plan(n, m, Pp, Pi, Ap, Ai, pl, false);
+}
+
 int validate_settings(const mpcqp_settings& s) {
     if (!(s.rho > 0) || !(s.sigma > 0) || s.max_iter <= 0 || s.eps_abs < 0 || s.eps_rel < 0 ||
         (s.eps_abs == 0 && s.eps_rel == 0) || !(s.eps_prim_inf > 0) || !(s.eps_dual_inf > 0) ||
@@ -280,7 +311,7 @@ int make_handle(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi, cons
     if (settings) h->set = *settings;
     else mpcqp_default_settings(&h->set);
     if (int e = validate_settings(h->set)) return e;
-    std::string err = build_plan(n, m, Pp, Pi, Ap, Ai, h->plan);
+    std::string err = choose_plan(n, m, Pp, Pi, Ap, Ai, h->set, h->plan);
     if (!err.empty()) {
         bool unsup = err.rfind("unsupported", 0) == 0;
         return fail(unsup ? MPCQP_EUNSUPPORTED : MPCQP_EINVAL, "%s", err.c_str());
@@ -374,8 +405,15 @@ const char* mpcqp_last_error(void) { return g_err.c_str(); }
 
 int mpcqp_analyze(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
                   const int32_t* Ai, int32_t* nb, int32_t* block, int32_t* var_pad, int32_t* bsize) {
+    return mpcqp_analyze_ex(n, m, Pp, Pi, Ap, Ai, 0, nb, block, var_pad, bsize, nullptr);
+}
+
+int mpcqp_analyze_ex(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
+                     const int32_t* Ai, int32_t eliminate, int32_t* nb, int32_t* block, int32_t* var_pad,
+                     int32_t* bsize, int32_t* n_eliminated) {
     Plan pl;
-    std::string err = build_plan(n, m, Pp, Pi, Ap, Ai, pl);
+    std::string err = build_plan(n, m, Pp, Pi, Ap, Ai, pl, eliminate != 0);
+    if (n_eliminated) *n_eliminated = pl.ne;
     if (!err.empty()) return fail(err.rfind("unsupported", 0) == 0 ? MPCQP_EUNSUPPORTED : MPCQP_EINVAL, "%s", err.c_str());
     if (nb) *nb = pl.nb;
     if (block) *block = kS;
@@ -714,6 +752,7 @@ int mpcqp_get_plan_info(const mpcqp_handle* h, mpcqp_plan_info* info) {
     info->gather_k = h->plan.gather_k;
     info->variant = h->shards.empty() ? -1 : h->shards[0].kp.variant;
     info->threads_per_qp = h->shards.empty() ? 0 : solve_threads(h->shards[0].kp.variant);
+    info->n_eliminated = h->plan.ne;
     return 0;
 }
 

@@ -31,6 +31,7 @@ enum : int {
 struct KParams {
     int n, m, nb, npad, nnzP, nnzA, amax, gk, pk, ntgt, term_max;
     int gk1;          // most nonzeros in a row >= 128 (the two-wave kernel's second row slot)
+    int gkr, gkc;     // most nonzeros in a row / a column of A (gk = the larger)
     int bmax, pmeet;  // two-sided factorisation (solve_big.hip): tail width, meeting block
     int variant;  // solve-kernel instantiation (solve.hip: launch_solve)
     int mode;     // factor storage of that variant (solve.hip: factorize)
@@ -40,6 +41,10 @@ struct KParams {
     const int *asm_blk_ptr, *asm_tgt, *tterm, *acsr_pos, *gcol, *grow, *gpsym, *toff;
     const int* bsize;  // [nb] real variables of each block (the rest of its 32 are padding, at the end)
     const int* tcnt;   // [ntgt] assembly terms per target, descending within a block (plan.cpp)
+    // eliminated variables (plan.h, Plan::eown): padded columns [nb S, nb S + ne), owned by
+    // block column eown[pc]'s lane; etterm: the ELL terms of their K_jj / K_pj (target 2e / 2e + 1)
+    int ne, ecnt, eterm_max;
+    const int *eown, *etterm;
     // workspace
     double *Px, *Ax, *q, *D, *l, *u, *E, *x, *z, *y, *scal, *F, *H, *Si, *dyc, *dxc;
     double *obj, *pri, *dua, *rho_est;

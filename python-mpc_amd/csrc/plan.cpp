@@ -2,6 +2,7 @@
 #include "plan.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <queue>
 
@@ -39,7 +40,7 @@ std::vector<std::vector<int>> bfs_levels(const Graph& g, int s, std::vector<int>
 }  // namespace
 
 std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
-                       const int32_t* Ai, Plan& pl) {
+                       const int32_t* Ai, Plan& pl, bool eliminate) {
     char buf[256];
     if (n <= 0 || m < 0) return "invalid dimensions";
     if (Pp[0] != 0 || Ap[0] != 0) return "CSC column pointers must start at 0";
@@ -75,12 +76,37 @@ std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const
         v.erase(std::unique(v.begin(), v.end()), v.end());
     }
 
+    // eliminated variables (Plan::eown): isolated vertices, and leaves whose neighbour keeps
+    // a degree >= 2 (of a two-vertex component the higher index goes), at most one leaf per
+    // parent, each with at most two A nonzeros (the four-wave kernel's rhs list, LE)
+    std::vector<int> par(n, -2);  // -2: kept, -1: eliminated isolated, >= 0: eliminated leaf of par
+    if (eliminate) {
+        std::vector<char> has_leaf(n, 0);
+        for (int j = 0; j < n; ++j) {
+            if (Ap[j + 1] - Ap[j] > 2) continue;
+            const size_t d = g.adj[j].size();
+            if (d == 0) { par[j] = -1; continue; }
+            if (d != 1) continue;
+            const int p = g.adj[j][0];
+            const size_t dp = g.adj[p].size();
+            if ((dp >= 2 || j > p) && !has_leaf[p]) { par[j] = p; has_leaf[p] = 1; }
+        }
+        // the reduced graph: eliminated vertices dropped
+        for (int j = 0; j < n; ++j)
+            if (par[j] != -2) g.adj[j].clear();
+        for (int v = 0; v < n; ++v) {
+            auto& a = g.adj[v];
+            a.erase(std::remove_if(a.begin(), a.end(), [&](int w) { return par[w] != -2; }), a.end());
+        }
+    }
+    auto kept = [&](int v) { return par[v] == -2; };
+
     // components, pseudo-peripheral BFS level structures
     std::vector<int> comp(n, -1), mark(n, -1);
     std::vector<std::vector<int>> all_levels, iso_levels;
     int stamp = 0;
     for (int v0 = 0; v0 < n; ++v0) {
-        if (comp[v0] >= 0) continue;
+        if (comp[v0] >= 0 || !kept(v0)) continue;
         // collect component
         std::vector<int> cv{v0};
         comp[v0] = v0;
@@ -125,20 +151,60 @@ std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const
         else
             blocks.push_back(L);
     }
-    pl.nb = (int)blocks.size();
-    pl.npad = pl.nb * kS;
-    pl.bsize.resize(pl.nb);
-    pl.var_pad.assign(n, -1);
-    pl.pad_var.assign(pl.npad, -1);
-    for (int k = 0; k < pl.nb; ++k) {
-        pl.bsize[k] = (int)blocks[k].size();
-        for (int t = 0; t < pl.bsize[k]; ++t) {
-            pl.var_pad[blocks[k][t]] = k * kS + t;
-            pl.pad_var[k * kS + t] = blocks[k][t];
+    if (eliminate) {
+        // greedy packing: consecutive runs of kS variables of the level order, a level split
+        // between two blocks.  Block-tridiagonal as long as no edge spans more than one block
+        // boundary (checked); taken when it saves a block (reduced slack layout: 125 variables
+        // in 4 blocks instead of 5 -- the four-wave kernel's shape)
+        std::vector<int> order;
+        for (auto& L : all_levels) order.insert(order.end(), L.begin(), L.end());
+        const int nbg = ((int)order.size() + kS - 1) / kS;
+        if (nbg < (int)blocks.size()) {
+            std::vector<int> bof(n, -1);
+            for (size_t t = 0; t < order.size(); ++t) bof[order[t]] = (int)t / kS;
+            bool ok = true;
+            for (int v : order)
+                for (int w : g.adj[v]) ok = ok && std::abs(bof[v] - bof[w]) <= 1;
+            if (ok) {
+                blocks.assign(nbg, {});
+                for (size_t t = 0; t < order.size(); ++t) blocks[t / kS].push_back(order[t]);
+            }
         }
     }
-    for (int j = 0; j < n; ++j)
+    pl.nb = (int)blocks.size();
+    pl.nbp = pl.nb * kS;
+    pl.bsize.resize(pl.nb);
+    pl.var_pad.assign(n, -1);
+    for (int k = 0; k < pl.nb; ++k) {
+        pl.bsize[k] = (int)blocks[k].size();
+        for (int t = 0; t < pl.bsize[k]; ++t) pl.var_pad[blocks[k][t]] = k * kS + t;
+    }
+    // eliminated columns: owners (the parent's block column; isolated ones on free block
+    // columns, lowest first), padded indices nbp + e in owner order
+    pl.eown.assign(pl.nbp, -1);
+    std::vector<int> owner_var(pl.nbp, -1);  // block column -> eliminated variable
+    if (eliminate) {
+        std::vector<int> iso;
+        for (int j = 0; j < n; ++j) {
+            if (par[j] >= 0) owner_var[pl.var_pad[par[j]]] = j;
+            else if (par[j] == -1) iso.push_back(j);
+        }
+        size_t next = 0;
+        for (int pc = 0; pc < pl.nbp && next < iso.size(); ++pc)
+            if (owner_var[pc] < 0) owner_var[pc] = iso[next++];
+        if (next < iso.size()) return build_plan(n, m, Pp, Pi, Ap, Ai, pl, false);  // no free columns left
+        for (int pc = 0; pc < pl.nbp; ++pc)
+            if (owner_var[pc] >= 0) {
+                pl.eown[pc] = pl.nbp + pl.ne;
+                pl.var_pad[owner_var[pc]] = pl.nbp + pl.ne++;
+            }
+    }
+    pl.npad = pl.nbp + ((pl.ne + 1) & ~1);  // even: the arrays after a padded-column vector stay 16-byte aligned
+    pl.pad_var.assign(pl.npad, -1);
+    for (int j = 0; j < n; ++j) {
         if (pl.var_pad[j] < 0) return "internal: unplaced variable";
+        pl.pad_var[pl.var_pad[j]] = j;
+    }
 
     // A by padded column
     pl.acsc_ptr.assign(pl.npad + 1, 0);
@@ -192,6 +258,7 @@ std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const
     const long SS = (long)kS * kS;
     std::string err;
     auto add = [&](int pi, int pj, int a, int b, int r) {
+        if (pi >= pl.nbp || pj >= pl.nbp) return;  // an eliminated column: its terms are etterm's
         int bi = pi / kS, bj = pj / kS, li = pi % kS, lj = pj % kS;
         if (bi == bj) terms.push_back({bi * 2 * SS + li * kS + lj, a, b, r});
         else if (bi == bj + 1) terms.push_back({bi * 2 * SS + SS + li * kS + lj, a, b, r});
@@ -293,6 +360,38 @@ std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const
     pl.acsr_pos.resize(pl.nnzA);
     for (int e = 0; e < pl.nnzA; ++e) pl.acsr_pos[e] = csc_pos[pl.acsr_v[e]];
     pl.csc_pos = csc_pos;
+    // eliminated columns: the terms of K_jj and K_pj (etterm)
+    if (pl.ne) {
+        auto pidx = [&](int i, int j) {  // value index of P(i, j) in the user's triu CSC, or -1
+            const int r = std::min(i, j), c = std::max(i, j);
+            for (int p = Pp[c]; p < Pp[c + 1]; ++p)
+                if (Pi[p] == r) return p;
+            return -1;
+        };
+        std::vector<std::vector<std::pair<int, int>>> et(2 * pl.ne);  // (a | b << 16, r)
+        for (int pc = 0; pc < pl.nbp; ++pc) {
+            if (pl.eown[pc] < 0) continue;
+            const int e = pl.eown[pc] - pl.nbp, j = pl.pad_var[pl.eown[pc]], p = par[j];
+            pl.ecnt = std::max(pl.ecnt, Ap[j + 1] - Ap[j]);
+            if (int v = pidx(j, j); v >= 0) et[2 * e].push_back({v, -1});
+            for (int q = Ap[j]; q < Ap[j + 1]; ++q) et[2 * e].push_back({csc_pos[q] | (csc_pos[q] << 16), Ai[q]});
+            if (p < 0) continue;
+            if (int v = pidx(p, j); v >= 0) et[2 * e + 1].push_back({v, -1});
+            for (int q = Ap[j]; q < Ap[j + 1]; ++q)
+                for (int qp = Ap[p]; qp < Ap[p + 1]; ++qp)
+                    if (Ai[qp] == Ai[q]) et[2 * e + 1].push_back({csc_pos[qp] | (csc_pos[q] << 16), Ai[q]});
+        }
+        pl.eterm_max = 1;
+        for (auto& t : et) pl.eterm_max = std::max(pl.eterm_max, (int)t.size());
+        const int nt = 2 * pl.ne;
+        pl.etterm.assign((size_t)2 * nt * pl.eterm_max, 0);
+        for (int t = 0; t < nt; ++t)
+            for (int k = 0; k < pl.eterm_max; ++k) {
+                int* w = &pl.etterm[2 * ((size_t)k * nt + t)];
+                if (k < (int)et[t].size()) { w[0] = et[t][k].first; w[1] = et[t][k].second; }
+                else { w[0] = pl.nnzA | (pl.nnzA << 16); w[1] = 0; }
+            }
+    }
     // packed gather lists (16-bit value position | 16-bit vector index << 16), padded
     // to kGS entries with (nnzA | 0): position nnzA holds a zero in the kernels' LDS copy
     pl.gather_k = std::max(pl.max_col_nnz, pl.max_row_nnz);

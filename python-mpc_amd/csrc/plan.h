@@ -64,10 +64,31 @@ struct Plan {
     // couple to block k+1, its last BFS level) lie in [toff[k], toff[k] + bmax)
     std::vector<int> toff;        // [nb]
     int bmax = 0;
+    // Eliminated variables (build_plan's `eliminate`): vertices of K's graph with at most one
+    // neighbour -- a leaf (the slack of a soft constraint couples only to the state it
+    // relaxes, vehicle_lateral_mpc_slack_increment.py:104-110) or an isolated vertex (the
+    // slack layout's dead u_prev slack columns) -- are taken out of the
+    // block-tridiagonal system by a scalar Schur complement: K_pp -= K_pj^2 / K_jj on the
+    // parent's diagonal, b_p -= (K_pj / K_jj) b_j on its right-hand side, and after the
+    // reduced solve  x_j = (b_j - K_pj x_p) / K_jj  elementwise.  They get the padded
+    // indices [nbp, nbp + ne) after the block columns (npad = nbp + ne, rounded up to
+    // even); every other per-column structure (gather lists, P rows) covers them as usual.
+    int nbp = 0;                  // block columns nb * S
+    int ne = 0;                   // eliminated variables
+    int ecnt = 0;                 // most A nonzeros in an eliminated column
+    std::vector<int> eown;        // [nbp] block column -> the eliminated column it owns (parent, or a
+                                  //       free column for an isolated one), -1: none
+    // K_jj (target 2e) and K_pj (target 2e + 1) of eliminated column nbp + e as ELL terms in
+    // tterm's format: slot j of target t at (j * 2 ne + t)
+    int eterm_max = 0;
+    std::vector<int> etterm;
 };
 
-// Returns "" on success, otherwise an error message.
+// Returns "" on success, otherwise an error message.  eliminate: take degree <= 1
+// vertices of K's graph out of the block system (see Plan::eown); the blocks are then
+// packed greedily (consecutive runs of S variables of the level order) when that gives
+// fewer blocks and stays block-tridiagonal.
 std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi,
-                       const int32_t* Ap, const int32_t* Ai, Plan& out);
+                       const int32_t* Ap, const int32_t* Ai, Plan& out, bool eliminate = false);
 
 }  // namespace mpcqp

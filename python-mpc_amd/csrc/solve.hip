@@ -692,6 +692,7 @@ static hipError_t go(const KParams& p, long B, double* xo, double* yo, int fo, h
 // three-phase solve.  variant_fits() is the exact precondition of each.
 bool variant_fits(const KParams& p, int v) {
     const int cs = (p.npad + T - 1) / T, rs = (p.m + T - 1) / T;
+    if (p.ne && v != 17) return false;  // eliminated variables: the four-wave kernel only
     switch (v) {
         case 0: case 7: return p.nb == 4 && p.amax <= 8 && p.gk <= 6 && cs <= 1 && rs <= 1;
         case 1: return p.nb == 8 && p.amax <= 8 && p.gk <= 8 && cs <= 1 && rs <= 1;
@@ -715,9 +716,18 @@ bool variant_fits(const KParams& p, int v) {
         case 14:
             return p.nb > 4 && p.nb <= 8 && p.amax <= 16 && p.bmax <= 16 && p.gk <= 8 && p.npad <= 256 &&
                    p.m <= 256 && lds_solve_bytes_big(p) <= 160 * 1024;
-        case 17:  // four waves, two workgroups per CU (two waves per SIMD): up to 80 KB of LDS each
-            return p.nb == 4 && p.amax <= 8 && p.gk <= 6 && p.pk <= 4 && p.m <= 256 && p.npad <= 128 &&
-                   p.nnzA <= 512 && p.nnzP <= 256 && lds_w2_bytes(p) <= 80 * 1024;
+        case 17: {  // four waves, two workgroups per CU (two waves per SIMD): up to 80 KB of LDS each
+            // with eliminated columns: one per upper-half lane (npad <= 256, the fused setup's one
+            // column per thread), at most two A nonzeros each (the rhs list LE), three A values per
+            // thread in the fused setup
+            KParams q2 = p;
+            q2.mode = 2;  // the LDS carve of mode 2 (fits may run before KParams::mode is set)
+            // (and column lists of up to 8 entries: the slack layout's u_prev columns have 7)
+            const bool el = p.ne > 0;
+            return p.nb == 4 && p.amax <= 8 && p.gkr <= 6 && p.gkc <= (el ? 8 : 6) && p.pk <= 4 && p.m <= 256 &&
+                   p.npad <= (el ? 256 : 128) && p.nnzA <= (el ? 768 : 512) && p.nnzP <= 256 &&
+                   (!el || (p.ecnt <= 2 && p.ne <= 128)) && lds_w2_bytes(q2) <= 80 * 1024;
+        }
         case 18: {  // eight waves, one workgroup per CU; the gather lists pack 16-bit LDS addresses
             KParams q2 = p;
             q2.mode = 2;  // the LDS carve of mode 2 (fits may run before KParams::mode is set)

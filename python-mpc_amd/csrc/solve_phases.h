@@ -501,7 +501,7 @@ __device__ __forceinline__ bool factorize_w2(const KP& p, SLds& L, const double 
 // The critical path of stage 1 is one block's pivots instead of two.  Same outputs.
 template <class KP>
 __device__ __forceinline__ bool factorize_w4(const KP& p, SLds& L, const double rho, double* __restrict__ Hg,
-                                             double* __restrict__ Sg) {
+                                             double* __restrict__ Sg, double* __restrict__ Fo) {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int amax = p.amax, as = amax * S;
     const long gstride = (long)amax * S;
@@ -525,6 +525,28 @@ __device__ __forceinline__ bool factorize_w4(const KP& p, SLds& L, const double 
 #endif
     assemble_block<false, true>(p, L, rho, w, Sg + (long)w * SS, Ek(w), lane, 64, wave_sync);
     wave_sync();
+    if (p.ne && lane < S) {
+        // eliminated columns (plan.h Plan::eown): the owner lane of block column w S + lane
+        // forms K_jj, K_pj of its column j, folds the Schur complement -K_pj^2 / K_jj into its
+        // diagonal entry of D_w, and leaves ec = K_pj / K_jj, ed = 1 / K_jj in the instance's F
+        // tiles (unused by the three-phase form) for the solve's rhs and x updates
+        const int pe = p.eown[w * S + lane];
+        if (pe >= 0) {
+            const int e = pe - p.nb * S, ne2 = 2 * p.ne;
+            const int2* __restrict__ et = (const int2*)p.etterm;
+            double kjj = p.sigma, kpj = 0.0;
+            for (int j = 0; j < p.eterm_max; ++j) {
+                const int2 a = et[(long)j * ne2 + 2 * e], c = et[(long)j * ne2 + 2 * e + 1];
+                kjj += a.y < 0 ? L.Pv[a.x] : rho_of(L.ct[a.y], rho) * L.Acsc[a.x & 0xFFFF] * L.Acsc[(unsigned)a.x >> 16];
+                kpj += c.y < 0 ? L.Pv[c.x] : rho_of(L.ct[c.y], rho) * L.Acsc[c.x & 0xFFFF] * L.Acsc[(unsigned)c.x >> 16];
+            }
+            const double ed = 1.0 / kjj, ec = kpj * ed;
+            Sg[(long)w * SS + lane * S + lane] -= kpj * ec;
+            Fo[2 * e] = ec;
+            Fo[2 * e + 1] = ed;
+        }
+        wave_sync();
+    }
     FPH(8)
     bool okw = gj_seg<1>(Sg + (long)w * SS, bufw, w ? amax : 0, p.bsize[w], nullptr);
     FPH(10)
@@ -797,7 +819,7 @@ __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, doub
     }
     if constexpr (TT == 256 && !POL) {  // the register-sweep kernels (variants 1-3), the four-wave kernel (17)
         if (p.mode == 1 && p.amax <= 16) return factorize_g(p, L, rho, Fg, Sg);
-        if (p.variant == 17 && p.mode == 2 && p.nb == 4 && p.amax <= 8) return factorize_w4(p, L, rho, Hg, Sg);
+        if (p.variant == 17 && p.mode == 2 && p.nb == 4 && p.amax <= 8) return factorize_w4(p, L, rho, Hg, Sg, Fg);
     }
     if constexpr (TT == 512 && !POL) {  // the eight-wave kernel (18)
         if (p.variant == 18 && p.mode == 2 && p.nb == 8 && p.amax <= 12) return factorize_w8(p, L, rho, Fg, Hg, Sg);

@@ -1025,13 +1025,23 @@ __global__ __launch_bounds__(T2, 1) void k_setup_solve_w2(KParams p, const doubl
 // every wave's path.  MPCQP_VARIANT=17 (A/B against variant 10).
 constexpr int T4 = 256;
 
-template <int K, int KPK, int QR>
+// EL: the plan has eliminated columns (plan.h Plan::eown; the slack layouts).  The upper
+// half-wave lane (1, r) of wave w then owns the eliminated column pe = eown[w S + r] of its
+// block column's variable: it folds -ec b_pe into its half of the block column's rhs sum
+// (b_p - (K_pj / K_jj) b_j, no extra exchange), keeps x_pe, q_pe and b_pe in its registers,
+// and after phase C sets  x~_pe = ed b_pe - ec x~_p  (ed = 1 / K_jj, ec = K_pj / K_jj,
+// factorize_w4) -- the elementwise back-substitution of the scalar Schur complement --
+// which the rows phase reads from xt like any other column.  Its termination-check column
+// is pe (the lower half keeps the block column).
+// K: row-list length, KC: column-list length (even: the rhs splits it over the half-waves).
+template <int K, int KPK, int QR, bool EL = false, int KC = K>
 __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restrict__ xo, double* __restrict__ yo) {
     const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int h = lane >> 5, r = lane & 31, rr = lane >> 3, ch = lane & 7;
     constexpr int NB = 4, NP = NB * (NB - 1) / 2;  // exactly four blocks (solve.hip::variant_fits)
-    static_assert(K % 2 == 0, "the rhs splits the column list over the half-waves");
-    constexpr int KH = K / 2;                       // column-list entries per half in the rhs
+    static_assert(KC % 2 == 0, "the rhs splits the column list over the half-waves");
+    constexpr int KH = KC / 2;                       // column-list entries per half in the rhs
+    constexpr int LE = 2;                           // A entries of an eliminated column (plan ecnt <= 2)
     const long b = instance_of(p);
     const int n = p.n, m = p.m, npad = p.npad, nnzP = p.nnzP, nnzA = p.nnzA;
     SL2 C = carve(p);
@@ -1082,12 +1092,19 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
     bool can_check = false, need_factor = true;
     const int pc = w * S + r;  // the lane's column (both halves; the lower half stores)
     const bool low = h == 0;
+    const int pe = (EL && !low) ? p.eown[pc] : -1;  // the upper lane's eliminated column, or -1
+    const int xc = pe >= 0 ? pe : pc;                // the column whose x, q the lane keeps
+    double* const Fo = p.F + b * (long)p.nb * SS;    // ec, ed of the eliminated columns (factorize_w4)
+    double ec = 0.0, ed = 0.0;
     const unsigned abase = lds_addr(L.Acsc), wbase = lds_addr(L.w), xbase = lds_addr(L.xt);
     const unsigned Xbase = lds_addr(C.X);
     bool cv = false;
     double Dv = 1.0, Ev = 1.0;
-    GatherW<K> cg, rg;
+    GatherW<KC> cg;
+    GatherW<K> rg;
     GatherW<KPK> pg;
+    GatherW<EL ? KH : 1> chs;  // EL: the half's share of the block column's list (cg holds pe's)
+    GatherW<LE> el;            // EL: the eliminated column's list (zero entries for other lanes)
     const int ri = min(tid, mp - 1);  // lanes past the padded rows repeat the inert last row
     const bool rows_wave = w * 64 < mp;  // wave-uniform
     PH(5)
@@ -1118,10 +1135,33 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 const int q = o >> 8, t = (o >> 5) & 7;
                 L.gl[o] = (q < NP && t < p.amax) ? Hg[(long)q * p.amax * S + (o & 255)] : 0.0;
             }
-            cv = low && p.pad_var[pc] >= 0;
-            cg.load(p.gcol + pc, npad, abase, wbase);
-            pg.load(p.gpsym + pc, npad, lds_addr(L.Pv), Xbase);
-            Dv = p.D[b * npad + pc];
+            if constexpr (EL) {
+                // the lane's check column: the block column (lower half) or pe (upper half)
+                const int col = low ? pc : pe;
+                cv = col >= 0 && p.pad_var[col] >= 0;
+                if (col >= 0) {
+                    cg.load(p.gcol + col, npad, abase, wbase);
+                    pg.load(p.gpsym + col, npad, lds_addr(L.Pv), Xbase);
+                } else {
+                    cg.clear(abase + 8u * nnzA, wbase);
+                    pg.clear(lds_addr(L.Pv) + 8u * nnzP, Xbase);
+                }
+                Dv = col >= 0 ? p.D[b * npad + col] : 1.0;
+                chs.load(p.gcol + (h ? KH : 0) * npad + pc, npad, abase, wbase);
+                if (pe >= 0) {
+                    el.load(p.gcol + pe, npad, abase, wbase);
+                    const int e = pe - p.nb * S;
+                    ec = Fo[2 * e];
+                    ed = Fo[2 * e + 1];
+                } else {
+                    el.clear(abase + 8u * nnzA, wbase);
+                }
+            } else {
+                cv = low && p.pad_var[pc] >= 0;
+                cg.load(p.gcol + pc, npad, abase, wbase);
+                pg.load(p.gpsym + pc, npad, lds_addr(L.Pv), Xbase);
+                Dv = p.D[b * npad + pc];
+            }
             Ev = ri < m ? p.E[b * m + ri] : 1.0;
             if (ri < m) rg.load(p.grow + ri, m, abase, xbase);  // by ri: duplicate lanes repeat its row
             else rg.clear(abase + 8u * nnzA, xbase);
@@ -1134,8 +1174,8 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
 #pragma unroll
             for (int c = 0; c < 16; c += 2) ld2(src + c, SB[c], SB[c + 1]);
         }
-        double X = C.X[pc], DX = 0.0;
-        const double Q = L.qv[pc];
+        double X = C.X[xc], DX = 0.0;
+        const double Q = L.qv[xc];
         // phase-C slots: pairs (j, w), j > w, split over the halves; pair NP is zero
         int gslot[2], tslot[2];
         {
@@ -1159,10 +1199,17 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
         // the half's share of the column list (KH entries; the list is zero-padded to K)
         GatherW<KH> ch2;
 #pragma unroll
-        for (int k = 0; k < KH; ++k) ch2.e[k] = h ? cg.e[k + KH] : cg.e[k];
+        for (int k = 0; k < KH; ++k) {
+            if constexpr (EL) ch2.e[k] = chs.e[k];
+            else ch2.e[k] = h ? cg.e[k + KH] : cg.e[k];
+        }
         double ca[KH];  // the half's A values of the column (registers for the run)
 #pragma unroll
         for (int k = 0; k < KH; ++k) ca[k] = lds_at(ch2.e[k] & 0xFFFFu);
+        double ea[LE];  // EL: the eliminated column's A values (zeros on the other lanes)
+#pragma unroll
+        for (int k = 0; k < LE; ++k) ea[k] = EL ? lds_at(el.e[k] & 0xFFFFu) : 0.0;
+        double bj = 0.0;  // EL: b of the eliminated column, from the rhs to phase C
         const double r_hi = RHO_EQ_OVER_RHO_INEQ * rho;
         double y = L.ys[ri], Z = C.Z[ri], dy = 0.0;
         // the row's A values and bounds stay in registers for the run (fewer LDS reads per
@@ -1211,7 +1258,21 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 double wv[KH];
 #pragma unroll
                 for (int k = 0; k < KH; ++k) wv[k] = lds_at(ch2.e[k] >> 16);
-                double v = low ? sigma * X - Q : 0.0;
+                double v;
+                if constexpr (EL) {
+                    // sigma x - q of the lane's column (upper: the eliminated one, whose list it
+                    // adds; zero entries on the other lanes), then the upper half's b_p share
+                    // carries -ec b_pe
+                    double we[LE];
+#pragma unroll
+                    for (int k = 0; k < LE; ++k) we[k] = lds_at(el.e[k] >> 16);
+                    bj = sigma * X - Q;
+#pragma unroll
+                    for (int k = 0; k < LE; ++k) bj += ea[k] * we[k];
+                    v = low ? bj : -(ec * bj);
+                } else {
+                    v = low ? sigma * X - Q : 0.0;
+                }
 #pragma unroll
                 for (int k = 0; k < KH; ++k) v += ca[k] * wv[k];
                 const unsigned vlo = (unsigned)__double2loint(v), vhi = (unsigned)__double2hiint(v);
@@ -1303,7 +1364,14 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 const double d1 = __hiloint2double((int)h2[1], (int)l2[1]);
                 const double xn = t + (d0 + d1);
                 if (low) L.xt[pc] = xn;
-                const double xnew = alpha * xn + (1.0 - alpha) * X;
+                double xl = xn;  // x~ of the lane's column
+                if constexpr (EL) {
+                    if (!low) {
+                        xl = ed * bj - ec * xn;
+                        if (pe >= 0) L.xt[pe] = xl;
+                    }
+                }
+                const double xnew = alpha * xl + (1.0 - alpha) * X;
                 DX = xnew - X;
                 X = xnew;
             }
@@ -1332,6 +1400,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
         }
         // run state back to LDS
         if (low) { C.X[pc] = X; L.dx[pc] = DX; }
+        if (EL && pe >= 0) { C.X[pe] = X; L.dx[pe] = DX; }
         if (rows_wave) { L.ys[ri] = y; C.Z[ri] = Z; C.dY[ri] = dy; }
         __syncthreads();
         can_check = p.check_term && (iter % p.check_term == 0);
@@ -1384,7 +1453,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                     pdx += pv * lds_at(va - Xbase + dxbase);
                 }
 #pragma unroll
-                for (int k = 0; k < K; ++k) {
+                for (int k = 0; k < KC; ++k) {
                     const unsigned e = cg.e[k];
                     aty += lds_at(e & 0xFFFFu) * lds_at((e >> 16) - wbase + ysbase);
                 }
@@ -1437,7 +1506,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                             double na[1] = {0.0};
                             double a = 0.0;
 #pragma unroll
-                            for (int k = 0; k < K; ++k) {
+                            for (int k = 0; k < KC; ++k) {
                                 const unsigned e = cg.e[k];
                                 a += lds_at(e & 0xFFFFu) * lds_at((e >> 16) - wbase + dYbase);
                             }
@@ -1529,16 +1598,16 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
 #undef PH
 }
 
-template <int K, int KPK, int QR>
+template <int K, int KPK, int QR, bool EL = false, int KC = K>
 __global__ __launch_bounds__(T4, 2) void k_solve_w4(KParams p, double* __restrict__ xo, double* __restrict__ yo,
                                                     int factor_only) {
-    solve_w4_body<K, KPK, QR>(p, xo, yo);
+    solve_w4_body<K, KPK, QR, EL, KC>(p, xo, yo);
     extern __shared__ __attribute__((aligned(16))) double sm[];
     order_epilogue<T4>(p, (int*)sm);
 }
 
 // setup (setup_r.h with 256 threads: one column and one row per thread) + solve
-template <int K, int KPK, int QR, int SK, int SAS>
+template <int K, int KPK, int QR, int SK, int SAS, bool EL = false, int KC = K>
 __global__ __launch_bounds__(T4, 2) void k_setup_solve_w4(KParams p, const double* __restrict__ Px_in,
                                                           const double* __restrict__ Ax_in,
                                                           const double* __restrict__ q_in,
@@ -1548,7 +1617,7 @@ __global__ __launch_bounds__(T4, 2) void k_setup_solve_w4(KParams p, const doubl
     extern __shared__ __attribute__((aligned(16))) double sm[];
     setup_r_body<T4, SK, 4, 1, SAS, 1>(p, instance_of(p), Px_in, Ax_in, q_in, l_in, u_in, sm);
     __syncthreads();
-    solve_w4_body<K, KPK, QR>(p, xo, yo);
+    solve_w4_body<K, KPK, QR, EL, KC>(p, xo, yo);
     order_epilogue<T4>(p, (int*)sm);
 }
 
@@ -2050,7 +2119,7 @@ __global__ __launch_bounds__(T8, 1) void k_solve_w8(KParams p, double* __restric
 // the fused kernel's instantiation for the plan, or 0: variant 10 and the 128-thread
 // register-list setup shape (one padded column per thread, two rows, four A values)
 static int setup_solve_fits(const KParams& p) {
-    if (p.variant == 17) return p.gk <= 6 && p.pk <= 4;  // variant_fits(17) covers the rest
+    if (p.variant == 17) return p.pk <= 4;  // variant_fits(17) covers the rest (list lengths, nnzA <= 2 or 3 x T4)
     return p.variant == 10 && p.npad <= T2 && p.m <= 2 * T2 && p.gk <= 6 && p.pk <= 4 && p.nnzA <= 4 * T2 &&
            p.nnzP <= 2 * T2;
 }
@@ -2064,7 +2133,9 @@ hipError_t launch_setup_solve(const KParams& p, long B, const double* Px, const 
     const size_t lds = std::max(lds_w2_bytes(p), lds_setup_r_bytes(p.nnzP, p.nnzA, p.npad, p.m));
     if (p.variant == 17) {
         // QR: rows of the G blocks phase C sums (the nonzero ones: amax)
-        auto k4 = p.amax <= 5 ? k_setup_solve_w4<6, 4, 5, 6, 2> : k_setup_solve_w4<6, 4, 8, 6, 2>;
+        // EL (eliminated columns, the slack layouts): three A values per setup thread
+        auto k4 = p.ne ? k_setup_solve_w4<6, 4, 8, 8, 3, true, 8>
+                       : (p.amax <= 5 ? k_setup_solve_w4<6, 4, 5, 6, 2> : k_setup_solve_w4<6, 4, 8, 6, 2>);
         hipError_t e = hipFuncSetAttribute((const void*)k4, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k4, dim3((unsigned)B), dim3(T4), lds, st, p, Px, Ax, q, l, u, xo, yo);
@@ -2116,7 +2187,7 @@ hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, i
         case 8: return go_w<6, 3>(p, B, xo, yo, factor_only, st, lds, ref);
         case 9: return go_w<8, 4>(p, B, xo, yo, factor_only, st, lds, ref);
         case 17: {
-            auto k = p.amax <= 5 ? k_solve_w4<6, 4, 5> : k_solve_w4<6, 4, 8>;
+            auto k = p.ne ? k_solve_w4<6, 4, 8, true, 8> : (p.amax <= 5 ? k_solve_w4<6, 4, 5> : k_solve_w4<6, 4, 8>);
             const size_t lds = lds_w2_bytes(p);
             if (ref) { *ref = {(const void*)k, T4, lds}; return hipSuccess; }
             hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -81,6 +81,7 @@ class _PlanInfo(C.Structure):
         ("npad", C.c_int32), ("max_level", C.c_int32), ("batch", C.c_int64),
         ("n_devices", C.c_int32), ("lds_bytes_solve", C.c_int64), ("bytes_per_instance", C.c_int64),
         ("amax", C.c_int32), ("gather_k", C.c_int32), ("variant", C.c_int32), ("threads_per_qp", C.c_int32),
+        ("n_eliminated", C.c_int32),
     ]
 
 
@@ -138,6 +139,8 @@ def lib():
     L.mpcqp_free.restype = None
     L.mpcqp_analyze.argtypes = [C.c_int32, C.c_int32, i32p, i32p, i32p, i32p,
                                 i32p, i32p, i32p, i32p]
+    L.mpcqp_analyze_ex.argtypes = [C.c_int32, C.c_int32, i32p, i32p, i32p, i32p, C.c_int32,
+                                   i32p, i32p, i32p, i32p, i32p]
     _lib = L
     return L
 
@@ -189,17 +192,20 @@ def canonical_data(P, A):
     return P, A
 
 
-def analyze(P, A):
-    """Host-only symbolic analysis (no GPU): returns (nb, block, var_pad, bsize)."""
+def analyze(P, A, eliminate=False):
+    """Host-only symbolic analysis (no GPU): returns (nb, block, var_pad, bsize), and with
+    `eliminate` (the plan of the four-wave kernel: degree <= 1 vertices of K taken out of
+    the blocks, padded indices from nb * block on) also the number eliminated."""
     P, A = canonical_data(P, A)
     n, m = P.shape[0], A.shape[0]
-    nb = C.c_int32(); blk = C.c_int32()
+    nb = C.c_int32(); blk = C.c_int32(); ne = C.c_int32()
     vp = np.empty(n, np.int32); bs = np.empty(max(n, 1), np.int32)
     Pp = np.ascontiguousarray(P.indptr, np.int32); Pi = np.ascontiguousarray(P.indices, np.int32)
     Ap = np.ascontiguousarray(A.indptr, np.int32); Ai = np.ascontiguousarray(A.indices, np.int32)
-    _check(lib().mpcqp_analyze(n, m, _ip(Pp), _ip(Pi), _ip(Ap), _ip(Ai), C.byref(nb), C.byref(blk),
-                               _ip(vp), _ip(bs)), "analyze")
-    return nb.value, blk.value, vp, bs[: nb.value].copy()
+    _check(lib().mpcqp_analyze_ex(n, m, _ip(Pp), _ip(Pi), _ip(Ap), _ip(Ai), int(eliminate), C.byref(nb),
+                                  C.byref(blk), _ip(vp), _ip(bs), C.byref(ne)), "analyze")
+    out = (nb.value, blk.value, vp, bs[: nb.value].copy())
+    return out + (ne.value,) if eliminate else out
 
 
 def _drop_common_zeros(M, V):

@@ -116,3 +116,67 @@ def test_no_cpu_fallback_without_device():
     P, q, A, l, u = _tiny()
     with pytest.raises(RuntimeError, match="no HIP device"):
         osqp_amd.OSQP().setup(P, q, A, l, u, verbose=False)
+
+
+@pytest.mark.parametrize("cfg", [1, 3])
+def test_elimination_plan_slack_layout(cfg):
+    """The plan the four-wave kernel runs for the slack layouts (plan.h Plan::eown): the 84
+    live slack columns (leaves of K's graph: each touches only the state it relaxes) and
+    the 21 dead u_prev slack columns (isolated) leave the block system, whose 125 variables
+    then pack into 4 blocks of 32 (block-tridiagonal in the reduced graph)."""
+    b = mpc.make_batch(cfg, B=2, seed=3)
+    P, _ = osqp_amd._drop_common_zeros(b["P"], b["Px"])
+    A, _ = osqp_amd._drop_common_zeros(b["A"], b["Ax"])
+    nb, blk, var_pad, bsize, ne = osqp_amd.analyze(P, A, eliminate=True)
+    n = P.shape[0]
+    assert (n, nb, ne) == (230, 4, 105) and bsize.sum() == n - ne
+    assert len(np.unique(var_pad)) == n
+    elim = var_pad >= nb * blk
+    assert elim.sum() == ne and np.all(elim[125:] == (np.arange(125, 230) >= 125))  # the slack block s_0..s_N
+    r, c = _kkt_pattern(P, A)
+    keep = ~elim[r] & ~elim[c]
+    block = var_pad // blk
+    assert np.max(np.abs(block[r[keep]] - block[c[keep]])) <= 1
+    # each eliminated column couples to at most one kept column, never to another eliminated one
+    off = r != c
+    assert not np.any(elim[r[off]] & elim[c[off]])
+    assert np.bincount(r[off & elim[r]], minlength=n).max() <= 1
+
+
+def test_elimination_schur_complement_solves_the_full_system():
+    """The algebra the four-wave kernel runs for an eliminated column j with parent p
+    (factorize_w4, solve_w4_body): K_pp -= K_pj^2 / K_jj, b_p -= (K_pj / K_jj) b_j, then
+    x_j = (b_j - K_pj x_p) / K_jj -- the exact solution of the full system K x = b."""
+    b = mpc.make_batch(3, B=1, seed=5)
+    P = b["P"]; A = b["A"]
+    n = P.shape[0]
+    Pf = (P + P.T - sparse.diags(P.diagonal())).toarray()
+    rho = np.where(b["u"][0] - b["l"][0] < 1e-4, 100.0, 0.1)
+    K = Pf + 1e-6 * np.eye(n) + A.T.toarray() @ np.diag(rho) @ A.toarray()
+    rhs = np.random.default_rng(0).normal(size=n)
+    x_ref = np.linalg.solve(K, rhs)
+    Pz, _ = osqp_amd._drop_common_zeros(b["P"], b["Px"])
+    Az, _ = osqp_amd._drop_common_zeros(b["A"], b["Ax"])
+    nb, blk, var_pad, bsize, ne = osqp_amd.analyze(Pz, Az, eliminate=True)
+    elim = np.flatnonzero(var_pad >= nb * blk)
+    keep = np.flatnonzero(var_pad < nb * blk)
+    Kr = K[np.ix_(keep, keep)].copy()
+    br = rhs[keep].copy()
+    pos = {v: i for i, v in enumerate(keep)}
+    coup = {}
+    for j in elim:
+        nbrs = [p for p in np.flatnonzero(K[j]) if p != j]
+        assert len(nbrs) <= 1
+        if nbrs:
+            p = nbrs[0]
+            ec = K[p, j] / K[j, j]
+            Kr[pos[p], pos[p]] -= K[p, j] * ec
+            br[pos[p]] -= ec * rhs[j]
+            coup[j] = (p, ec)
+    xr = np.linalg.solve(Kr, br)
+    x = np.empty(n)
+    x[keep] = xr
+    for j in elim:
+        p, ec = coup.get(j, (None, 0.0))
+        x[j] = rhs[j] / K[j, j] - (ec * x[p] if p is not None else 0.0)
+    assert np.allclose(x, x_ref, rtol=1e-9, atol=1e-12)

@@ -617,3 +617,32 @@ def test_repeat_solves_are_bitwise_identical(cfg, B):
     for r in outs[1:]:
         assert np.array_equal(r.x, outs[0].x) and np.array_equal(r.y, outs[0].y)
         assert np.array_equal(r.iter, outs[0].iter)
+
+
+@pytest.mark.parametrize("B", [512, 1000])
+def test_slack_elimination_matches_full_system(monkeypatch, B):
+    """The slack layout runs the four-wave kernel on its reduced system (plan.h Plan::eown:
+    105 slack columns eliminated by a scalar Schur complement, 125 variables in 4 blocks);
+    MPCQP_ELIM=0 runs the full 230-variable system (8 blocks, the 256-thread register-sweep
+    kernel).  Both must match the oracle and each other: same statuses, iteration counts
+    for >= 99 % of the instances, and u within the north-star 1e-4."""
+    b = mpc.make_batch(3, B=B, seed=13)
+    s = dict(warm_start=True)
+    bg = OSQPBatch()
+    bg.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
+    info = bg.plan_info()
+    assert (info["nb"], info["n_eliminated"], info["variant"]) == (4, 105, 17)
+    rg = bg.solve()
+    monkeypatch.setenv("MPCQP_ELIM", "0")
+    bf = OSQPBatch()
+    bf.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
+    assert bf.plan_info()["n_eliminated"] == 0 and bf.plan_info()["nb"] == 8
+    rf = bf.solve()
+    assert (rg.status_val == rf.status_val).all()
+    same = rg.iter == rf.iter
+    assert same.mean() >= 0.99
+    du = np.abs(rg.x[:, b["u_block"]] - rf.x[:, b["u_block"]]).max(axis=1)
+    assert np.all(du[same] < U_TOL), du.max()
+    # slack values (the eliminated columns) agree too
+    sl = slice(125, 230)
+    assert np.all(np.abs(rg.x[same][:, sl] - rf.x[same][:, sl]).max(axis=1) < 1e-4)
