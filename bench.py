@@ -220,7 +220,7 @@ def solve_kernel_name(info, fused):
 
 def pmc_traffic(workload, batch, kernel):
     """HBM bytes per k_solve launch from rocprofv3 PMC passes committed under
-    profiles/ (tools/pmc_traffic.py writes profiles/traffic_<workload>_b<B>.json:
+    profiles/ (tools/gpu_profile.sh + tools/pmc_summary.py give traffic.json, copied to profiles/traffic_<workload>_b<B>.json:
     FETCH_SIZE and WRITE_SIZE from separate --pmc passes, FETCH_SIZE doubled per
     the gfx950 note of MI355X_MICROARCH.md).  {} when not measured."""
     path = os.path.join(ROOT, "profiles", f"traffic_{workload}_b{batch}.json")

@@ -1094,17 +1094,14 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
     const bool low = h == 0;
     const int pe = (EL && !low) ? p.eown[pc] : -1;  // the upper lane's eliminated column, or -1
     const int xc = pe >= 0 ? pe : pc;                // the column whose x, q the lane keeps
+    const bool colv = low && p.pad_var[pc] >= 0;     // a real block column (padding: rb = 0)
     double* const Fo = p.F + b * (long)p.nb * SS;    // ec, ed of the eliminated columns (factorize_w4)
     double ec = 0.0, ed = 0.0;
     const unsigned abase = lds_addr(L.Acsc), wbase = lds_addr(L.w), xbase = lds_addr(L.xt);
     const unsigned Xbase = lds_addr(C.X);
-    bool cv = false;
-    double Dv = 1.0, Ev = 1.0;
-    GatherW<KC> cg;
     GatherW<K> rg;
-    GatherW<KPK> pg;
-    GatherW<EL ? KH : 1> chs;  // EL: the half's share of the block column's list (cg holds pe's)
-    GatherW<LE> el;            // EL: the eliminated column's list (zero entries for other lanes)
+    GatherW<KH> chs;  // the half's share of the block column's list (the rhs sums)
+    GatherW<LE> el;   // EL: the eliminated column's list (zero entries for the other lanes)
     const int ri = min(tid, mp - 1);  // lanes past the padded rows repeat the inert last row
     const bool rows_wave = w * 64 < mp;  // wave-uniform
     PH(5)
@@ -1135,19 +1132,8 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 const int q = o >> 8, t = (o >> 5) & 7;
                 L.gl[o] = (q < NP && t < p.amax) ? Hg[(long)q * p.amax * S + (o & 255)] : 0.0;
             }
+            chs.load(p.gcol + (h ? KH : 0) * npad + pc, npad, abase, wbase);
             if constexpr (EL) {
-                // the lane's check column: the block column (lower half) or pe (upper half)
-                const int col = low ? pc : pe;
-                cv = col >= 0 && p.pad_var[col] >= 0;
-                if (col >= 0) {
-                    cg.load(p.gcol + col, npad, abase, wbase);
-                    pg.load(p.gpsym + col, npad, lds_addr(L.Pv), Xbase);
-                } else {
-                    cg.clear(abase + 8u * nnzA, wbase);
-                    pg.clear(lds_addr(L.Pv) + 8u * nnzP, Xbase);
-                }
-                Dv = col >= 0 ? p.D[b * npad + col] : 1.0;
-                chs.load(p.gcol + (h ? KH : 0) * npad + pc, npad, abase, wbase);
                 if (pe >= 0) {
                     el.load(p.gcol + pe, npad, abase, wbase);
                     const int e = pe - p.nb * S;
@@ -1156,13 +1142,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 } else {
                     el.clear(abase + 8u * nnzA, wbase);
                 }
-            } else {
-                cv = low && p.pad_var[pc] >= 0;
-                cg.load(p.gcol + pc, npad, abase, wbase);
-                pg.load(p.gpsym + pc, npad, lds_addr(L.Pv), Xbase);
-                Dv = p.D[b * npad + pc];
             }
-            Ev = ri < m ? p.E[b * m + ri] : 1.0;
             if (ri < m) rg.load(p.grow + ri, m, abase, xbase);  // by ri: duplicate lanes repeat its row
             else rg.clear(abase + 8u * nnzA, xbase);
             PH(0)
@@ -1197,12 +1177,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
         }
         const int nsw = (NB - w) >> 1;  // phase-C slots of the wave (wave 0: 2, waves 1-2: 1, wave 3: 0)
         // the half's share of the column list (KH entries; the list is zero-padded to K)
-        GatherW<KH> ch2;
-#pragma unroll
-        for (int k = 0; k < KH; ++k) {
-            if constexpr (EL) ch2.e[k] = chs.e[k];
-            else ch2.e[k] = h ? cg.e[k + KH] : cg.e[k];
-        }
+        const GatherW<KH>& ch2 = chs;
         double ca[KH];  // the half's A values of the column (registers for the run)
 #pragma unroll
         for (int k = 0; k < KH; ++k) ca[k] = lds_at(ch2.e[k] & 0xFFFFu);
@@ -1280,7 +1255,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 const auto h2 = __builtin_amdgcn_permlane32_swap(vhi, vhi, false, false);
                 const double v0 = __hiloint2double((int)h2[0], (int)l2[0]);
                 const double v1 = __hiloint2double((int)h2[1], (int)l2[1]);
-                if (low) L.rb[pc] = cv ? v0 + v1 : 0.0;
+                if (low) L.rb[pc] = colv ? v0 + v1 : 0.0;
             }
             __syncthreads();
             PH(1)
@@ -1409,6 +1384,23 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
         info_iter = iter;
         bool stop = false;
         {
+            // the check's per-lane operands come from the plan (shared by every instance: L2
+            // hits) and the workspace here, not from registers held through the run: the lane's
+            // column (EL: the upper half checks its eliminated column pe) with its A and P lists
+            // and D, the row's E
+            const int col = EL ? (low ? pc : pe) : pc;
+            const bool cv = col >= 0 && (EL || low) && p.pad_var[col] >= 0;
+            GatherW<KC> cg;
+            GatherW<KPK> pg;
+            if (col >= 0) {
+                cg.load(p.gcol + col, npad, abase, wbase);
+                pg.load(p.gpsym + col, npad, lds_addr(L.Pv), Xbase);
+            } else {
+                cg.clear(abase + 8u * nnzA, wbase);
+                pg.clear(lds_addr(L.Pv) + 8u * nnzP, Xbase);
+            }
+            const double Dv = col >= 0 ? p.D[b * npad + col] : 1.0;
+            const double Ev = ri < m ? p.E[b * m + ri] : 1.0;
             // inline update_info + check_termination (as solve_w2_body's), one row per thread
             const bool unscale = p.scaling && !p.scaled_term;
             const unsigned ysbase = lds_addr(L.ys), dYbase = lds_addr(C.dY), dxbase = lds_addr(L.dx);

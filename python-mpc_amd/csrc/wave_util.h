@@ -13,6 +13,10 @@ template <int K>
 struct GatherW {
     unsigned e[K];
     __device__ __forceinline__ void load(const int* list, int stride, unsigned abase, unsigned vbase) {
+        // the stride passes through an empty asm: the K entry addresses are formed here, at
+        // each (re)load, instead of being hoisted out of the solve loop as K loop-invariant
+        // 64-bit pointers per lane (which the four-wave kernel then spilled to scratch)
+        asm volatile("" : "+s"(stride));
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const unsigned raw = (unsigned)list[(long)k * stride];
