@@ -73,6 +73,10 @@ def parse(argv=None):
                     help="per-step jitter of the initial states, fraction of the D2 half-range")
     ap.add_argument("--independent", action="store_true",
                     help="every step's initial states drawn afresh from the D2 ranges (no correlation between steps)")
+    ap.add_argument("--assemble", action="store_true",
+                    help="lateral layouts (cfg 2/3/4): each step builds q, l, u on the device from the instances' "
+                         "(x0, xr, bound regime) (SURVEY.md §8f F1) and solves with one shared P, A -- timed "
+                         "from x0 alone; a separate metric, not the headline")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--separate-setup", action="store_true",
@@ -181,29 +185,49 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
-def bound_sequence(b, count, seed, to_dev, jitter=JITTER, independent=False):
-    """`count` distinct (l, u) device pairs of batch `b`: the first unchanged, each later
-    one with the initial-state rows (l = u = -x0) jittered (`jitter`, clipped to the D2
-    ranges) or, `independent`, drawn afresh from the D2 ranges.  Everything else of the
-    QP (P, A, q, the other bounds) is shared."""
+def x0_sequence(b, count, seed, jitter=JITTER, independent=False):
+    """`count` initial-state arrays (B, nx0) of batch `b`: the first its own, each later one
+    jittered (`jitter` of the D2 half-range, clipped to the D2 ranges) or, `independent`,
+    drawn afresh from the D2 ranges."""
     from osqp_amd import mpc
     rng = np.random.default_rng(seed + 7919)
     lo, hi = (np.array(v) for v in zip(*X0_RANGES[mpc.CONFIGS[b["cfg"]]["layout"]]))
-    nx0 = lo.size
-    x0 = -b["l"][:, :nx0]
-    dl0, du0 = to_dev(b["l"]), to_dev(b["u"])
-    seq = [(dl0, du0)]
+    x0 = -b["l"][:, :lo.size]
+    seq = [x0]
     for _ in range(count - 1):
         if independent:
-            xt = lo + (hi - lo) * rng.uniform(0, 1, x0.shape)
+            seq.append(lo + (hi - lo) * rng.uniform(0, 1, x0.shape))
         else:
-            xt = np.clip(x0 + jitter * 0.5 * (hi - lo) * rng.uniform(-1, 1, x0.shape), lo, hi)
+            seq.append(np.clip(x0 + jitter * 0.5 * (hi - lo) * rng.uniform(-1, 1, x0.shape), lo, hi))
+    return seq
+
+
+def bound_sequence(b, count, seed, to_dev, jitter=JITTER, independent=False):
+    """`count` distinct (l, u) device pairs of batch `b`: the initial-state rows (l = u = -x0)
+    from x0_sequence; everything else of the QP (P, A, q, the other bounds) is shared."""
+    xs = x0_sequence(b, count, seed, jitter, independent)
+    nx0 = xs[0].shape[1]
+    dl0, du0 = to_dev(b["l"]), to_dev(b["u"])
+    seq = [(dl0, du0)]
+    for xt in xs[1:]:
         dxt = to_dev(-xt)
         dl, du = dl0.clone(), du0.clone()
         dl[:, :nx0] = dxt
         du[:, :nx0] = dxt
         seq.append((dl, du))
     return seq
+
+
+def theta_sequence(b, count, seed, to_dev, jitter=JITTER, independent=False):
+    """The same steps as parameters theta = (x0, xr) of the lateral assembler (F1,
+    osqp_amd.mpc_device.LateralAssembler): the device builds q, l, u from them."""
+    xs = x0_sequence(b, count, seed, jitter, independent)
+    out = []
+    for xt in xs:
+        th = b["theta"].copy()
+        th[:, :xt.shape[1]] = xt
+        out.append(to_dev(th))
+    return out
 
 
 def solve_kernel_name(info, fused):
@@ -279,8 +303,23 @@ def main(argv=None, solver_cls=None, device=None):
 
     dPx, dAx, dq = (to_dev(a) for a in (Px, Ax, b["q"]))
     # the base batch, then one distinct batch per warmup and timed step
-    seq = bound_sequence(b, 1 + args.warmup + args.steps, instance_seed(args.config, rank), to_dev,
-                         jitter=args.jitter, independent=args.independent)
+    nsteps = 1 + args.warmup + args.steps
+    if args.assemble:
+        if b.get("theta") is None:
+            raise SystemExit("--assemble: the lateral layouts only (cfg 2, 3, 4)")
+        from osqp_amd.mpc_device import LateralAssembler
+        asm = LateralAssembler(spec["layout"], N=b["N"], device=local)
+        dPx, dAx = (to_dev(v) for v in asm.matrices())  # ONE P and A for the batch (shared-matrix mode)
+        ths = theta_sequence(b, nsteps, instance_seed(args.config, rank), to_dev, jitter=args.jitter,
+                             independent=args.independent)
+        dreg = to_dev(b["regime"], dtype=torch.int32)
+        dq = torch.empty((B, b["n"]), dtype=torch.float64, device=dev)
+        dlv = torch.empty((B, b["m"]), dtype=torch.float64, device=dev)
+        duv = torch.empty((B, b["m"]), dtype=torch.float64, device=dev)
+        seq = [(dlv, duv)] * nsteps
+    else:
+        seq = bound_sequence(b, nsteps, instance_seed(args.config, rank), to_dev,
+                             jitter=args.jitter, independent=args.independent)
     dl, du = seq[0]
     dx = torch.empty((B, n), dtype=torch.float64, device=dev)
     dy = torch.empty((B, m), dtype=torch.float64, device=dev)
@@ -303,6 +342,8 @@ def main(argv=None, solver_cls=None, device=None):
 
     def step(t, sv=solver, fused=not args.separate_setup):
         sl, su = seq[t]
+        if args.assemble:  # F1: q, l, u from theta on the device, on the solver's stream order
+            asm.assemble(ths[t], dreg, out=(dq, sl, su), stream=sv.stream_handle())
         if warm:  # setup, then the warm start, then the solve
             sv.setup(dPx, dAx, dq, sl, su)
             sv.warm_start(xs, ys)
@@ -376,6 +417,8 @@ def main(argv=None, solver_cls=None, device=None):
     nnzP_alg = float(np.count_nonzero(Px) / B)
     nnzA_alg = float(np.count_nonzero(Ax) / B)
     bytes_per_solve = 8 * (nnzP_alg + nnzA_alg + n + 2 * m) + 8 * (n + m) + (8 * (n + m) if warm else 0)
+    if args.assemble:  # from the parameters: theta in, x and y out (P, A shared: read once per launch)
+        bytes_per_solve = 8 * ths[0].shape[1] + 4 + 8 * (n + m)
     solve_ms = kt["solve_ms"] / max(1, kt["n_solve"])
     setup_ms = kt["setup_ms"] / kt["n_setup"] if kt["n_setup"] else None  # None: setup runs inside the fused kernel
     achieved = bytes_per_solve * B / (solve_ms * 1e-3) / 1e9
@@ -424,8 +467,9 @@ def main(argv=None, solver_cls=None, device=None):
     if rank == 0:
         kname = solve_kernel_name(info, fused=fused)
         line = {
-            "metric": "QP solves/sec (batch) at N=20 nx=4 nu=1" if args.config == 2 else
-                      f"QP solves/sec (batch), {spec['name']}",
+            "metric": ("QP solves/sec (batch) at N=20 nx=4 nu=1" if args.config == 2 else
+                       f"QP solves/sec (batch), {spec['name']}") +
+                      (", incl. on-device QP assembly from x0 (F1, shared P/A)" if args.assemble else ""),
             "value": value,
             "unit": "QP solves/s",
             "n_gpus": world,

@@ -159,6 +159,14 @@ int mpcqp_solve_device(mpcqp_handle *h, double *dx, double *dy, int32_t *dstatus
 int mpcqp_setup_solve_device(mpcqp_handle *h, const double *dPx, const double *dAx, const double *dq,
                              const double *dl, const double *du, double *dx, double *dy, int32_t *dstatus,
                              int32_t *diters, void *stream);
+/* LTI batches ("LTI shared-matrix mode"): with shared != 0 the following
+ * mpcqp_setup_device / mpcqp_setup_solve_device calls read ONE Px[nnzP] and ONE Ax[nnzA]
+ * for every instance of the batch instead of B copies (the lateral MPC's P and A do not
+ * change between instances or steps: vehicle_lateral_mpc_slack_increment.py:79-115). */
+int mpcqp_set_shared_matrices(mpcqp_handle *h, int32_t shared);
+/* The handle's own hipStream_t (the one a NULL `stream` selects; first shard), so that a
+ * caller's kernels (e.g. mpcqp_affine_apply_device) can be ordered with the handle's calls. */
+void *mpcqp_get_stream(const mpcqp_handle *h);
 /* Blocks until every call enqueued on the handle so far has finished, on the handle's
  * own stream(s) and on the caller stream the last *_device call used. */
 int mpcqp_synchronize(mpcqp_handle *h);
@@ -241,6 +249,24 @@ int mpcqp_incr_assemble_device(const mpcqp_incr_layout *L, int64_t B, const doub
                                const double *dgd, const double *dxt0, const double *dXr, double *dAx, double *dq,
                                double *dl, double *du, void *stream);
 void mpcqp_incr_layout_free(mpcqp_incr_layout *L);
+
+/* F1 for the LTI lateral layouts (vehicle_lateral_mpc_slack_increment.py:32-121 and its loop
+ * :201-229; Control/MPC/mpc_kinematics.py:148-191 with the lateral model): their P and A
+ * are the same for every instance and step (mpcqp_set_shared_matrices), and every entry of
+ * the concatenated (q | l | u) is affine in the instance's parameters theta = (x0, xr) with
+ * a base vector per bound regime (the script's i <= 400 / <= 900 / else schedule, :158-172):
+ *     v[i] = base[regime][i] + sum_{t < T} coef[i*T + t] * theta[idx[i*T + t]]   (idx -1: none)
+ * The map is built once on the host from the layout's builder (osqp_amd.mpc_device.
+ * LateralAssembler); mpcqp_affine_apply_device then writes q[B*seglen0], l[B*seglen1],
+ * u[B*seglen2] from theta[b*theta_stride + k] and regime[b] (NULL: regime 0; clamped to
+ * [0, nregimes)), one thread per (instance, entry).  An entry with terms is the terms' sum
+ * (plus its base where that is nonzero), so a product the builder forms alone is exact. */
+typedef struct mpcqp_affine mpcqp_affine;
+int mpcqp_affine_create(int32_t nseg, const int32_t *seglen, int32_t nregimes, int32_t T, const double *base,
+                        const int32_t *idx, const double *coef, int32_t device, mpcqp_affine **out);
+int mpcqp_affine_apply_device(const mpcqp_affine *a, int64_t B, const double *dtheta, int32_t theta_stride,
+                              const int32_t *dregime, double *dout0, double *dout1, double *dout2, void *stream);
+void mpcqp_affine_free(mpcqp_affine *a);
 
 /* F3 -- reference_search (mpc_dynamics.py:44-90, nearest_point :30-41) for every
  * vehicle: pred[b*(N+1)*nxa + k*nxa + 0..nxa) predicted augmented states

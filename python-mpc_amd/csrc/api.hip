@@ -688,6 +688,16 @@ int mpcqp_setup_solve_device(mpcqp_handle* h, const double* dPx, const double* d
     return stream_leave(s, st);
 }
 
+void* mpcqp_get_stream(const mpcqp_handle* h) {
+    return (h && !h->shards.empty()) ? (void*)h->shards[0].stream : nullptr;
+}
+
+int mpcqp_set_shared_matrices(mpcqp_handle* h, int32_t shared) {
+    if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "device entry points need a single-device handle");
+    h->shards[0].kp.mat_shared = shared ? 1 : 0;
+    return 0;
+}
+
 int mpcqp_synchronize(mpcqp_handle* h) {
     if (!h) return fail(MPCQP_EINVAL, "NULL handle");
     return sync_all(h);

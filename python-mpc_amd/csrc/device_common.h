@@ -4,6 +4,25 @@
 
 #include "kernels.h"
 
+#ifdef MPCQP_SKEW
+// Barrier-race debug build (make skew -> libmpcqp_skew.so; tests/test_skew.py): after every
+// workgroup barrier about half of the waves, picked by their wave index and the scalar clock
+// (so a different half at each barrier), sleep ~1,300 cycles before going on.  A hand-off
+// between waves that lacks a barrier -- a wave reading what another writes, or overwriting
+// what another still reads -- then sees the other wave's stale or new data within a few
+// barriers, instead of in 1 of ~4 runs (the round-2 y-park race).  Results of a race-free
+// kernel are bit-identical to the production build's.
+__device__ inline __attribute__((convergent)) void mpcqp_skew_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const unsigned w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const unsigned t = (unsigned)(__builtin_amdgcn_s_memtime() >> 3);
+    if (((t ^ (w * 0x9E3779B9u)) >> 7) & 1u) __builtin_amdgcn_s_sleep(20);
+}
+#define __syncthreads() mpcqp_skew_barrier()
+#endif
+
 namespace mpcqp {
 
 // OSQP 0.6 constants (constants.h of the published solver)

@@ -66,6 +66,9 @@ struct KParams {
     // k_setup_solve_w2) sort the order themselves in their last workgroup (device_common.h::order_epilogue)
     // when the batch is at most kOrderFuseMax: arrival counter (zero between launches), or null
     int* done;
+    // setup calls: P and A values shared by every instance (Px[nnzP], Ax[nnzA] instead of
+    // B copies; LTI MPC -- mpcqp_set_shared_matrices)
+    int mat_shared;
 };
 constexpr long kOrderFuseMax = 16384;  // larger batches sort in k_order (1024 threads)
 

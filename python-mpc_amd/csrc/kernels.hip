@@ -63,8 +63,9 @@ __global__ __launch_bounds__(T) void k_setup(KParams p, const double* __restrict
     const int *acsr_ptr = rebase(p.acsr_ptr), *acsr_v = rebase(p.acsr_v);
     const int *p_r = rebase(p.p_r), *p_c = rebase(p.p_c), *a_r = rebase(p.a_r), *a_c = rebase(p.a_c);
 
-    for (int i = tid; i < nnzP; i += T) Pv[i] = Px_in[b * nnzP + i];
-    for (int i = tid; i < nnzA; i += T) Av[i] = Ax_in[b * nnzA + i];
+    const long bm = p.mat_shared ? 0 : b;  // LTI batches: one P, A for every instance
+    for (int i = tid; i < nnzP; i += T) Pv[i] = Px_in[bm * nnzP + i];
+    for (int i = tid; i < nnzA; i += T) Av[i] = Ax_in[bm * nnzA + i];
     __syncthreads();  // the staged indices
     for (int pc = tid; pc < npad; pc += T) {
         int j = pad_var[pc];

@@ -374,11 +374,59 @@ __global__ __launch_bounds__(128) void k_incr_shift(VehicleK vk, IncrK L, long B
     for (int j = 0; j < nu; ++j) db[N * nu + j] = db[(N - 1) * nu + j];
 }
 
+// ---- F1 for the LTI (lateral) layouts: affine vector assembly ----
+// vehicle_lateral_mpc_slack_increment.py:32-121 / its loop :201-229 and
+// Control/MPC/mpc_kinematics.py:148-191 rebuild P, q, A, l, u every step although with the
+// fixed lateral model only q (from xr), the initial-state rows of l = u (from x0) and the
+// bound regime's inequality rows change.  Every entry of the concatenated (q, l, u) is an
+// affine function of the instance's parameters theta = (x0, xr), with a base vector per
+// bound regime:  v_i = base[regime][i] + sum_t coef[i][t] theta[idx[i][t]].  One thread per
+// (instance, entry), consecutive threads on consecutive entries (coalesced stores).
+struct AffineK {
+    int L, R, T, seg0, seg1;  // entries, regimes, terms per entry, segment starts (q | l | u)
+    const double *base, *coef;
+    const int* idx;
+};
+
+__global__ __launch_bounds__(256) void k_affine(AffineK a, long B, const double* __restrict__ theta, int tstride,
+                                                const int* __restrict__ regime, double* __restrict__ o0,
+                                                double* __restrict__ o1, double* __restrict__ o2) {
+    const long g = (long)blockIdx.x * 256 + threadIdx.x;
+    if (g >= B * a.L) return;
+    const long b = g / a.L;
+    const int i = (int)(g - b * a.L);
+    int r = regime ? regime[b] : 0;
+    r = r < 0 ? 0 : (r >= a.R ? a.R - 1 : r);
+    const double bv = a.base[(long)r * a.L + i];
+    // the terms first, the base added only where it is nonzero: an entry the builder forms
+    // as a product alone (q = -Q xr, l = u = -x0) is that product, bit for bit
+    double v = 0.0;
+    bool any = false;
+    for (int t = 0; t < a.T; ++t) {
+        const int k = a.idx[i * a.T + t];
+        if (k >= 0) {
+            const double term = a.coef[i * a.T + t] * theta[b * tstride + k];
+            v = any ? v + term : term;
+            any = true;
+        }
+    }
+    v = !any ? bv : (bv != 0.0 ? bv + v : v);
+    if (i < a.seg0) o0[b * a.seg0 + i] = v;
+    else if (i < a.seg1) o1[b * (a.seg1 - a.seg0) + (i - a.seg0)] = v;
+    else o2[b * (a.L - a.seg1) + (i - a.seg1)] = v;
+}
+
 }  // namespace mpcqp
 
 using namespace mpcqp;
 
 struct mpcqp_incr_layout : IncrLayout {};
+
+struct mpcqp_affine {
+    int dev = 0, L = 0, R = 0, T = 0, seg0 = 0, seg1 = 0, nparam = 0;
+    double *d_base = nullptr, *d_coef = nullptr;
+    int* d_idx = nullptr;
+};
 
 namespace {
 
@@ -612,6 +660,66 @@ int mpcqp_incr_warm_shift_device(int64_t B, int32_t N, int32_t nxa, int32_t nu, 
     }
     MHIPCHK(hipGetLastError());
     return 0;
+}
+
+int mpcqp_affine_create(int32_t nseg, const int32_t* seglen, int32_t nregimes, int32_t T, const double* base,
+                        const int32_t* idx, const double* coef, int32_t device, mpcqp_affine** out) {
+    if (!out || !seglen || !base || (T > 0 && (!idx || !coef)) || nseg < 1 || nseg > 3 || nregimes < 1 || T < 0)
+        return set_error(MPCQP_EINVAL, "affine_create: bad arguments");
+    *out = nullptr;
+    auto a = std::make_unique<mpcqp_affine>();
+    int L = 0, st[3] = {0, 0, 0};
+    for (int s = 0; s < nseg; ++s) {
+        if (seglen[s] < 0) return set_error(MPCQP_EINVAL, "affine_create: negative segment length");
+        L += seglen[s];
+        st[s] = L;
+    }
+    if (L == 0) return set_error(MPCQP_EINVAL, "affine_create: empty map");
+    a->dev = device; a->L = L; a->R = nregimes; a->T = T;
+    a->seg0 = st[0]; a->seg1 = nseg > 1 ? st[1] : L;
+    if (nseg == 1) a->seg0 = a->seg1 = L;
+    std::vector<double> vb(base, base + (size_t)nregimes * L), vc;
+    std::vector<int> vi;
+    if (T > 0) {
+        vc.assign(coef, coef + (size_t)L * T);
+        vi.assign(idx, idx + (size_t)L * T);
+    } else {
+        vc.assign(1, 0.0);
+        vi.assign(1, -1);
+    }
+    for (int k : vi) a->nparam = std::max(a->nparam, k + 1);
+    MHIPCHK(hipSetDevice(device));
+    if (int e = upload(vb, &a->d_base)) return e;
+    if (int e = upload(vc, &a->d_coef)) return e;
+    if (int e = upload(vi, &a->d_idx)) return e;
+    *out = a.release();
+    return 0;
+}
+
+int mpcqp_affine_apply_device(const mpcqp_affine* a, int64_t B, const double* dtheta, int32_t theta_stride,
+                              const int32_t* dregime, double* dout0, double* dout1, double* dout2, void* stream) {
+    if (!a || B < 0 || (a->nparam > 0 && (!dtheta || theta_stride < a->nparam)) || !dout0 ||
+        (a->seg1 > a->seg0 && !dout1) || (a->L > a->seg1 && !dout2))
+        return set_error(MPCQP_EINVAL, "affine_apply: bad arguments (theta_stride must cover the %d parameters)",
+                         a ? a->nparam : 0);
+    if (B == 0) return 0;
+    MHIPCHK(hipSetDevice(a->dev));
+    AffineK k;
+    k.L = a->L; k.R = a->R; k.T = a->T; k.seg0 = a->seg0; k.seg1 = a->seg1;
+    k.base = a->d_base; k.coef = a->d_coef; k.idx = a->d_idx;
+    if (a->T == 0) k.T = 0;
+    hipLaunchKernelGGL(k_affine, dim3(grid_of((long)B * a->L, 256)), dim3(256), 0, (hipStream_t)stream, k, (long)B,
+                       dtheta, (int)theta_stride, dregime, dout0, dout1, dout2);
+    MHIPCHK(hipGetLastError());
+    return 0;
+}
+
+void mpcqp_affine_free(mpcqp_affine* a) {
+    if (!a) return;
+    (void)hipSetDevice(a->dev);
+    for (void* p : {(void*)a->d_base, (void*)a->d_coef, (void*)a->d_idx})
+        if (p) (void)hipFree(p);
+    delete a;
 }
 
 void mpcqp_incr_layout_free(mpcqp_incr_layout* L) {

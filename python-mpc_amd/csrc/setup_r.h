@@ -59,6 +59,7 @@ __device__ __forceinline__ void setup_r_body(const KParams& p, const long b, con
 #pragma unroll
     for (int k = 0; k < KP; ++k)
         pg[k] = pbase + 8u * (colv ? ((unsigned)p.gpsym[(long)k * npad + pc] & 0xFFFFu) : (unsigned)nnzP);
+    const long bm = p.mat_shared ? 0 : b;  // LTI batches: one P, A for every instance
     int ar[AS], ac[AS], pr[PS], pcol[PS];
 #pragma unroll
     for (int s = 0; s < AS; ++s) {
@@ -67,7 +68,7 @@ __device__ __forceinline__ void setup_r_body(const KParams& p, const long b, con
         const int v = in ? p.acsc_v[e] : 0;
         ar[s] = in ? p.acsc_row[e] : 0;
         ac[s] = in ? p.a_c[v] : 0;
-        if (in) Ac[e] = Ax_in[b * nnzA + v];
+        if (in) Ac[e] = Ax_in[bm * nnzA + v];
     }
 #pragma unroll
     for (int s = 0; s < PS; ++s) {
@@ -75,7 +76,7 @@ __device__ __forceinline__ void setup_r_body(const KParams& p, const long b, con
         const bool in = v < nnzP;
         pr[s] = in ? p.p_r[v] : 0;
         pcol[s] = in ? p.p_c[v] : 0;
-        if (in) Pv[v] = Px_in[b * nnzP + v];
+        if (in) Pv[v] = Px_in[bm * nnzP + v];
     }
     if (tid == 0) { Pv[nnzP] = 0.0; Ac[nnzA] = 0.0; }
     double qv = colv ? q_in[b * n + p.pad_var[pc]] : 0.0, Dv = 1.0, Ev[RS];

@@ -25,10 +25,14 @@ import scipy.sparse as sparse
 
 __all__ = ["OSQP", "OSQPBatch", "DeviceBatch", "constant", "STATUS", "lib", "LIB_PATH"]
 
-# MPCQP_PHASE_PROF=1 selects the diagnostic build with in-kernel phase timers
-# (make -C python-mpc_amd/csrc prof -> libmpcqp_prof.so)
+# Diagnostic builds: MPCQP_PHASE_PROF=1 (or MPCQP_BUILD=prof) selects the build with in-kernel
+# phase timers (make -C python-mpc_amd/csrc prof -> libmpcqp_prof.so), MPCQP_BUILD=skew the
+# barrier-race build whose barriers skew the waves (libmpcqp_skew.so, tests/test_skew.py)
+_BUILD = os.environ.get("MPCQP_BUILD") or ("prof" if os.environ.get("MPCQP_PHASE_PROF") == "1" else "")
+if _BUILD not in ("", "prof", "skew"):
+    raise ImportError(f"MPCQP_BUILD={_BUILD!r}: expected prof or skew")
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                        "libmpcqp_prof.so" if os.environ.get("MPCQP_PHASE_PROF") == "1" else "libmpcqp.so")
+                        f"libmpcqp_{_BUILD}.so" if _BUILD else "libmpcqp.so")
 OSQP_INFTY = 1e30
 
 STATUS = {
@@ -129,6 +133,9 @@ def lib():
     L.mpcqp_warm_start_device.argtypes = [vp, vp, vp, vp]
     L.mpcqp_solve_device.argtypes = [vp, vp, vp, vp, vp, vp]
     L.mpcqp_synchronize.argtypes = [vp]
+    L.mpcqp_set_shared_matrices.argtypes = [vp, C.c_int32]
+    L.mpcqp_get_stream.argtypes = [vp]
+    L.mpcqp_get_stream.restype = vp
     L.mpcqp_last_kernel_ms.argtypes = [vp]
     L.mpcqp_last_kernel_ms.restype = C.c_double
     L.mpcqp_get_plan_info.argtypes = [vp, _P(_PlanInfo)]
@@ -433,7 +440,17 @@ class DeviceBatch:
     def _ptr(t):
         return None if t is None else C.c_void_p(t.data_ptr())
 
+    def _shared(self, Px, Ax):
+        """1-D Px / Ax: one P and A for every instance (LTI batches; mpcqp_set_shared_matrices)."""
+        shared = Px.dim() == 1
+        if shared != (Ax.dim() == 1):
+            raise ValueError("Px and Ax must both be per-instance (2-D) or both shared (1-D)")
+        if shared and (Px.shape[0] != self.nnzP or Ax.shape[0] != self.nnzA):
+            raise ValueError("shared Px / Ax must have nnz(P) / nnz(A) entries")
+        _check(lib().mpcqp_set_shared_matrices(self._h.ptr, int(shared)), "set_shared_matrices")
+
     def setup(self, Px, Ax, q, l, u, stream=None):
+        self._shared(Px, Ax)
         _check(lib().mpcqp_setup_device(self._h.ptr, self._ptr(Px), self._ptr(Ax), self._ptr(q), self._ptr(l),
                                         self._ptr(u), stream), "setup_device")
 
@@ -450,13 +467,20 @@ class DeviceBatch:
 
     def setup_solve(self, Px, Ax, q, l, u, x=None, y=None, status=None, iters=None, stream=None):
         """setup(Px, Ax, q, l, u) then solve(x, y, status, iters) -- one fused kernel where the
-        solve kernel allows it (mpcqp_setup_solve_device), identical results."""
+        solve kernel allows it (mpcqp_setup_solve_device), identical results.  Px / Ax 1-D:
+        one P and A shared by the batch (LTI layouts)."""
+        self._shared(Px, Ax)
         _check(lib().mpcqp_setup_solve_device(self._h.ptr, self._ptr(Px), self._ptr(Ax), self._ptr(q), self._ptr(l),
                                               self._ptr(u), self._ptr(x), self._ptr(y), self._ptr(status),
                                               self._ptr(iters), stream), "setup_solve_device")
 
     def synchronize(self):
         _check(lib().mpcqp_synchronize(self._h.ptr), "synchronize")
+
+    def stream_handle(self):
+        """The handle's own HIP stream (what stream=None means), for work the caller wants
+        ordered with the handle's calls without a synchronisation."""
+        return C.c_void_p(lib().mpcqp_get_stream(self._h.ptr))
 
     def timing(self, enable=True, setup=True):
         """HIP-event timing of the solve launches (and of the setup launches when

@@ -284,6 +284,8 @@ def make_batch(cfg: int, B: int | None = None, seed: int | None = None, N: int |
         Px = np.tile(P.data, (B, 1)); Ax = np.tile(A.data, (B, 1))
         ucol = (N + 1) * nx
         settings = dict(verbose=False, warm_start=True)           # mpc_kinematics.py:195
+        theta = np.concatenate([x0, np.zeros((B, 4 * (N + 1)))], axis=1)  # (x0, Xr): mpc_device.LateralAssembler
+        regime = np.zeros(B, np.int32)
     elif layout == "slack":
         nx, nu = 5, 1
         x0 = np.concatenate([_lateral_x0(rng, B), rng.uniform(-5, 5, (B, 1)) * DEG], axis=1)
@@ -296,6 +298,8 @@ def make_batch(cfg: int, B: int | None = None, seed: int | None = None, N: int |
         Px = np.tile(P.data, (B, 1)); Ax = np.tile(A.data, (B, 1))
         ucol = (N + 1) * nx
         settings = dict(warm_start=True)                           # slack script :121
+        theta = np.concatenate([x0, np.zeros((B, 4))], axis=1)     # (x~0, xr): mpc_device.LateralAssembler
+        regime = reg.astype(np.int32)
     elif layout == "dynamic":
         veh = VehicleParams(dt=0.05)
         nx, nu = 6, 2
@@ -345,13 +349,14 @@ def make_batch(cfg: int, B: int | None = None, seed: int | None = None, N: int |
         u = np.concatenate([leq, np.tile(uineq, (B, 1))], axis=1)
         ucol = n_x
         settings = dict(verbose=True, polish=False, warm_start=False)   # mpc_dynamics.py:393
+        theta = regime = None
     else:
         raise ValueError(layout)
     n, m = P.shape[0], A.shape[0]
     return dict(P=P, A=A, Px=np.ascontiguousarray(Px), Ax=np.ascontiguousarray(Ax), q=np.ascontiguousarray(q),
                 l=np.ascontiguousarray(l), u=np.ascontiguousarray(u), n=n, m=m, N=N, B=B, nu=nu,
                 u_slice=slice(ucol, ucol + nu), u_block=slice(ucol, ucol + N * nu), name=spec["name"],
-                settings=settings, cfg=cfg)
+                settings=settings, cfg=cfg, theta=theta, regime=regime)
 
 
 def _stage_positions(A, N, nx, nu, maskA, maskB):

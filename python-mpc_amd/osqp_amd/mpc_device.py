@@ -59,6 +59,10 @@ def _bind():
     L.mpcqp_reference_search_device.argtypes = [i64, i32, i32, i32, vp, vp, vp, d, vp, i32, vp]
     L.mpcqp_incr_shift_device.argtypes = [vp, _P(Vehicle), i64, vp, vp, vp, vp, vp, vp, vp, vp]
     L.mpcqp_incr_warm_shift_device.argtypes = [i64, i32, i32, i32, vp, vp, vp, vp, i32, vp]
+    L.mpcqp_affine_create.argtypes = [i32, vp, i32, i32, vp, vp, vp, i32, _P(vp)]
+    L.mpcqp_affine_apply_device.argtypes = [vp, i64, vp, i32, vp, vp, vp, vp, vp]
+    L.mpcqp_affine_free.argtypes = [vp]
+    L.mpcqp_affine_free.restype = None
     L._mpc_bound = True
     return L
 
@@ -163,6 +167,147 @@ class IncrementalLayout:
         Ax, q, l, u = out
         _check(lib().mpcqp_incr_assemble_device(self._h, B, _p(Ad), _p(Bd), _p(gd), _p(xt0), _p(Xr), _p(Ax), _p(q),
                                                 _p(l), _p(u), _stream(torch, Ad.device)), "incr_assemble")
+        return out
+
+
+class AffineMap:
+    """v = base[regime] + sum_t coef[:, t] * theta[idx[:, t]] over the concatenated (q | l | u)
+    of an LTI layout -- the host description of mpcqp_affine (include/mpcqp.h), built by
+    probing an assembler that is affine in theta: base[r] = build(0, r), and the terms of
+    entry i from build(e_k, 0) for each parameter k.  `evaluate` applies it on the host
+    (the CPU tests' check of the map against the builder); `LateralAssembler` uploads it."""
+
+    def __init__(self, build, nparam, nregimes):
+        outs0 = [np.concatenate(build(np.zeros(nparam), r)) for r in range(nregimes)]
+        self.seglen = [len(v) for v in build(np.zeros(nparam), 0)]
+        self.base = np.ascontiguousarray(np.stack(outs0))
+        cols = []
+        for k in range(nparam):
+            e = np.zeros(nparam)
+            e[k] = 1.0
+            cols.append(np.concatenate(build(e, 0)) - outs0[0])
+        Cm = np.stack(cols, axis=1) if cols else np.zeros((self.base.shape[1], 0))
+        L = Cm.shape[0]
+        nz = [np.flatnonzero(Cm[i]) for i in range(L)]
+        self.T = max([len(z) for z in nz] + [0])
+        self.idx = np.full((L, max(self.T, 1)), -1, np.int32)
+        self.coef = np.zeros((L, max(self.T, 1)))
+        for i, z in enumerate(nz):
+            self.idx[i, :len(z)] = z
+            self.coef[i, :len(z)] = Cm[i, z]
+        # an entry that varies with theta has the same base in every regime (bounds change only
+        # on constant rows), so one affine form per entry covers every regime
+        var = np.array([len(z) > 0 for z in nz])
+        if var.any() and not np.all(self.base[:, var] == self.base[:1, var]):
+            raise ValueError("a theta-dependent entry changes with the regime: not an affine layout of this form")
+        self.nparam, self.nregimes = nparam, nregimes
+
+    def evaluate(self, theta, regime=None):
+        """The device kernel's arithmetic (mpc_device.hip::k_affine) in numpy, per instance."""
+        theta = np.atleast_2d(theta)
+        B = theta.shape[0]
+        reg = np.zeros(B, int) if regime is None else np.clip(np.asarray(regime), 0, self.nregimes - 1)
+        out = np.empty((B, self.base.shape[1]))
+        for b in range(B):
+            bv = self.base[reg[b]]
+            for i in range(out.shape[1]):
+                v, anyt = 0.0, False
+                for t in range(self.T):
+                    k = self.idx[i, t]
+                    if k >= 0:
+                        term = self.coef[i, t] * theta[b, k]
+                        v = v + term if anyt else term
+                        anyt = True
+                out[b, i] = bv[i] if not anyt else (bv[i] + v if bv[i] != 0.0 else v)
+        s0, s1 = self.seglen[0], self.seglen[0] + self.seglen[1]
+        return out[:, :s0], out[:, s0:s1], out[:, s1:]
+
+
+def lateral_builder(layout, N):
+    """(build(theta, regime) -> (q, l, u), nparam, nregimes, (P, A)) of a lateral layout.
+    vanilla (Control/MPC/mpc_kinematics.py:148-191 with the lateral Ad / Bd, cfg 2):
+      theta = (x0 (4), Xr stage-major ((N+1) x 4)), one regime;
+    slack (vehicle_lateral_mpc_slack_increment.py:48-115 and :201-229, cfg 1 / 3 / 4):
+      theta = (x~0 (5), xr (4)), regime 0 (i <= 400 or i > 900) / 1 (400 < i <= 900, :163-167)."""
+    from . import mpc
+    if layout == "vanilla":
+        def build(theta, regime):
+            x0, Xr = theta[:4], theta[4:].reshape(N + 1, 4).T
+            P, q, A, l, u = mpc.vanilla_qp(mpc.LATERAL_AD, mpc.LATERAL_BD, np.zeros(4), x0, Xr, mpc.VANILLA_Q,
+                                           mpc.VANILLA_Q, mpc.VANILLA_R, N, mpc.VANILLA_XMIN, -mpc.VANILLA_XMIN,
+                                           -mpc.VANILLA_UMAX, mpc.VANILLA_UMAX)
+            return q, l, u
+        nparam, nreg = 4 + 4 * (N + 1), 1
+        P, _, A, _, _ = mpc.vanilla_qp(mpc.LATERAL_AD, mpc.LATERAL_BD, np.zeros(4), np.zeros(4), np.zeros((4, N + 1)),
+                                       mpc.VANILLA_Q, mpc.VANILLA_Q, mpc.VANILLA_R, N, mpc.VANILLA_XMIN,
+                                       -mpc.VANILLA_XMIN, -mpc.VANILLA_UMAX, mpc.VANILLA_UMAX)
+    elif layout == "slack":
+        def build(theta, regime):
+            _, q, _, l, u = mpc.slack_qp(N, theta[:5], xr=theta[5:9], regime=regime)
+            return q, l, u
+        nparam, nreg = 9, 2
+        P, _, A, _, _ = mpc.slack_qp(N, np.zeros(5))
+    else:
+        raise ValueError(layout)
+    return build, nparam, nreg, (P, A)
+
+
+class LateralAssembler:
+    """F1 for the lateral layouts on the device: q, l, u of B instances from their parameters
+    theta = (x0, xr) and bound regimes (mpcqp_affine_apply_device); P and A are the layout's
+    own, the same for every instance (DeviceBatch.setup_solve with 1-D Px / Ax: the shared-
+    matrix mode).  Replaces the reference's per-step rebuild of the whole QP in Python
+    (vehicle_lateral_mpc_slack_increment.py:132-229, ~6.5 ms per step)."""
+
+    def __init__(self, layout, N=20, device=0):
+        L = _bind()
+        build, nparam, nreg, (P, A) = lateral_builder(layout, N)
+        self.map = AffineMap(build, nparam, nreg)
+        self.P, self.A = P, A
+        self.n, self.m = P.shape[0], A.shape[0]
+        self.nparam, self.nregimes = nparam, nreg
+        m = self.map
+        seg = np.ascontiguousarray(np.array(m.seglen, np.int32))
+        self._keep = (seg, m.base, np.ascontiguousarray(m.idx), np.ascontiguousarray(m.coef))
+        h = C.c_void_p()
+        _check(L.mpcqp_affine_create(len(m.seglen), _np_ptr(seg), m.nregimes, m.T, _np_ptr(m.base),
+                                     _np_ptr(self._keep[2]), _np_ptr(self._keep[3]), int(device), C.byref(h)),
+               "affine_create")
+        self._h = h.value
+        self._free = L.mpcqp_affine_free
+        self.device = int(device)
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            self._free(h)
+
+    def matrices(self):
+        """(Px, Ax): the layout's P (upper triangle) and A values in CSC order (host numpy)."""
+        import scipy.sparse as sp
+        P = sp.triu(sp.csc_matrix(self.P), format="csc")
+        P.sort_indices()
+        A = sp.csc_matrix(self.A)
+        A.sort_indices()
+        return P.data.copy(), A.data.copy()
+
+    def assemble(self, theta, regime=None, out=None, stream=None):
+        """theta (B, nparam) float64 and regime (B,) int32 device tensors -> (q, l, u) device
+        tensors (into `out` when given)."""
+        import torch
+        L = _bind()
+        B = theta.shape[0]
+        if theta.dim() != 2 or theta.shape[1] < self.nparam or theta.stride(1) != 1:
+            raise ValueError(f"theta must be (B, >= {self.nparam}) with a contiguous last axis")
+        if regime is not None and (regime.dtype != torch.int32 or regime.shape[0] != B):
+            raise ValueError("regime must be an int32 (B,) tensor")
+        if out is None:
+            kw = dict(dtype=torch.float64, device=theta.device)
+            out = (torch.empty((B, self.n), **kw), torch.empty((B, self.m), **kw), torch.empty((B, self.m), **kw))
+        st = stream if stream is not None else _stream(torch, theta.device)
+        _check(L.mpcqp_affine_apply_device(self._h, B, _p(theta), theta.stride(0),
+                                           None if regime is None else _p(regime), *(_p(t) for t in out), st),
+               "affine_apply")
         return out
 
 

@@ -126,3 +126,47 @@ def test_make_batch_dynamic_consistent():
     assert np.array_equal(dense(A), dense(A2))
     assert np.allclose(b["q"][0], q2, rtol=1e-15, atol=0)
     assert np.array_equal(b["l"][0], l2) and np.array_equal(b["u"][0], u2)
+
+
+@pytest.mark.parametrize("layout,cfg", [("vanilla", 2), ("slack", 3)])
+def test_lateral_affine_map_reproduces_the_builders(layout, cfg):
+    """F1 for the lateral layouts (osqp_amd.mpc_device.AffineMap, evaluated here with the
+    device kernel's arithmetic): q, l, u of seeded batches -- random x0, xr and bound
+    regimes -- equal the host builders' (mpc.py, themselves equal to the reference's
+    assembly: test_*_golden above) bit for bit, and make_batch's vectors from its theta."""
+    from osqp_amd.mpc_device import AffineMap, lateral_builder
+    N = 20
+    build, nparam, nreg, (P, A) = lateral_builder(layout, N)
+    amap = AffineMap(build, nparam, nreg)
+    assert amap.T <= 1  # diagonal weights: every entry one product (q = -Q xr, l = u = -x0) or a constant
+    rng = np.random.default_rng(9)
+    theta = rng.normal(size=(6, nparam)) * 3
+    reg = rng.integers(0, nreg, 6)
+    q, l, u = amap.evaluate(theta, reg)
+    for b in range(6):
+        qr, lr, ur = build(theta[b], int(reg[b]))
+        assert np.array_equal(q[b], qr) and np.array_equal(l[b], lr) and np.array_equal(u[b], ur)
+    bt = mpc.make_batch(cfg, B=16, seed=4)
+    q, l, u = amap.evaluate(bt["theta"], bt["regime"])
+    assert np.array_equal(q, bt["q"]) and np.array_equal(l, bt["l"]) and np.array_equal(u, bt["u"])
+
+
+def test_lateral_affine_map_on_reference_fixtures(golden):
+    """The same map against the vectors the reference's own code built: the slack script's
+    update(q, l, u) of loop steps 0, 401 and 901 (x~0 from their l = u rows, regime by the
+    script's schedule :158-172) and mpc_kinematics.mpc's four captured QPs."""
+    from osqp_amd.mpc_device import AffineMap, lateral_builder
+    g = golden("slack_n20.npz")
+    amap = AffineMap(*lateral_builder("slack", 20)[:3])
+    for k, step in enumerate(g["steps"]):
+        theta = np.concatenate([-g["upd_l"][k][:5], np.zeros(4)])
+        reg = 0 if step <= 400 or step > 900 else 1
+        q, l, u = amap.evaluate(theta[None], [reg])
+        assert np.array_equal(q[0], g["upd_q"][k]) and np.array_equal(l[0], g["upd_l"][k])
+        assert np.array_equal(u[0], g["upd_u"][k])
+    g = golden("vanilla_n20.npz")
+    amap = AffineMap(*lateral_builder("vanilla", 20)[:3])
+    for t in range(g["x0"].shape[0]):
+        theta = np.concatenate([g["x0"][t], np.zeros(4 * 21)])
+        q, l, u = amap.evaluate(theta[None])
+        assert np.array_equal(q[0], g["q"][t]) and np.array_equal(l[0], g["l"][t]) and np.array_equal(u[0], g["u"][t])

@@ -141,41 +141,71 @@ def test_dual_infeasible_status():
     assert rg.info.status == ro.info.status and rg.info.iter == ro.info.iter
 
 
-def _slack_closed_loop(osqp_mod, steps=60, N=20):
-    """BASELINE.json configs[0] plumbing: the slack script's receding-horizon loop
-    (vehicle_lateral_mpc_slack_increment.py:121-269 at N=20): setup once with
-    warm_start, then per step update(l=, u=) with the new initial state (and the
-    e_y bound regime switch of :158-172) + solve, apply du_0 = x[(N+1)*nx] to the
-    augmented lateral model."""
-    x = np.array([0.0, 0.0, 5 * mpc.DEG, 3.0, 0.0])
-    P, q, A, l, u = mpc.slack_qp(N, x)
+def _slack_script_loop(osqp_mod, nsim=1500, N=20, states=None):
+    """BASELINE.json configs[0]: vehicle_lateral_mpc_slack_increment.py as written, at N = 20
+    (the script ships N = 100, :14; test_slack_script_default_horizon covers that size).
+    setup once with warm_start (:118-121), then every step exactly the script's calls:
+    update(q=, l=, u=) with the rebuilt vectors (:201-229, :237) under the bound schedule
+    i <= 400 / <= 900 / else (:158-172), solve (:248), raise unless 'solved' (:252-253),
+    du_0 = x[(N+1) nx] (:256), the plant x0 = A~ x0 + B~ du_0 (:257), the slack of e_y
+    (:259), then update(l=, u=) with the new initial state (:267-269).  Returns per step
+    (du_0, iterations, slack) and the plant states.  `states`: drive the loop along these
+    plant states instead of its own (the solver still warm-starts from its own solutions)."""
+    x0 = np.array([0.0, 0.0, 5 * mpc.DEG, 3.0, 0.0])                         # :27
+    P, q, A, l, u = mpc.slack_qp(N, x0)
     prob = osqp_mod.OSQP()
-    prob.setup(P, q, A, l, u, warm_start=True, verbose=False)
+    prob.setup(P, q, A, l, u, warm_start=True)                               # :121
     At, Bt = mpc.augment(mpc.LATERAL_AD, mpc.LATERAL_BD)
     nx = At.shape[0]
-    out = []
-    for i in range(steps):
-        res = prob.solve()
-        assert res.info.status == "solved"
-        du = res.x[(N + 1) * nx]
-        out.append((du, res.info.iter))
-        x = At @ x + Bt[:, 0] * du
-        _, _, _, l, u = mpc.slack_qp(N, x, regime=1 if 20 <= i < 40 else 0)
-        prob.update(l=l, u=u)
-    return np.array(out)
+    out, xs = [], [x0]
+    for i in range(nsim):
+        regime = 0 if i <= 400 else (1 if i <= 900 else 0)                   # :158-172
+        _, q_new, _, l_new, u_new = mpc.slack_qp(N, x0, regime=regime)       # :201-229 (xr = 0, :126-129)
+        prob.update(q=q_new, l=l_new, u=u_new)                               # :237
+        res = prob.solve()                                                   # :248
+        if res.info.status != "solved":                                      # :252-253
+            raise ValueError("OSQP did not solve the problem!")
+        del_ctrl = res.x[(N + 1) * nx:(N + 1) * nx + 1]                      # :256
+        x0 = At @ x0 + Bt @ del_ctrl                                         # :257
+        if states is not None:
+            x0 = states[i + 1]
+        xs.append(x0)
+        slack = res.x[-(N + 1) * nx:][3]                                     # :259
+        out.append((del_ctrl[0], res.info.iter, slack))
+        l_new[:nx] = -x0                                                     # :267-269
+        u_new[:nx] = -x0
+        prob.update(l=l_new, u=u_new)
+    return np.array(out), np.array(xs)
 
 
-def test_shim_closed_loop_matches_oracle():
+def test_slack_script_configs0_1500_steps():
+    """configs[0] through the `import osqp` drop-in (python-mpc_amd/shim/osqp.py): the
+    script's 1500-step closed loop, every call as the script makes it, against the oracle.
+    At N = 20 the loop is poorly damped (e_y swings to +-200 m and the slack carries it),
+    so rounding-level differences in du_0 grow through the plant: run free, the device's
+    and the oracle's trajectories part after ~1000 steps.  The device loop is therefore
+    driven along the oracle's plant states (warm-starting from its own solutions).  Bar:
+    every step's iteration count equal; du_0 within the north-star 1e-4 while the state
+    stays moderate (the first 800 steps, |x0| < 135); at every step within a tenth of
+    OSQP's own termination tolerance eps_abs + eps_rel |x0| at that step's scale.  Past
+    |x0| ~ 100 the warm-started solve chain itself amplifies rounding: the oracle against
+    itself with the states perturbed by 1e-14 (relative) moves du_0 by 3e-4
+    (tools/diag_configs0.py; profiles/r3_diag_configs0.txt)."""
     import importlib.util
     import os
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     spec = importlib.util.spec_from_file_location("osqp", os.path.join(root, "python-mpc_amd", "shim", "osqp.py"))
     shim = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(shim)
-    g = _slack_closed_loop(shim)
-    o = _slack_closed_loop(pyoracle)
-    assert np.all(g[:, 1] == o[:, 1])
-    assert np.abs(g[:, 0] - o[:, 0]).max() < U_TOL
+    o, xo = _slack_script_loop(pyoracle)
+    g, _ = _slack_script_loop(shim, states=xo)
+    assert g.shape == (1500, 3)
+    assert np.array_equal(g[:, 1], o[:, 1]), np.flatnonzero(g[:, 1] != o[:, 1])[:10]
+    d = np.abs(g[:, 0] - o[:, 0])
+    tol = 1e-3 + 1e-3 * np.abs(xo[:-1]).max(axis=1)  # eps_abs + eps_rel |x0|_inf per step
+    assert d[:800].max() < U_TOL, d[:800].max()
+    assert np.all(d <= 0.1 * tol), np.max(d / tol)
+    assert np.all(np.abs(g[:, 2] - o[:, 2]) <= 0.1 * tol)
 
 
 def _stage_shift(v, N, nxa, nu, groups):

@@ -319,3 +319,55 @@ def _stage_shift(v, N, nxa, nu, groups):
     d = v[:, groups * (N + 1) * nxa:].reshape(B, N, nu)
     out.append(np.concatenate([d[:, 1:], d[:, -1:]], 1).reshape(B, -1))
     return np.concatenate(out, 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout,cfg,B", [("vanilla", 2, 1000), ("slack", 3, 777)])
+def test_lateral_assembly_on_device(layout, cfg, B):
+    """F1 for the lateral layouts (mpcqp_affine_apply_device): q, l, u of a seeded batch from
+    its parameters (x0, xr) and bound regimes equal the host builders' bit for bit; the
+    solve of the device-assembled batch with ONE shared P and A (mpcqp_set_shared_matrices)
+    equals the solve of the host-built per-instance arrays bit for bit."""
+    import torch
+    from osqp_amd import DeviceBatch, _drop_common_zeros
+    from osqp_amd.mpc_device import LateralAssembler
+    b = mpc.make_batch(cfg, B=B, seed=21)
+    rng = np.random.default_rng(5)
+    theta = b["theta"].copy()
+    theta[:, b["theta"].shape[1] - 4:] = rng.normal(size=(B, 4)) * 0.1   # a nonzero reference too
+    dev = torch.device("cuda", 0)
+    asm = LateralAssembler(layout, N=20, device=0)
+    dth = torch.from_numpy(np.ascontiguousarray(theta)).to(dev)
+    dreg = torch.from_numpy(b["regime"]).to(dev)
+    q, l, u = asm.assemble(dth, dreg)
+    torch.cuda.synchronize()
+    qh, lh, uh = asm.map.evaluate(theta, b["regime"])
+    for d, h in ((q, qh), (l, lh), (u, uh)):
+        assert torch.equal(d.cpu(), torch.from_numpy(np.ascontiguousarray(h)))
+    # the builder itself, instance by instance (a few)
+    build = __import__("osqp_amd.mpc_device", fromlist=["lateral_builder"]).lateral_builder(layout, 20)[0]
+    for k in (0, B // 2, B - 1):
+        qr, lr, ur = build(theta[k], int(b["regime"][k]))
+        assert np.array_equal(q[k].cpu().numpy(), qr) and np.array_equal(l[k].cpu().numpy(), lr)
+    # solve: shared matrices + device vectors vs per-instance host arrays
+    P, Px = _drop_common_zeros(b["P"], b["Px"])
+    A, Ax = _drop_common_zeros(b["A"], b["Ax"])
+    assert np.array_equal(Px[0], asm.matrices()[0]) and np.array_equal(Ax[0], asm.matrices()[1])
+    s = {k: v for k, v in b["settings"].items() if k != "verbose"}
+
+    def out():
+        return (torch.empty((B, b["n"]), dtype=torch.float64, device=dev),
+                torch.empty((B, b["m"]), dtype=torch.float64, device=dev),
+                torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev))
+
+    h1, h2 = DeviceBatch(P, A, B, device=0, **s), DeviceBatch(P, A, B, device=0, **s)
+    Pxs, Axs = (torch.from_numpy(np.ascontiguousarray(v)).to(dev) for v in asm.matrices())
+    o1, o2 = out(), out()
+    h1.setup_solve(Pxs, Axs, q, l, u, *o1)
+    qb, lb, ub = (torch.from_numpy(np.ascontiguousarray(v)).to(dev) for v in (qh, lh, uh))
+    Pb, Ab = (torch.from_numpy(np.ascontiguousarray(v)).to(dev) for v in (Px, Ax))
+    h2.setup_solve(Pb, Ab, qb, lb, ub, *o2)
+    torch.cuda.synchronize()
+    for a, c in zip(o1, o2):
+        assert torch.equal(a, c)
+    assert (o1[2] == 1).all()
