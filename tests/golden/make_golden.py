@@ -22,6 +22,21 @@ Fixtures:
                      Vehicle_Kinematics.get_kinematics_model
   linearise.npz      Vehicle_Dynamics.get_dynamics_model at 48 seeded (x, u), incl. the
                      low-speed guard branch (vehicle_models.py:143-159)
+  refsearch.npz      Control/MPC/mpc_dynamics.py:30-90 reference_search (with nearest_point) on
+                     main()'s path (:468-469) for 64 seeded predicted horizons
+  dyn_main_n30.npz   Control/MPC/mpc_dynamics.py:main (:437-617) run for 3 steps (its float
+                     linspace count made int, sim_time = 3), each step's inputs (x~, the
+                     predicted horizon, Xr, Ad/Bd/gd lists), its QP, the solution, and the
+                     state after the plant step and horizon shift.  The solution comes from
+                     this repository's CPU oracle (oracle/pyoracle.py) behind the osqp stub --
+                     OSQP itself is not installed -- so the fixture pins the reference's
+                     data path around the solve (F1-F3), not the solve.
+  kin_ltv_n40.npz    Control/MPC/mpc_kinematics_pred_matrix.py:268-352 mpc__ (LTV, per-stage
+                     Ad/Bd/gd from Vehicle_Kinematics.get_kinematics_model)
+  kin_corridor_n30.npz  Control/MPC/mpc_kinematics.py:202-265 mpc_ (per-stage x/y corridor bounds)
+  dyn_ltv_n30.npz    Control/MPC/mpc_dynamics.py:160-279 mpc (LTV dynamic model, not incremental)
+  incr_func_n40.npz  Control/MPC/mpc_incre_kine_func.py:83-221 mpc_increment (the
+                     functionised simulate()'s builder; polish / warm start off)
 """
 import io
 import json
@@ -51,6 +66,23 @@ class _CaptureOSQP:
     def solve(self):
         x = np.zeros(self._n)
         return types.SimpleNamespace(x=x, y=None, info=types.SimpleNamespace(status="solved", iter=0))
+
+
+class _OracleOSQP(_CaptureOSQP):
+    """Capture stub whose solve() returns this repository's CPU oracle's solution, so that
+    a reference main() loop can run several steps on meaningful solutions."""
+
+    def setup(self, P, q, A, l, u, **kw):
+        super().setup(P, q, A, l, u, **kw)
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(OUT)), "oracle"))
+        import pyoracle
+        self._o = pyoracle.OSQP()
+        self._o.setup(P, q, A, l, u, **{k: v for k, v in kw.items() if k != "verbose"})
+
+    def solve(self):
+        r = self._o.solve()
+        captured.append(dict(kind="solve", x=r.x.copy(), iter=r.info.iter, status=r.info.status))
+        return r
 
 
 def _install_stub():
@@ -251,10 +283,189 @@ def linearise():
                                 x_guarded=np.stack(Xg), u_guarded=np.stack(Ug), dt=np.array(0.05)))
 
 
+def _main_path():
+    """mpc_dynamics.main's path (:468-469) with the float sample count made an int."""
+    px = np.linspace(-10, 100, int(100 / 0.5))
+    return px, px * 0.5 + 5
+
+
+def refsearch():
+    import mpc_dynamics
+    px, py = _main_path()
+    rng = np.random.default_rng(3)
+    B, N, dt = 64, 30, 0.05
+    preds, xrs = [], []
+    for b in range(B):
+        s0 = rng.uniform(-5, 60)
+        pred = np.zeros((6, N + 1))
+        pred[0] = s0 + rng.normal(0, 1)
+        pred[1] = 0.5 * s0 + 5 + rng.normal(0, 3)
+        pred[3] = rng.uniform(0, 30, N + 1) * (-1 if b < B // 4 else 1)  # reversing: |vx| is used
+        Xr, _ = mpc_dynamics.reference_search(px, py, pred, dt, N)
+        preds.append(pred); xrs.append(Xr)
+    _save("refsearch.npz", dict(path_x=px, path_y=py, pred=np.stack(preds), Xr=np.stack(xrs), dt=np.array(dt)))
+
+
+def dyn_main(steps=3):
+    """mpc_dynamics.main run for `steps` steps, instrumented: before each solve the step's
+    inputs, after each shift the new state (the capture calls are inserted into the source
+    text executed here; nothing of it is kept)."""
+    import inspect
+    import mpc_dynamics
+    src = inspect.getsource(mpc_dynamics.main)
+    src = src.replace("100/0.5", "int(100/0.5)").replace("sim_time = 1000", f"sim_time = {steps}")
+    src = src.replace("        # Solve MPC\n",
+                      "        _cap_in(i, x_tilda_vec, pred_x_tilda, pred_del_u, Xr, Ad_list, Bd_list, gd_list)\n"
+                      "        # Solve MPC\n")
+    src = src.replace("        toc = time.time()\n", "        _cap_out(i, x_tilda, pred_x_tilda, pred_del_u)\n"
+                                                     "        toc = time.time()\n")
+    assert "_cap_in" in src and "_cap_out" in src
+    rec = {"in": [], "out": []}
+    ns = dict(vars(mpc_dynamics))
+    ns["_cap_in"] = lambda i, xt, pred, pdu, Xr, A_, B_, g_: rec["in"].append(
+        dict(xt=xt.copy(), pred=pred.copy(), pdu=pdu.copy(), Xr=Xr.copy(), Ad=np.stack(A_), Bd=np.stack(B_),
+             gd=np.stack(g_)[..., 0]))
+    ns["_cap_out"] = lambda i, xt, pred, pdu: rec["out"].append(dict(xt=xt[:, 0].copy(), pred=pred.copy(),
+                                                                   pdu=pdu.copy()))
+    exec(compile(src, "mpc_dynamics.py", "exec"), ns)
+    sys.modules["osqp"].OSQP = _OracleOSQP
+    captured.clear()
+    try:
+        with contextlib.redirect_stdout(io.StringIO()):
+            ns["main"]()
+    finally:
+        sys.modules["osqp"].OSQP = _CaptureOSQP
+    setups = [c for c in captured if c["kind"] == "setup"]
+    sols = [c for c in captured if c["kind"] == "solve"]
+    d = {}
+    _csc("P", setups[0]["P"], d)
+    d["settings"] = np.array(json.dumps(setups[0]["kw"]))
+    for k in ("xt", "pred", "pdu", "Xr", "Ad", "Bd", "gd"):
+        d["in_" + k] = np.stack([r[k] for r in rec["in"]])
+    for k in ("xt", "pred", "pdu"):
+        d["out_" + k] = np.stack([r[k] for r in rec["out"]])
+    for t, s_ in enumerate(setups):  # A's structural zeros follow the step's Ad / Bd: one CSC per step
+        _csc(f"A{t}", s_["A"], d)
+    d.update(q=np.stack([s_["q"] for s_ in setups]), l=np.stack([s_["l"] for s_ in setups]),
+             u=np.stack([s_["u"] for s_ in setups]), sol=np.stack([s_["x"] for s_ in sols]),
+             sol_iter=np.array([s_["iter"] for s_ in sols]))
+    px, py = _main_path()
+    d.update(path_x=px, path_y=py)
+    _save("dyn_main_n30.npz", d)
+
+
+def _kin_rollout(veh, x0, u0, N):
+    Ads, Bds, gds = [], [], []
+    xk = x0.copy()
+    for k in range(N):
+        A_, B_, C_ = veh.get_kinematics_model(xk.copy(), u0.copy())
+        Ads.append(A_); Bds.append(B_); gds.append(C_)
+        xk = A_ @ xk + B_ @ u0 + C_[:, 0]
+    return Ads, Bds, gds
+
+
+def _qp_fixture(name, call, **extra):
+    captured.clear()
+    with contextlib.redirect_stdout(io.StringIO()):
+        try:
+            call()
+        except Exception:
+            pass  # the stub's zero solution may break the parse after setup; only setup is needed
+    s = [c for c in captured if c["kind"] == "setup"][-1]
+    d = {}
+    _csc("P", s["P"], d)
+    _csc("A", s["A"], d)
+    d.update(q=s["q"], l=s["l"], u=s["u"], settings=np.array(json.dumps(s["kw"])), **extra)
+    _save(name, d)
+
+
+def kin_ltv():
+    import scipy.sparse as sparse
+    import mpc_kinematics_pred_matrix as mk
+    import vehicle_models
+    veh = vehicle_models.Vehicle_Kinematics(l_f=1.25, l_r=1.40, dt=0.02)
+    N = 40
+    x0 = np.array([0.0, 0.5, 20.0, np.deg2rad(3.0)])
+    u0 = np.array([np.deg2rad(1.0), 0.01])
+    Ads, Bds, gds = _kin_rollout(veh, x0, u0, N)
+    Xr = np.zeros((4, N + 1)); Xr[0] = np.arange(N + 1) * 20.0 * 0.02; Xr[2] = 20.0
+    Q = sparse.diags([10.0, 10.0, 100.0, 10.0]); QN = sparse.diags([100.0, 100.0, 1000.0, 100.0])
+    R = sparse.diags([1000, 100])
+    umin = np.array([-np.deg2rad(15), -3.]); umax = np.array([np.deg2rad(15), 1.])
+    xmin = np.array([-np.inf, -np.inf, -100., -2 * np.pi]); xmax = np.array([np.inf, np.inf, 100., 2 * np.pi])
+    _qp_fixture("kin_ltv_n40.npz", lambda: mk.mpc__(Ads, Bds, gds, x0, Xr, Q, QN, R, N, xmin, xmax, umin, umax))
+
+
+def kin_corridor():
+    import scipy.sparse as sparse
+    import mpc_kinematics
+    import vehicle_models
+    veh = vehicle_models.Vehicle_Kinematics(l_f=1.25, l_r=1.40, dt=0.02)
+    N = 30
+    x0 = np.array([0.0, 0.3, 10.0, np.deg2rad(2.0)])
+    u0 = np.array([0.0, 0.0])
+    Ad, Bd, gd = veh.get_kinematics_model(x0.copy(), u0.copy())
+    Xr = np.zeros((4, N + 1)); Xr[0] = np.arange(N + 1) * 10.0 * 0.02; Xr[2] = 10.0
+    s = np.arange(N + 1) * 10.0 * 0.02
+    lb_x, ub_x = s - 1.0, s + 1.0                # a corridor around the reference
+    lb_y, ub_y = -0.5 + 0 * s, 0.5 + 0.02 * s    # narrowing to the left
+    Q = sparse.diags([10.0, 10.0, 100.0, 10.0]); R = sparse.diags([1000, 100])
+    umin = np.array([-np.deg2rad(15), -3.]); umax = np.array([np.deg2rad(15), 1.])
+    _qp_fixture("kin_corridor_n30.npz", lambda: mpc_kinematics.mpc_(Ad, Bd, gd, x0, Xr, Q, Q, R, N, lb_x, ub_x, lb_y,
+                                                                     ub_y, umin, umax))
+
+
+def dyn_ltv():
+    import scipy.sparse as sparse
+    import mpc_dynamics
+    import vehicle_models
+    veh = vehicle_models.Vehicle_Dynamics(m=1300, l_f=1.25, l_r=1.40, width=1.78, length=4.25, turning_circle=10.4,
+                                          C_d=0.34, A_f=2.0, C_roll=0.015, dt=0.05)
+    N = 30
+    x0 = np.array([[0.], [0.5], [np.deg2rad(4.0)], [12.0], [0.1], [0.02]])
+    u0 = np.array([[np.deg2rad(1.0)], [0.2]])
+    Ads, Bds, gds = [], [], []
+    xk = x0.copy()
+    for k in range(N):
+        Ad, Bd, gd = veh.get_dynamics_model(xk.copy(), u0.copy())
+        Ads.append(Ad); Bds.append(Bd); gds.append(gd)
+        xk = Ad @ xk + Bd @ u0 + gd
+    Xr = np.zeros((6, N + 1)); Xr[0] = np.arange(N + 1) * 10.0 * 0.05; Xr[3] = 10.0
+    Q = sparse.diags([100.0, 100.0, 100.0, 50.0, 50.0, 50.0])
+    QN = sparse.diags([1000.0, 1000.0, 1000.0, 500.0, 500.0, 500.0])
+    R = sparse.diags([50, 50])
+    umin = np.array([-np.deg2rad(15), -3.]); umax = np.array([np.deg2rad(15), 1.])
+    xmin = np.array([-np.inf, -np.inf, -2 * np.pi, -100., -30., -0.5 * np.pi])
+    xmax = np.array([np.inf, np.inf, 2 * np.pi, 100., 30., 0.5 * np.pi])
+    pred_x = np.zeros((6, N + 1)); pred_u = np.zeros((2, N + 1))
+    _qp_fixture("dyn_ltv_n30.npz", lambda: mpc_dynamics.mpc(Ads, Bds, gds, x0[:, 0], Xr, pred_x, pred_u, Q, QN, R, N,
+                                                            xmin, xmax, umin, umax))
+
+
+def incr_func():
+    import scipy.sparse as sparse
+    import mpc_incre_kine_func as mf
+    import vehicle_models
+    veh = vehicle_models.Vehicle_Kinematics(l_f=1.25, l_r=1.40, dt=0.02)
+    N = 40
+    x0 = np.array([0.0, 1.0, 15.0, np.deg2rad(-2.0)])
+    u0 = np.array([np.deg2rad(0.5), 0.0])
+    Ads, Bds, gds = _kin_rollout(veh, x0, u0, N)
+    Xr = np.zeros((4, N + 1)); Xr[0] = np.arange(N + 1) * 15.0 * 0.02; Xr[2] = 15.0
+    Q = sparse.diags([100.0, 100.0, 10.0, 100.0]); QN = sparse.diags([1000.0, 1000.0, 100.0, 1000.0])
+    R = sparse.diags([100, 100])
+    dumin = np.array([-np.deg2rad(0.5), -0.5]); dumax = np.array([np.deg2rad(0.5), 0.5])
+    xmin_t = np.array([-np.inf, -np.inf, -100., -2 * np.pi, -np.deg2rad(15), -3.])
+    xmax_t = np.array([np.inf, np.inf, 100., 2 * np.pi, np.deg2rad(15), 1.])
+    _qp_fixture("incr_func_n40.npz", lambda: mf.mpc_increment(Ads, Bds, gds, np.concatenate([x0, u0]), Xr,
+                                                              np.zeros((6, N + 1)), np.zeros((2, N + 1)), Q, QN, R, N,
+                                                              xmin_t, xmax_t, dumin, dumax))
+
+
 if __name__ == "__main__":
     _install_stub()
-    slack()
-    vanilla()
-    dyn_incr()
-    kin_incr()
-    linearise()
+    which = set(sys.argv[1:])
+    for f in (slack, vanilla, dyn_incr, kin_incr, linearise, refsearch, dyn_main, kin_ltv, kin_corridor, dyn_ltv,
+              incr_func):
+        if not which or f.__name__ in which:
+            f()

@@ -78,6 +78,19 @@ def test_kinematic_incremental_golden(golden):
     _cmp_single(g["P"], g["q"], g["A"], g["l"], g["u"], _settings(g), slice(246, 326))
 
 
+@pytest.mark.parametrize("name,nu", [("kin_ltv_n40.npz", 2), ("kin_corridor_n30.npz", 2), ("dyn_ltv_n30.npz", 2),
+                                     ("incr_func_n40.npz", 2)])
+def test_reference_builder_qps(golden, name, nu):
+    """QPs of the reference's other builders, captured from its own code (make_golden.py):
+    mpc_kinematics_pred_matrix.mpc__ (LTV), mpc_kinematics.mpc_ (per-stage corridor bounds),
+    mpc_dynamics.mpc (LTV dynamic model), mpc_incre_kine_func.mpc_increment -- each with the
+    settings its call site passes.  The controls are the last N nu variables."""
+    g = golden(name)
+    n = g["P"].shape[0]
+    N = int(name.split("_n")[1].split(".")[0])
+    _cmp_single(g["P"], g["q"], g["A"], g["l"], g["u"], _settings(g), slice(n - N * nu, n))
+
+
 def _batch_parity(b, settings, nthreads=16, min_match=0.99):
     bo = pyoracle.solve_batch(b["P"], b["A"], b["Px"], b["q"], b["Ax"], b["l"], b["u"], nthreads=nthreads,
                               **settings)

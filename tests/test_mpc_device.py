@@ -9,8 +9,15 @@ restatements of the reference's steps and the reference's own fixtures.
                        fed the device's own state, with the solve checked against the
                        CPU oracle on the host-built QP.
 
+The reference's own outputs pin those restatements (tests/golden/make_golden.py):
+  refsearch.npz      reference_search / nearest_point (mpc_dynamics.py:30-90) on main()'s path
+  dyn_main_n30.npz   three steps of mpc_dynamics.main (:437-617): each step's inputs, QP,
+                     solution (the oracle's, behind the osqp stub) and shifted state
+The host restatements are checked against them on CPU; the device kernels on the GPU.
 The pattern test runs on CPU (layout creation is host-only); the rest needs the GPU.
 """
+import json
+
 import numpy as np
 import pytest
 
@@ -115,7 +122,119 @@ def shift(sol, Ad0, Bd0, gd0, xt, veh, N):
     return xt_new, pred, pdu
 
 
+# ------------------------------------------- the restatements against the reference --
+def test_reference_search_restatement_matches_reference(golden):
+    """The host restatement above equals the reference's reference_search (captured:
+    refsearch.npz, 64 predicted horizons on main()'s path, a quarter reversing)."""
+    g = golden("refsearch.npz")
+    N = g["pred"].shape[2] - 1
+    for b in range(g["pred"].shape[0]):
+        assert np.array_equal(reference_search(g["path_x"], g["path_y"], g["pred"][b], float(g["dt"]), N), g["Xr"][b])
+
+
+def _main_qp(g, t):
+    A = __import__("scipy.sparse", fromlist=["csc_matrix"]).csc_matrix(
+        (g[f"A{t}_data"], g[f"A{t}_indices"], g[f"A{t}_indptr"]), shape=tuple(g[f"A{t}_shape"]))
+    return g["P"], g["q"][t], A, g["l"][t], g["u"][t]
+
+
+def test_main_steps_restatements_match_reference(golden):
+    """Three steps of mpc_dynamics.main as the reference ran them (dyn_main_n30.npz): the
+    host restatements -- linearisation, mpc_increment's QP, the plant step and horizon
+    shift -- reproduce each step from the captured inputs and solution."""
+    g = golden("dyn_main_n30.npz")
+    veh = mpc.VehicleParams(dt=0.05)
+    N = 30
+    for t in range(g["in_xt"].shape[0]):
+        pred = g["in_pred"][t].T                                  # (N+1, 8)
+        Xr = reference_search(g["path_x"], g["path_y"], pred.T[:6], 0.05, N)
+        assert np.array_equal(Xr, g["in_Xr"][t])
+        Ad, Bd, gd = mpc.linearise_dynamics(veh, pred[:N, :6], pred[:N, 6:])
+        assert np.allclose(Ad, g["in_Ad"][t], rtol=1e-13, atol=1e-15)
+        assert np.allclose(Bd, g["in_Bd"][t], rtol=1e-13, atol=1e-15)
+        assert np.allclose(gd, g["in_gd"][t], rtol=1e-12, atol=1e-13)
+        P, q, A, l, u = mpc.incremental_qp(list(g["in_Ad"][t]), list(g["in_Bd"][t]), list(g["in_gd"][t]),
+                                           g["in_xt"][t], g["in_Xr"][t], mpc.DYN_Q, mpc.DYN_QN, mpc.DYN_R, N,
+                                           mpc.DYN_XMIN_T, mpc.DYN_XMAX_T, mpc.DYN_DUMIN, -mpc.DYN_DUMIN)
+        Pr, qr, Ar, lr, ur = _main_qp(g, t)
+        assert np.array_equal(dense(P), dense(Pr)) and np.array_equal(dense(A), dense(Ar))
+        assert np.array_equal(q, qr) and np.array_equal(l, lr) and np.array_equal(u, ur)
+        xt_new, pred_new, pdu_new = shift(g["sol"][t], g["in_Ad"][t][0], g["in_Bd"][t][0], g["in_gd"][t][0],
+                                          g["in_xt"][t], veh, N)
+        assert np.allclose(xt_new, g["out_xt"][t], rtol=1e-14, atol=1e-14)
+        assert np.allclose(pred_new, g["out_pred"][t].T, rtol=1e-12, atol=1e-12)
+        assert np.array_equal(pdu_new, g["out_pdu"][t].T)
+    # consecutive steps chain: a step's output is the next step's input
+    assert np.array_equal(g["out_xt"][:-1], g["in_xt"][1:]) and np.array_equal(g["out_pred"][:-1], g["in_pred"][1:])
+
+
 # ------------------------------------------------------------------------- GPU tests --
+@pytest.mark.gpu
+def test_reference_search_matches_reference_fixture(golden):
+    import torch
+    from osqp_amd.mpc_device import reference_search as dev_search
+    g = golden("refsearch.npz")
+    pred = np.zeros((g["pred"].shape[0], g["pred"].shape[2], 8))
+    pred[:, :, :6] = g["pred"].transpose(0, 2, 1)
+    Xr = dev_search(torch.tensor(g["path_x"], device="cuda"), torch.tensor(g["path_y"], device="cuda"),
+                    torch.tensor(pred, device="cuda"), float(g["dt"])).cpu().numpy()
+    assert np.array_equal(Xr, g["Xr"])
+
+
+@pytest.mark.gpu
+def test_main_steps_on_device_match_reference(golden):
+    """Each captured step of mpc_dynamics.main through the device kernels: reference search
+    (bit-exact), linearisation, mpc_increment's QP, and the plant step + shift applied to
+    the step's captured solution -- against the reference's own values; and the device
+    solve of the step's QP against that solution."""
+    import ctypes as C
+    import torch
+    import pyoracle
+    from osqp_amd import OSQP
+    from osqp_amd.mpc_device import Vehicle, _bind, _p, linearise, reference_search as dev_search
+    g = golden("dyn_main_n30.npz")
+    N, dev = 30, torch.device("cuda", 0)
+    T = g["in_xt"].shape[0]
+    L = _layout(N)
+    veh = Vehicle(dt=0.05)
+    t_ = lambda a: torch.tensor(np.ascontiguousarray(a), dtype=torch.float64, device=dev)
+    pred = t_(g["in_pred"].transpose(0, 2, 1))                   # (T, N+1, 8)
+    Xr = dev_search(t_(g["path_x"]), t_(g["path_y"]), pred, 0.05)
+    assert np.array_equal(Xr.cpu().numpy(), g["in_Xr"])
+    Ad, Bd, gd = linearise(veh, pred[:, :N, :6], pred[:, :N, 6:])
+    assert np.allclose(Ad.cpu().numpy(), g["in_Ad"], rtol=1e-13, atol=1e-15)
+    assert np.allclose(gd.cpu().numpy(), g["in_gd"], rtol=1e-12, atol=1e-13)
+    Ax, q, l, u = L.assemble(t_(g["in_Ad"]), t_(g["in_Bd"]), t_(g["in_gd"]), t_(g["in_xt"]), t_(g["in_Xr"]))
+    Apat = L.pattern()[1]
+    for t in range(T):
+        Pr, qr, Ar, lr, ur = _main_qp(g, t)
+        A_dev = Apat.copy(); A_dev.data = Ax[t].cpu().numpy()
+        assert np.allclose(dense(A_dev), dense(Ar), rtol=1e-15, atol=0)
+        assert np.allclose(q[t].cpu().numpy(), qr, rtol=1e-15, atol=0)
+        assert np.array_equal(l[t].cpu().numpy(), np.clip(lr, -INF, INF))
+    # plant step + shift of the captured solutions
+    xt = t_(g["in_xt"]); pr = pred.clone(); pdu = t_(g["in_pdu"].transpose(0, 2, 1))
+    Lb = _bind()
+    _check = __import__("osqp_amd", fromlist=["_check"])._check
+    _check(Lb.mpcqp_incr_shift_device(L._h, C.byref(veh), T, _p(t_(g["sol"])), _p(t_(g["in_Ad"])),
+                                      _p(t_(g["in_Bd"])), _p(t_(g["in_gd"])), _p(xt), _p(pr), _p(pdu), None),
+           "incr_shift")
+    torch.cuda.synchronize()
+    assert np.allclose(xt.cpu().numpy(), g["out_xt"], rtol=1e-14, atol=1e-14)
+    assert np.allclose(pr.cpu().numpy(), g["out_pred"].transpose(0, 2, 1), rtol=1e-12, atol=1e-12)
+    assert np.array_equal(pdu.cpu().numpy(), g["out_pdu"].transpose(0, 2, 1))
+    # the solve of each captured QP: device and oracle agree, and the oracle reproduces the
+    # solution the reference's loop ran on
+    s = json.loads(str(g["settings"]))
+    s.pop("verbose", None)
+    for t in range(T):
+        P, q_, A, l_, u_ = _main_qp(g, t)
+        o = pyoracle.OSQP(); o.setup(P, q_, A, l_, u_, **s); ro = o.solve()
+        assert np.array_equal(ro.x, g["sol"][t]) and ro.info.iter == g["sol_iter"][t]
+        d = OSQP(); d.setup(P, q_, A, l_, u_, **s); rd = d.solve()
+        assert rd.info.status == ro.info.status and rd.info.iter == ro.info.iter
+        assert np.abs(rd.x[(N + 1) * 8:] - ro.x[(N + 1) * 8:]).max() < 1e-4
+
 @pytest.mark.gpu
 def test_linearise_matches_reference_fixture(golden):
     import torch
