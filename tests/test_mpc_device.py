@@ -216,8 +216,8 @@ def test_main_steps_on_device_match_reference(golden):
     xt = t_(g["in_xt"]); pr = pred.clone(); pdu = t_(g["in_pdu"].transpose(0, 2, 1))
     Lb = _bind()
     _check = __import__("osqp_amd", fromlist=["_check"])._check
-    _check(Lb.mpcqp_incr_shift_device(L._h, C.byref(veh), T, _p(t_(g["sol"])), _p(t_(g["in_Ad"])),
-                                      _p(t_(g["in_Bd"])), _p(t_(g["in_gd"])), _p(xt), _p(pr), _p(pdu), None),
+    keep = [t_(g[k]) for k in ("sol", "in_Ad", "in_Bd", "in_gd")]  # alive until the kernel has run
+    _check(Lb.mpcqp_incr_shift_device(L._h, C.byref(veh), T, *(_p(v) for v in keep), _p(xt), _p(pr), _p(pdu), None),
            "incr_shift")
     torch.cuda.synchronize()
     assert np.allclose(xt.cpu().numpy(), g["out_xt"], rtol=1e-14, atol=1e-14)
