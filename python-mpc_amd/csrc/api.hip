@@ -279,8 +279,7 @@ std::string choose_plan(int32_t n, int32_t m, const int32_t* Pp, const int32_t* 
     const char* vv = getenv("MPCQP_VARIANT");
     if (!st.polish && !(ev && ev[0] == '0') && !(vv && *vv && atoi(vv) != 17)) {
         std::string err = build_plan(n, m, Pp, Pi, Ap, Ai, pl, true);
-        if (err.empty() && pl.ne == 0) return err;  // nothing to eliminate: the plain plan
-        if (err.empty()) {
+        if (err.empty() && pl.ne > 0) {  // (nothing eliminated: the plain plan, level-merged blocks)
             KParams k{};
             shape_params(pl, k);
             k.mode = 2;

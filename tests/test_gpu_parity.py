@@ -689,3 +689,16 @@ def test_slack_elimination_matches_full_system(monkeypatch, B):
     # slack values (the eliminated columns) agree too
     sl = slice(125, 230)
     assert np.all(np.abs(rg.x[same][:, sl] - rf.x[same][:, sl]).max(axis=1) < 1e-4)
+
+
+@pytest.mark.parametrize("cfg,nb,ne,variant", [(2, 4, 0, 17), (3, 4, 105, 17), (5, 17, 0, 12)])
+def test_plan_and_kernel_per_config(cfg, nb, ne, variant):
+    """The plan and solve kernel each BASELINE workload runs with (guards against a plan
+    change moving a config to another kernel: cfg 5 on a greedily packed plan -- 16 blocks,
+    15 coupling rows -- ran 2x slower in the long-horizon kernel)."""
+    b = mpc.make_batch(cfg, B=4, seed=1)
+    bg = OSQPBatch()
+    bg.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"],
+             **{k: v for k, v in b["settings"].items() if k != "verbose"})
+    info = bg.plan_info()
+    assert (info["nb"], info["n_eliminated"], info["variant"]) == (nb, ne, variant)
