@@ -190,6 +190,13 @@ int mpcqp_get_plan_info(const mpcqp_handle *h, mpcqp_plan_info *info);
  * Gauss-Jordan, block epilogue, then the block-solve split of the wave kernels:
  * phase A, B, C, spare).  Only when MPCQP_PHASE_PROF=1 was set at creation. */
 int mpcqp_debug_phase_times(mpcqp_handle *h, int64_t *out);
+/* Diagnostics: the dispatch order the next solve will use (B int32 instance indices, each
+ * shard's own order offset by its first instance): after a solve, that solve's instances by
+ * descending iteration bucket (iter >> shift, 256 buckets; order within a bucket is not
+ * fixed).  Sorted in the solve kernel's last workgroup (four- and two-wave kernels) or by
+ * k_order (MPCQP_ORDER_KERNEL=1 at creation); identity before the first solve and under
+ * MPCQP_DISPATCH=identity. */
+int mpcqp_debug_dispatch_order(mpcqp_handle *h, int32_t *out);
 
 void mpcqp_free(mpcqp_handle *h);
 const char *mpcqp_last_error(void);

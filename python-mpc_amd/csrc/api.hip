@@ -767,11 +767,28 @@ int mpcqp_get_plan_info(const mpcqp_handle* h, mpcqp_plan_info* info) {
 
 int mpcqp_debug_phase_times(mpcqp_handle* h, int64_t* out) {
     if (!h || !out) return fail(MPCQP_EINVAL, "NULL argument");
-    for (auto& s : h->shards) {
+    for (auto& s : h->shards)
         if (!s.kp.prof) return fail(MPCQP_EINVAL, "phase timers not enabled (set MPCQP_PHASE_PROF=1 before create)");
+    if (int e = sync_all(h)) return e;
+    for (auto& s : h->shards) {
         HIPCHK(hipSetDevice(s.dev));
-        HIPCHK(hipStreamSynchronize(s.stream));
         HIPCHK(hipMemcpy(out + s.b0 * kProfSlots, s.kp.prof, sizeof(int64_t) * s.B * kProfSlots, hipMemcpyDeviceToHost));
+    }
+    return 0;
+}
+
+int mpcqp_debug_dispatch_order(mpcqp_handle* h, int32_t* out) {
+    if (!h || !out) return fail(MPCQP_EINVAL, "NULL argument");
+    if (int e = sync_all(h)) return e;
+    for (auto& s : h->shards) {
+        int32_t* o = out + s.b0;
+        if (!s.kp.order) {
+            for (long i = 0; i < s.B; ++i) o[i] = (int32_t)(s.b0 + i);
+            continue;
+        }
+        HIPCHK(hipSetDevice(s.dev));
+        HIPCHK(hipMemcpy(o, s.kp.order, sizeof(int32_t) * s.B, hipMemcpyDeviceToHost));
+        for (long i = 0; i < s.B; ++i) o[i] += (int32_t)s.b0;
     }
     return 0;
 }

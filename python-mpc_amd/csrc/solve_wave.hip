@@ -2108,6 +2108,16 @@ __global__ __launch_bounds__(T8, 1) void k_solve_w8(KParams p, double* __restric
     order_epilogue<T8>(p, (int*)sm);
 }
 
+// Host-side guard tying an instantiation's compile-time list lengths to the plan: gather
+// lists are kGS deep in memory (plan.cpp), so a shorter K never reads out of the list, but
+// it would drop A entries; K / KC: row / column gather lengths, KPK: P terms per column,
+// QR: nonzero G rows, K1: the slot-1 rows' length (two-wave kernel)
+static hipError_t lists_fit(const KParams& p, int K, int KC, int KPK, int QR, int K1 = 1 << 30) {
+    const bool ok = p.gkr <= K && p.gkc <= KC && p.gk <= std::max(K, KC) && p.pk <= KPK && p.amax <= QR &&
+                    p.gk1 <= K1 && K <= kGS && KC <= kGS;
+    return ok ? hipSuccess : hipErrorInvalidValue;
+}
+
 // the fused kernel's instantiation for the plan, or 0: variant 10 and the 128-thread
 // register-list setup shape (one padded column per thread, two rows, four A values)
 static int setup_solve_fits(const KParams& p) {
@@ -2128,7 +2138,9 @@ hipError_t launch_setup_solve(const KParams& p, long B, const double* Px, const 
         // EL (eliminated columns, the slack layouts): three A values per setup thread
         auto k4 = p.ne ? k_setup_solve_w4<6, 4, 8, 8, 3, true, 8>
                        : (p.amax <= 5 ? k_setup_solve_w4<6, 4, 5, 6, 2> : k_setup_solve_w4<6, 4, 8, 6, 2>);
-        hipError_t e = hipFuncSetAttribute((const void*)k4, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipError_t e = lists_fit(p, 6, p.ne ? 8 : 6, 4, p.ne || p.amax > 5 ? 8 : 5);
+        if (e != hipSuccess) return e;
+        e = hipFuncSetAttribute((const void*)k4, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k4, dim3((unsigned)B), dim3(T4), lds, st, p, Px, Ax, q, l, u, xo, yo);
         e = hipGetLastError();
@@ -2136,7 +2148,9 @@ hipError_t launch_setup_solve(const KParams& p, long B, const double* Px, const 
         return launch_polish(p, B, xo, yo, st);
     }
     auto k = p.gk1 <= 1 ? k_setup_solve_w2<6, 2, 4, 1, 6, 2, 4, 2> : k_setup_solve_w2<6, 2, 4, 6, 6, 2, 4, 2>;
-    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = lists_fit(p, 6, 6, 4, 1 << 30, 6);
+    if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(T2), lds, st, p, Px, Ax, q, l, u, xo, yo);
     e = hipGetLastError();
@@ -2148,8 +2162,10 @@ template <int K, int RS, int KPK, int K1>
 static hipError_t go_w2(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st, size_t lds,
                         KernelRef* ref) {
     auto k = k_solve_w2<K, RS, KPK, K1>;
+    hipError_t e = lists_fit(p, K, K, KPK, 1 << 30, K1);
+    if (e != hipSuccess) return e;
     if (ref) { *ref = {(const void*)k, T2, lds}; return hipSuccess; }
-    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(T2), lds, st, p, xo, yo, fo);
     return hipGetLastError();
@@ -2181,8 +2197,10 @@ hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, i
         case 17: {
             auto k = p.ne ? k_solve_w4<6, 4, 8, true, 8> : (p.amax <= 5 ? k_solve_w4<6, 4, 5> : k_solve_w4<6, 4, 8>);
             const size_t lds = lds_w2_bytes(p);
+            hipError_t e = lists_fit(p, 6, p.ne ? 8 : 6, 4, p.ne || p.amax > 5 ? 8 : 5);
+            if (e != hipSuccess) return e;
             if (ref) { *ref = {(const void*)k, T4, lds}; return hipSuccess; }
-            hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
             hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(T4), lds, st, p, xo, yo, factor_only);
             return hipGetLastError();

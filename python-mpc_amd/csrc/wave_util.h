@@ -11,6 +11,7 @@ namespace mpcqp {
 // Built at run start from the plan's (vector index << 16) | (A position) lists.
 template <int K>
 struct GatherW {
+    static_assert(K <= 16, "gather lists are kGS = 16 deep (plan.h)");
     unsigned e[K];
     __device__ __forceinline__ void load(const int* list, int stride, unsigned abase, unsigned vbase) {
         // the stride passes through an empty asm: the K entry addresses are formed here, at

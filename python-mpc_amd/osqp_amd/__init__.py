@@ -142,6 +142,7 @@ def lib():
     L.mpcqp_timing.argtypes = [vp, C.c_int32]
     L.mpcqp_timing_read.argtypes = [vp, dp, i32p, dp, i32p]
     L.mpcqp_debug_phase_times.argtypes = [vp, _P(C.c_int64)]
+    L.mpcqp_debug_dispatch_order.argtypes = [vp, _P(C.c_int32)]
     L.mpcqp_free.argtypes = [vp]
     L.mpcqp_free.restype = None
     L.mpcqp_analyze.argtypes = [C.c_int32, C.c_int32, i32p, i32p, i32p, i32p,
@@ -341,6 +342,13 @@ class OSQPBatch:
         _check(lib().mpcqp_get_plan_info(self._need(), C.byref(info)), "plan_info")
         return {f[0]: getattr(info, f[0]) for f in _PlanInfo._fields_}
 
+    def phase_times(self):
+        """Per-instance phase timers of the last solve, shape (B, 16) int64 (diagnostic;
+        needs MPCQP_PHASE_PROF=1 in the environment before setup)."""
+        out = np.zeros((self.B, 16), dtype=np.int64)
+        _check(lib().mpcqp_debug_phase_times(self._need(), out.ctypes.data_as(_P(C.c_int64))), "phase_times")
+        return out
+
 
 class OSQP:
     """Single-instance mirror of osqp.OSQP (runs as a batch of one on the GPU)."""
@@ -503,4 +511,11 @@ class DeviceBatch:
         needs MPCQP_PHASE_PROF=1 in the environment when the batch was created)."""
         out = np.zeros((self.B, 16), dtype=np.int64)
         _check(lib().mpcqp_debug_phase_times(self._h.ptr, out.ctypes.data_as(_P(C.c_int64))), "phase_times")
+        return out
+
+    def dispatch_order(self):
+        """The dispatch order the next solve uses, shape (B,) int32 (diagnostic; see
+        mpcqp.h::mpcqp_debug_dispatch_order)."""
+        out = np.zeros(self.B, dtype=np.int32)
+        _check(lib().mpcqp_debug_dispatch_order(self._h.ptr, out.ctypes.data_as(_P(C.c_int32))), "dispatch_order")
         return out

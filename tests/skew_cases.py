@@ -1,5 +1,5 @@
 """Solves of tests/test_skew.py, run once with the production library and once (in a child
-process, MPCQP_BUILD=skew) with the barrier-race build -- TEST INFRASTRUCTURE ONLY.
+process, MPCQP_BUILD=skew or prof) with a diagnostic build -- TEST INFRASTRUCTURE ONLY.
 Every kernel family with hand-offs between waves: the four-wave kernel (cfg 2, and the
 slack layout's reduced system), the two-wave and eight-wave kernels, the 256-thread
 register-sweep kernel, the 512-thread long-horizon kernel."""
@@ -35,7 +35,10 @@ def run(name, cfg, B, variant, elim):
     u[:, :2] *= 0.95
     h.update(l=l, u=u)
     r2 = h.solve()  # warm-started, in the dispatch order the first solve left
-    return {f"{name}_{k}{i}": getattr(r, k) for i, r in enumerate((r1, r2)) for k in ("x", "y", "iter", "status_val")}
+    res = {f"{name}_{k}{i}": getattr(r, k) for i, r in enumerate((r1, r2)) for k in ("x", "y", "iter", "status_val")}
+    if os.environ.get("MPCQP_PHASE_PROF") == "1":
+        res[f"{name}_phase_times"] = h.phase_times()
+    return res
 
 
 def main(out):

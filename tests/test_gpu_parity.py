@@ -412,6 +412,50 @@ def test_longest_first_dispatch_is_result_neutral(monkeypatch, cfg, B):
     assert o1[3].max().item() > o1[3].min().item()  # the counts vary, so the order is not the identity
 
 
+@pytest.mark.parametrize("cfg", [2, 3])
+def test_fused_dispatch_order_matches_order_kernel(monkeypatch, cfg):
+    """The order the solve kernel's last workgroup sorts (device_common.h::order_epilogue)
+    against the separate sort kernel (kernels.hip::k_order, MPCQP_ORDER_KERNEL=1), read back
+    through mpcqp_debug_dispatch_order after one solve of B = 1024 > resident slots: both
+    are permutations that visit the instances by non-increasing iteration bucket
+    (iter >> shift, 256 buckets) -- which fixes each bucket's set of instances, the order
+    inside a bucket being the atomics' -- and neither is the identity it starts from.  A
+    silent no-op or a differently keyed sort fails here, not only in timing."""
+    import torch
+    from osqp_amd import DeviceBatch
+    B = 1024
+    b = mpc.make_batch(cfg, B=B, seed=31)
+    s = {k: v for k, v in b["settings"].items() if k != "verbose"}
+    s.update(warm_start=False, polish=False)
+    dev = torch.device("cuda", 0)
+    X = [torch.from_numpy(np.ascontiguousarray(b[k])).to(dev) for k in ("Px", "Ax", "q", "l", "u")]
+    max_iter = s.get("max_iter", 4000)
+    shift = 0
+    while (max_iter >> shift) >= 256:
+        shift += 1
+    keys = {}
+    for mode in ("fused", "kernel"):
+        if mode == "kernel":
+            monkeypatch.setenv("MPCQP_ORDER_KERNEL", "1")
+        d = DeviceBatch(b["P"], b["A"], B, device=0, **s)
+        assert np.array_equal(d.dispatch_order(), np.arange(B))
+        o = (torch.empty((B, b["n"]), dtype=torch.float64, device=dev),
+             torch.empty((B, b["m"]), dtype=torch.float64, device=dev),
+             torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev))
+        d.setup(*X)
+        d.solve(*o)
+        d.synchronize()
+        it = o[3].cpu().numpy()
+        order = d.dispatch_order()
+        assert np.array_equal(np.sort(order), np.arange(B)), mode
+        k = it[order] >> shift
+        assert np.all(np.diff(k) <= 0), mode
+        assert not np.array_equal(order, np.arange(B)), mode
+        keys[mode] = (it, k)
+    assert np.array_equal(keys["fused"][0], keys["kernel"][0])
+    assert np.array_equal(keys["fused"][1], keys["kernel"][1])
+
+
 def test_invalid_update_reports_zero_iterations():
     """An instance whose update() makes its bounds invalid (l > u) exits before any
     ADMM iteration: status 'non convex' with NaN outputs (osqp refuses such data) and
@@ -598,27 +642,36 @@ def _random_banded_batch(B, n, m, band, seed):
 @pytest.mark.parametrize("n,m,band,seed", [(60, 40, 2, 1), (150, 90, 3, 2), (300, 200, 1, 3)])
 def test_random_banded_qps(n, m, band, seed):
     """Non-MPC sparsity (random banded P and A) through the generic kernels (variants 6
-    and 11 here).  The batches mix solved and primal-infeasible instances (random
-    equality rows contradict each other) and are far less well conditioned than the MPC
-    layouts: two exact-arithmetic-equivalent CPU solvers already part ways on them --
-    the oracle (LDL') and tests/osqp_dense_ref.py (explicit inverse) stop instance 85
-    of the first batch at 525 and 425 iterations, and iterates that drift apart at
-    rounding level end up eps-close, not 1e-4-close (first batch, instance 73: same
-    525 iterations, |x - x_ref| = 1.5e-3).  So the bar here is OSQP's own: >= 95 %
-    equal statuses and iteration counts, and every instance the device reports
-    solved meets the termination test it claims, recomputed on the host from the
-    returned (x, y) in unscaled form: dist(Ax, [l, u]) <= eps_abs + eps_rel ||Ax||
-    and ||Px + q + A'y|| <= eps_abs + eps_rel max(||Px||, ||A'y||, ||q||) (inf-norms;
-    z is within eps_prim of Ax, so the box distance can only be smaller than OSQP's
-    residual)."""
+    and 11 here).  The batches mix solved, primal-infeasible, max-iteration and inaccurate
+    instances and need up to 1,050 iterations -- long ADMM runs on far worse conditioned
+    systems than the MPC layouts, where rounding-level differences between linear solvers
+    grow.  tools/diag_random.py (profiles/r3_diag_random_banded.txt) puts three solvers side
+    by side: the statuses agree on all 288 instances; the iteration counts on all but two,
+    both in the first batch -- instance 55 (device 975, oracle 1,050, the dense numpy
+    restatement 1,050) and instance 85 (500 / 525 / 425: the two CPU solvers, equal in exact
+    arithmetic, disagree as well).  The reduced matrix P + sigma I + A' rho A the device
+    factors is 15-18x worse conditioned there than the quasi-definite KKT matrix OSQP
+    factors (about 5e2 vs 3e1; not the square), and those two instances are the batch's
+    longest solves.  Bar: statuses equal for >= 99 %, iteration counts for >= 95 %; where
+    both agree, x within 5e-3 relative (eps-level: the first batch's worst such instance is
+    1.5e-3 apart after 525 identical-count iterations) with a median below 1e-6; and every
+    instance the device reports solved meets the termination test it claims, recomputed on
+    the host from the returned (x, y) in unscaled form: dist(Ax, [l, u]) <= eps_abs +
+    eps_rel ||Ax|| and ||Px + q + A'y|| <= eps_abs + eps_rel max(||Px||, ||A'y||, ||q||)
+    (inf-norms; z is within eps_prim of Ax, so the box distance can only be smaller than
+    OSQP's residual)."""
     b = _random_banded_batch(96, n, m, band, seed)
     s = dict(warm_start=False, polish=False)
     bo = pyoracle.solve_batch(b["P"], b["A"], b["Px"], b["q"], b["Ax"], b["l"], b["u"], nthreads=16, **s)
     bg = OSQPBatch()
     bg.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
     rg = bg.solve()
-    assert np.mean(rg.status_val == bo.status_val) >= 0.95
+    assert np.mean(rg.status_val == bo.status_val) >= 0.99
     assert np.mean(rg.iter == bo.iter) >= 0.95
+    same = (rg.iter == bo.iter) & (rg.status_val == bo.status_val) & np.isfinite(bo.x).all(axis=1)
+    dx = np.abs(rg.x - bo.x).max(axis=1) / np.maximum(1.0, np.abs(bo.x).max(axis=1))
+    assert np.all(dx[same] < 5e-3), dx[same].max()
+    assert np.median(dx[same]) < 1e-6
     P, A = b["P"].copy(), b["A"].copy()
     for k in np.flatnonzero(rg.status_val == 1):
         P.data, A.data = b["Px"][k], b["Ax"][k]
