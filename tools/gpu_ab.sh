@@ -2,7 +2,7 @@
 # Same-box A/B/n of several builds (through gpurun, from the repo root): the cfg-2 bench
 # alternated over the packages under ab/<name> and this tree's (".") <reps> times each,
 # optionally after the GPU tests of this tree.
-# usage: bash tools/gpu_abn.sh <tag> <run_tests:0|1> "<name> <name> ..." <reps> [bench args...]
+# usage: bash tools/gpu_ab.sh <tag> <run_tests:0|1> "<name> <name> ..." <reps> [bench args...]
 set -o pipefail
 tag=$1; tests=$2; names=$3; reps=$4; shift 4
 cd /tmp && export TMPDIR=/tmp
