@@ -670,7 +670,9 @@ hipError_t launch_polish(const KParams& p, long B, double* xo, double* yo, hipSt
 size_t lds_solve_bytes(const KParams& p) { return lds_base_bytes(p); }
 
 size_t lds_kernel_bytes(const KParams& p) {
+#ifdef MPCQP_EXPERIMENTAL
     if (p.variant == 16) return lds_dense_bytes(p);
+#endif
     if (p.variant == 10 || p.variant == 17) return lds_w2_bytes(p);
     return p.variant >= 11 && p.variant <= 14 ? lds_solve_bytes_big(p) : lds_solve_bytes(p);
 }
@@ -693,6 +695,11 @@ static hipError_t go(const KParams& p, long B, double* xo, double* yo, int fo, h
 bool variant_fits(const KParams& p, int v) {
     const int cs = (p.npad + T - 1) / T, rs = (p.m + T - 1) / T;
     if (p.ne && v != 17) return false;  // eliminated variables: the four-wave kernel only
+#ifndef MPCQP_EXPERIMENTAL
+    // measured and not taken: one-wave 8 / 9, two-wave two-sided 14, dense
+    // inverse 16, eight-wave 18 -- only in the exp / diagnostic builds (MPCQP_BUILD=exp)
+    if (v == 8 || v == 9 || v == 14 || v == 16 || v == 18) return false;
+#endif
     switch (v) {
         case 0: case 7: return p.nb == 4 && p.amax <= 8 && p.gk <= 6 && cs <= 1 && rs <= 1;
         case 1: return p.nb == 8 && p.amax <= 8 && p.gk <= 8 && cs <= 1 && rs <= 1;
@@ -735,15 +742,17 @@ bool variant_fits(const KParams& p, int v) {
             return p.nb == 8 && p.amax <= 12 && p.gk <= 8 && p.pk <= 8 && p.m <= 512 && p.npad <= 256 &&
                    packed < 65536 && lds_solve_bytes(q2) <= 160 * 1024;
         }
+#ifdef MPCQP_EXPERIMENTAL
         case 16:  // dense inverse: one variable per lane pair of a 256-thread workgroup, packed LDS addresses
             return p.n <= kDenseR && p.npad <= 128 && p.gk <= 6 && p.pk <= 4 && p.m <= 2 * 128 &&
                    lds_dense_bytes(p) < 65536;
+#endif
         default: return false;
     }
 }
 
 int solve_variant(const KParams& p) {
-    static const int order[] = {17, 10, 8, 9, 0, 1, 2, 3, 11, 12, 13, 4, 5, 6};  // 14, 16, 18: MPCQP_VARIANT only
+    static const int order[] = {17, 10, 0, 1, 2, 3, 11, 12, 13, 4, 5, 6};  // 8, 9, 14, 16, 18: MPCQP_VARIANT only
     for (int v : order)
         if (variant_fits(p, v)) return v;
     return -1;
@@ -784,7 +793,9 @@ static hipError_t launch_solve_only(const KParams& p, long B, double* xo, double
         case 6: return go<0, 32, 16, 8, 8, 1>(p, B, xo, yo, factor_only, st, lds, ref);
         case 7: return go<4, 8, 6, 1, 1, 4, false>(p, B, xo, yo, factor_only, st, lds, ref);
         case 8: case 9: case 10: case 17: case 18: return launch_solve_wave(p, B, xo, yo, factor_only, st, ref);
+#ifdef MPCQP_EXPERIMENTAL
         case 16: return launch_solve_dense(p, B, xo, yo, factor_only, st, ref);
+#endif
         case 11: case 12: case 13: case 14: return launch_solve_big(p, B, xo, yo, factor_only, st, ref);
         default: return hipErrorInvalidValue;
     }

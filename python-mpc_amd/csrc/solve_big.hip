@@ -807,7 +807,9 @@ hipError_t launch_solve_big(const KParams& p, long B, double* xo, double* yo, in
         case 11: return go_b<512, 6, 8, 1, 2>(p, B, xo, yo, factor_only, st, ref);   // nb <= 12
         case 12: return go_b<512, 9, 8, 2, 2>(p, B, xo, yo, factor_only, st, ref);   // nb <= 18
         case 13: return go_b<512, 12, 8, 2, 3>(p, B, xo, yo, factor_only, st, ref);  // nb <= 24
+#ifdef MPCQP_EXPERIMENTAL
         case 14: return go_b<128, 4, 8, 2, 2>(p, B, xo, yo, factor_only, st, ref);   // nb <= 8, two waves
+#endif
         default: return hipErrorInvalidValue;
     }
 }

@@ -41,6 +41,7 @@ namespace mpcqp {
 
 constexpr int TW = 64;
 
+#ifdef MPCQP_EXPERIMENTAL  // the one-wave kernels (variants 8, 9): make exp / MPCQP_BUILD=exp
 // S^{-1} rows of the lane's two blocks, SB[e][c] = S_{kb_e}^{-1}[r][c] (128 VGPRs)
 struct WaveFactor {
     double SB[2][S];
@@ -401,6 +402,8 @@ __global__ __launch_bounds__(TW, 1) void k_solve_w(KParams p, double* __restrict
 #endif
 #undef PH
 }
+
+#endif  // MPCQP_EXPERIMENTAL
 
 // ---------------------------------------------------------------------------
 // Two-wave variant: one 128-thread workgroup (2 waves, on 2 SIMDs) per QP.
@@ -1614,6 +1617,7 @@ __global__ __launch_bounds__(T4, 2) void k_setup_solve_w4(KParams p, const doubl
 }
 
 
+#ifdef MPCQP_EXPERIMENTAL  // the eight-wave kernel (variant 18): make exp / MPCQP_BUILD=exp
 // ---------------------------------------------------------------------------
 // Eight-wave variant (variant 18, k_solve_w8): the four-wave kernel's iteration for nb = 8
 // plans (the slack-variable MPC, SURVEY.md configs[2]/[3]): one 512-thread workgroup per
@@ -2108,6 +2112,8 @@ __global__ __launch_bounds__(T8, 1) void k_solve_w8(KParams p, double* __restric
     order_epilogue<T8>(p, (int*)sm);
 }
 
+#endif  // MPCQP_EXPERIMENTAL
+
 // Host-side guard tying an instantiation's compile-time list lengths to the plan: gather
 // lists are kGS deep in memory (plan.cpp), so a shorter K never reads out of the list, but
 // it would drop A entries; K / KC: row / column gather lengths, KPK: P terms per column,
@@ -2171,6 +2177,7 @@ static hipError_t go_w2(const KParams& p, long B, double* xo, double* yo, int fo
     return hipGetLastError();
 }
 
+#ifdef MPCQP_EXPERIMENTAL
 template <int K, int RS>
 static hipError_t go_w(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st, size_t lds,
                        KernelRef* ref) {
@@ -2181,6 +2188,7 @@ static hipError_t go_w(const KParams& p, long B, double* xo, double* yo, int fo,
     hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(TW), lds, st, p, xo, yo, fo);
     return hipGetLastError();
 }
+#endif
 
 // the two-wave kernel's LDS: the carve plus the nb S_k^{-1} tiles
 size_t lds_w2_bytes(const KParams& p) {
@@ -2192,8 +2200,10 @@ hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, i
                              KernelRef* ref) {
     const size_t lds = lds_solve_bytes(p);
     switch (p.variant) {
+#ifdef MPCQP_EXPERIMENTAL
         case 8: return go_w<6, 3>(p, B, xo, yo, factor_only, st, lds, ref);
         case 9: return go_w<8, 4>(p, B, xo, yo, factor_only, st, lds, ref);
+#endif
         case 17: {
             auto k = p.ne ? k_solve_w4<6, 4, 8, true, 8> : (p.amax <= 5 ? k_solve_w4<6, 4, 5> : k_solve_w4<6, 4, 8>);
             const size_t lds = lds_w2_bytes(p);
@@ -2205,6 +2215,7 @@ hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, i
             hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(T4), lds, st, p, xo, yo, factor_only);
             return hipGetLastError();
         }
+#ifdef MPCQP_EXPERIMENTAL
         case 18: {
             auto k = k_solve_w8<8, 8>;
             if (ref) { *ref = {(const void*)k, T8, lds}; return hipSuccess; }
@@ -2213,6 +2224,7 @@ hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, i
             hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(T8), lds, st, p, xo, yo, factor_only);
             return hipGetLastError();
         }
+#endif
         case 10:  // slot-1 rows (>= 128) with at most one nonzero (cfg 2's box rows): K1 = 1
             return p.gk1 <= 1 ? go_w2<6, 2, 4, 1>(p, B, xo, yo, factor_only, st, lds_w2_bytes(p), ref)
                               : go_w2<6, 2, 4, 6>(p, B, xo, yo, factor_only, st, lds_w2_bytes(p), ref);

@@ -25,12 +25,13 @@ import scipy.sparse as sparse
 
 __all__ = ["OSQP", "OSQPBatch", "DeviceBatch", "constant", "STATUS", "lib", "LIB_PATH"]
 
-# Diagnostic builds: MPCQP_PHASE_PROF=1 (or MPCQP_BUILD=prof) selects the build with in-kernel
-# phase timers (make -C python-mpc_amd/csrc prof -> libmpcqp_prof.so), MPCQP_BUILD=skew the
-# barrier-race build whose barriers skew the waves (libmpcqp_skew.so, tests/test_skew.py)
+# Diagnostic builds (python-mpc_amd/csrc/Makefile): MPCQP_BUILD=exp adds the kernel variants
+# measured and not taken (libmpcqp_exp.so), MPCQP_PHASE_PROF=1 (or MPCQP_BUILD=prof) selects
+# the build with in-kernel phase timers (libmpcqp_prof.so), MPCQP_BUILD=skew the barrier-race
+# build whose barriers skew the waves (libmpcqp_skew.so, tests/test_skew.py)
 _BUILD = os.environ.get("MPCQP_BUILD") or ("prof" if os.environ.get("MPCQP_PHASE_PROF") == "1" else "")
-if _BUILD not in ("", "prof", "skew"):
-    raise ImportError(f"MPCQP_BUILD={_BUILD!r}: expected prof or skew")
+if _BUILD not in ("", "exp", "prof", "skew"):
+    raise ImportError(f"MPCQP_BUILD={_BUILD!r}: expected exp, prof or skew")
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)),
                         f"libmpcqp_{_BUILD}.so" if _BUILD else "libmpcqp.so")
 OSQP_INFTY = 1e30

@@ -9,6 +9,8 @@ instances and a 1e-6 bound on the whole primal vector (relative to its scale).
 """
 import json
 
+from types import SimpleNamespace
+
 import numpy as np
 import pytest
 
@@ -91,12 +93,13 @@ def test_reference_builder_qps(golden, name, nu):
     _cmp_single(g["P"], g["q"], g["A"], g["l"], g["u"], _settings(g), slice(n - N * nu, n))
 
 
-def _batch_parity(b, settings, nthreads=16, min_match=0.99):
+def _batch_parity(b, settings, nthreads=16, min_match=0.99, rg=None):
     bo = pyoracle.solve_batch(b["P"], b["A"], b["Px"], b["q"], b["Ax"], b["l"], b["u"], nthreads=nthreads,
                               **settings)
-    bg = OSQPBatch()
-    bg.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **settings)
-    rg = bg.solve()
+    if rg is None:
+        bg = OSQPBatch()
+        bg.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **settings)
+        rg = bg.solve()
     ok = np.isfinite(bo.x).all(axis=1)
     du = np.abs(rg.x[:, b["u_block"]] - bo.x[:, b["u_block"]]).max(axis=1)
     same_status = rg.status_val == bo.status_val
@@ -293,20 +296,45 @@ def test_polish_batch_cfg2():
     assert np.all(du[same] < 1e-6), du.max()
 
 
-@pytest.mark.parametrize("variant,cfg,B", [(11, 3, 256), (14, 3, 256), (12, 5, 64), (8, 2, 256), (16, 2, 256),
-                                             (10, 2, 1024), (17, 2, 1024), (18, 3, 256)])
+@pytest.mark.parametrize("variant,cfg,B", [(11, 3, 256), (12, 5, 64), (10, 2, 1024), (17, 2, 1024)])
 def test_alternative_kernel_variants(monkeypatch, variant, cfg, B):
     """Kernel instantiations that are not the default choice for a plan stay exact:
-    the 512-thread two-sided kernel on the slack layout (variant 11), the two-wave
-    two-sided kernel (14), the long-horizon kernel on cfg 5 (12), the one-wave
-    kernel on cfg 2 (8), the dense-inverse kernel on cfg 2 (16), the two-wave kernel (10,
-    the default before the four-wave one) and the four-wave kernel (17) on cfg 2, the
-    eight-wave kernel (18) on the slack layout, selected
-    with the MPCQP_VARIANT override."""
+    the 512-thread two-sided kernel on the slack layout (variant 11), the long-horizon
+    kernel on cfg 5 (12), the two-wave kernel (10, the default before the four-wave one)
+    and the four-wave kernel (17) on cfg 2, selected with the MPCQP_VARIANT override."""
     monkeypatch.setenv("MPCQP_VARIANT", str(variant))
     b = mpc.make_batch(cfg, B=B)
     settings = dict(warm_start=True) if cfg == 3 else dict(polish=False, warm_start=False)
     _batch_parity(b, settings)
+
+
+EXPERIMENTAL = [(14, 3, 256), (8, 2, 256), (16, 2, 256), (18, 3, 256)]
+
+
+def test_experimental_kernel_variants(tmp_path):
+    """The variants measured and not taken are built only into the exp
+    library (python-mpc_amd/csrc/Makefile, MPCQP_EXPERIMENTAL): the two-wave two-sided
+    kernel on the slack layout (14), the one-wave kernel (8) and the dense-inverse kernel
+    (16) on cfg 2, the eight-wave kernel (18) on the slack layout.  They stay exact against
+    the oracle, solved in a child process under MPCQP_BUILD=exp; and the production
+    library refuses them (MPCQP_VARIANT=v does not fit)."""
+    import build_cases
+    sets = {2: dict(polish=False, warm_start=False), 3: dict(warm_start=True)}
+    specs = [("batch", f"v{v}", cfg, B, str(v), sets[cfg]) for v, cfg, B in EXPERIMENTAL]
+    got = build_cases.in_build("exp", specs, tmp_path / "exp.npz")
+    for v, cfg, B in EXPERIMENTAL:
+        assert int(got[f"v{v}_variant"]) == v
+        rg = SimpleNamespace(x=got[f"v{v}_x"], iter=got[f"v{v}_iter"], status_val=got[f"v{v}_status_val"])
+        _batch_parity(mpc.make_batch(cfg, B=B), sets[cfg], rg=rg)
+
+
+@pytest.mark.parametrize("variant", [v for v, _, _ in EXPERIMENTAL])
+def test_production_library_refuses_experimental_variants(monkeypatch, variant):
+    cfg = next(c for v, c, _ in EXPERIMENTAL if v == variant)
+    monkeypatch.setenv("MPCQP_VARIANT", str(variant))
+    b = mpc.make_batch(cfg, B=4)
+    with pytest.raises(Exception, match="does not fit"):
+        OSQPBatch().setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"])
 
 
 @pytest.mark.parametrize("settings", [
