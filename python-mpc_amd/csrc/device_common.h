@@ -272,12 +272,18 @@ __device__ __forceinline__ void block_max_sum_tr(double (&v)[K], double (&sm)[KS
     // lane q < 4 (quad position q = b0 + 2 b1) holds value j + K2 b1 + K1 b0
     double* rs = red + 4 * NW * K2;
     if (lane < 4) {
+        // (the lane index through an empty asm: the write addresses are formed here, not
+        // kept from the kernel's start across a solve loop that has no register to spare)
+        int lq = lane;
+        asm volatile("" : "+v"(lq));
 #pragma unroll
-        for (int j = 0; j < K2; ++j) red[(lane * K2 + j) * NW + wid] = t2[j];
+        for (int j = 0; j < K2; ++j) red[(lq * K2 + j) * NW + wid] = t2[j];
     }
     if (lane == 0) {
+        int wq = wid;
+        asm volatile("" : "+v"(wq));  // (as lq above)
 #pragma unroll
-        for (int k = 0; k < KS; ++k) rs[wid * KS + k] = s[k];
+        for (int k = 0; k < KS; ++k) rs[wq * KS + k] = s[k];
     }
     __syncthreads();
     if constexpr (NW > 4) {

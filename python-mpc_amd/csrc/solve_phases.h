@@ -1368,7 +1368,6 @@ __device__ __forceinline__ void finalize_ph(const KParams* gp, long b, double* _
     const double* Dg = p.D + b * npad;
     Res R;
     R.restore(c.L.res);
-    const double obj = c.L.res[14];
     double rho_est;
     {
         const double pr = R.rpri / (cmax(R.rz, R.rax) + DIVISION_TOL);
@@ -1380,6 +1379,9 @@ __device__ __forceinline__ void finalize_ph(const KParams* gp, long b, double* _
                            status == MPCQP_NON_CVX_);
     const bool pinf = status == MPCQP_PRIMAL_INFEASIBLE_ || status == MPCQP_PRIMAL_INFEASIBLE_INACCURATE_;
     const bool dinf = status == MPCQP_DUAL_INFEASIBLE_ || status == MPCQP_DUAL_INFEASIBLE_INACCURATE_;
+    // the objective: computed (objective_nl) when there is a solution, else the value the
+    // status implies (OSQP: +inf primal infeasible, -inf dual infeasible, NaN non-convex)
+    const double obj = has_sol ? c.L.res[14] : (pinf ? OSQP_INFTY : (dinf ? -OSQP_INFTY : __builtin_nan("")));
     const bool dx_scaled = c.L.flag[2] != 0, dy_scaled = c.L.flag[3] != 0;
     double nrm[2] = {0.0, 0.0};
 #pragma unroll 1

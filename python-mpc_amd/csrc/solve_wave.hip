@@ -1066,7 +1066,14 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
 #else
 #define PH(k)
 #endif
-    const double cval = p.scal[b * 4 + 0], cinv = p.scal[b * 4 + 1];
+    // OPQ: the instantiations whose solve loop leaves no register for values used only at run
+    // starts, refactorisations and checks (the eliminated-column and QR = 8 ones); they form
+    // those values where used (see the lane identity at the top of the outer loop)
+    constexpr bool OPQ = EL || QR > 5;
+    // c and 1 / c of the cost scaling, from the instance's scal slots where used
+    auto cscal = [&](int k) __attribute__((always_inline)) {
+        return OPQ ? opaque_ptr(p.scal + b * 4)[k] : p.scal[b * 4 + k];
+    };
     double rho = p.scal[b * 4 + 2];
     const double sigma = p.sigma, alpha = p.alpha;
     const bool warm = p.warm_start != 0;
@@ -1093,11 +1100,9 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
 
     int status = MPCQP_UNSOLVED_, rho_updates = 0, iter = 0, info_iter = 0;
     bool can_check = false, need_factor = true;
-    const int pc = w * S + r;  // the lane's column (both halves; the lower half stores)
     const bool low = h == 0;
-    const int pe = (EL && !low) ? p.eown[pc] : -1;  // the upper lane's eliminated column, or -1
-    const int xc = pe >= 0 ? pe : pc;                // the column whose x, q the lane keeps
-    const bool colv = low && p.pad_var[pc] >= 0;     // a real block column (padding: rb = 0)
+    const int pe0 = (EL && !low) ? p.eown[w * S + r] : -1;  // the upper lane's eliminated column, or -1
+    const bool colv = low && p.pad_var[w * S + r] >= 0;     // a real block column (padding: rb = 0)
     double* const Fo = p.F + b * (long)p.nb * SS;    // ec, ed of the eliminated columns (factorize_w4)
     double ec = 0.0, ed = 0.0;
     const unsigned abase = lds_addr(L.Acsc), wbase = lds_addr(L.w), xbase = lds_addr(L.xt);
@@ -1105,22 +1110,35 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
     GatherW<K> rg;
     GatherW<KH> chs;  // the half's share of the block column's list (the rhs sums)
     GatherW<LE> el;   // EL: the eliminated column's list (zero entries for the other lanes)
-    const int ri = min(tid, mp - 1);  // lanes past the padded rows repeat the inert last row
     const bool rows_wave = w * 64 < mp;  // wave-uniform
     PH(5)
     for (;;) {
+        // The lane's identity through an empty asm at each pass (opaque_v): the addresses and
+        // slot offsets that a refactorisation, the run start and a check form from it are
+        // formed in the pass, instead of once per kernel and then held -- spilled to scratch
+        // -- across the solve.  Only where the solve loop leaves no register for them (the
+        // eliminated-column and QR = 8 instantiations: 42 and 17 spilled values without it,
+        // none with it, cfg 3 45.5 -> 44.0 ms); the cfg-2 kernel (QR = 5) spills nothing
+        // either way and is 1 % faster keeping them (same-box A/B 0.433 vs 0.439 ms).
+        const int tid = OPQ ? opaque_v(threadIdx.x) : (int)threadIdx.x;
+        const int lane = tid & 63, h = lane >> 5, r = lane & 31, rr = lane >> 3, ch = lane & 7;
+        const int pc = w * S + r;  // the lane's column (both halves; the lower half stores)
+        const int pe = OPQ ? opaque_v(pe0) : pe0;
+        const int xc = pe >= 0 ? pe : pc;  // the column whose x, q the lane keeps
+        const int ri = min(tid, mp - 1);   // lanes past the padded rows repeat the inert last row
         __syncthreads();
         if (need_factor) {
             need_factor = false;
             if (iter > 0) {
-                for (int i = tid; i < m; i += T4) p.y[b * m + i] = L.ys[i];
+                double* const yp = opaque_ptr(p.y + b * m);
+                for (int i = tid; i < m; i += T4) yp[i] = L.ys[i];
                 __syncthreads();  // every ys read is done before factorize_w4's E tiles overwrite it
             }
             const bool ok = factorize_nl<T4>(p.self, b, rho, Sg);
             if (!ok) {
                 if (iter == 0) {
-                    for (int j = tid; j < n; j += T4) if (xo) xo[b * n + j] = __builtin_nan("");
-                    for (int i = tid; i < m; i += T4) if (yo) yo[b * m + i] = __builtin_nan("");
+                    if (xo) for (int j = tid; j < n; j += T4) opaque_ptr(xo + b * n)[j] = __builtin_nan("");
+                    if (yo) for (int i = tid; i < m; i += T4) opaque_ptr(yo + b * m)[i] = __builtin_nan("");
                     if (tid == 0) fail_status(p, b);
                     return;
                 }
@@ -1130,7 +1148,10 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
             }
             __syncthreads();
             const bool have_y = iter > 0 || warm;
-            for (int i = tid; i < mp; i += T4) L.ys[i] = (have_y && i < m) ? p.y[b * m + i] : 0.0;
+            {
+                const double* const yp = opaque_ptr(p.y + b * m);
+                for (int i = tid; i < mp; i += T4) L.ys[i] = (have_y && i < m) ? yp[i] : 0.0;
+            }
             for (int o = tid; o < (NP + 1) * 8 * S; o += T4) {
                 const int q = o >> 8, t = (o >> 5) & 7;
                 L.gl[o] = (q < NP && t < p.amax) ? Hg[(long)q * p.amax * S + (o & 255)] : 0.0;
@@ -1376,10 +1397,11 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
             __syncthreads();
             PH(3)
         }
-        // run state back to LDS
-        if (low) { C.X[pc] = X; L.dx[pc] = DX; }
-        if (EL && pe >= 0) { C.X[pe] = X; L.dx[pe] = DX; }
-        if (rows_wave) { L.ys[ri] = y; C.Z[ri] = Z; C.dY[ri] = dy; }
+        // run state back to LDS (lds_put: the addresses are formed here, not held across the
+        // loop)
+        if (low) { lds_put(C.X, pc, X); lds_put(L.dx, pc, DX); }
+        if (EL && pe >= 0) { lds_put(C.X, pe, X); lds_put(L.dx, pe, DX); }
+        if (rows_wave) { lds_put(L.ys, ri, y); lds_put(C.Z, ri, Z); lds_put(C.dY, ri, dy); }
         __syncthreads();
         can_check = p.check_term && (iter % p.check_term == 0);
         const bool do_rho = p.adaptive_rho && p.rho_interval && (iter % p.rho_interval == 0);
@@ -1392,7 +1414,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
             // column (EL: the upper half checks its eliminated column pe) with its A and P lists
             // and D, the row's E
             const int col = EL ? (low ? pc : pe) : pc;
-            const bool cv = col >= 0 && (EL || low) && p.pad_var[col] >= 0;
+            const bool cv = col >= 0 && (EL || low) && opaque_ptr(p.pad_var)[col] >= 0;
             GatherW<KC> cg;
             GatherW<KPK> pg;
             if (col >= 0) {
@@ -1402,8 +1424,9 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 cg.clear(abase + 8u * nnzA, wbase);
                 pg.clear(lds_addr(L.Pv) + 8u * nnzP, Xbase);
             }
-            const double Dv = col >= 0 ? p.D[b * npad + col] : 1.0;
-            const double Ev = ri < m ? p.E[b * m + ri] : 1.0;
+            const int oz = opaque_zero();
+            const double Dv = col >= 0 ? opaque_ptr(p.D + b * npad)[col] : 1.0;
+            const double Ev = ri < m ? opaque_ptr(p.E + b * m)[ri] : 1.0;
             // inline update_info + check_termination (as solve_w2_body's), one row per thread
             const bool unscale = p.scaling && !p.scaled_term;
             const unsigned ysbase = lds_addr(L.ys), dYbase = lds_addr(C.dY), dxbase = lds_addr(L.dx);
@@ -1466,11 +1489,11 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                     mx[16] = fabs(unscale ? pdx * di : pdx);
                 }
             }
-            if (tid < npad && p.pad_var[tid] >= 0) sm[1] = L.qv[tid] * L.dx[tid];
+            if (tid < npad && opaque_ptr(p.pad_var)[tid] >= 0) sm[1] = L.qv[tid + oz] * L.dx[tid + oz];
             block_max_sum_tr<T4, 17, 2>(mx, sm, L.red);
             Res R;
             if (unscale) {
-                R.pri = mx[0]; R.dua = cinv * mx[1];
+                R.pri = mx[0]; R.dua = cscal(1) * mx[1];
                 R.nz = mx[2]; R.nax = mx[3]; R.nq = mx[4]; R.naty = mx[5]; R.npx = mx[6];
             } else {
                 R.pri = mx[7]; R.dua = mx[8];
@@ -1481,21 +1504,19 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
             if (tid == 0) R.save(L.res);
             if (can_check) {
                 int st = MPCQP_UNSOLVED_;
-                double obj = 0.0;
                 bool done = false;
                 if (R.pri > OSQP_INFTY || R.dua > OSQP_INFTY) {
                     st = MPCQP_NON_CVX_;
-                    obj = __builtin_nan("");
                     done = true;
                 } else {
                     const bool prim_ok = m == 0 || R.pri < p.eps_abs + p.eps_rel * cmax(R.nz, R.nax);
                     double mxd = cmax(cmax(R.nq, R.naty), R.npx);
-                    if (unscale) mxd *= cinv;
+                    if (unscale) mxd *= cscal(1);
                     const bool dual_ok = R.dua < p.eps_abs + p.eps_rel * mxd;
                     bool prim_inf = false, dual_inf = false;
                     if (!prim_ok || !dual_ok) {
                         const double norm_dy = mx[14], norm_dx = mx[15], epi = p.eps_pinf, edi = p.eps_dinf;
-                        const double cs = unscale ? cval : 1.0;
+                        const double cs = unscale ? cscal(0) : 1.0;
                         if (!prim_ok && m != 0 && norm_dy > epi && sm[0] < epi * norm_dy) {
                             __syncthreads();
                             double na[1] = {0.0};
@@ -1526,18 +1547,17 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                         done = true;
                     } else if (prim_inf) {
                         st = MPCQP_PRIMAL_INFEASIBLE_;
-                        obj = OSQP_INFTY;
                         if (tid == 0) L.flag[3] = unscale;
                         done = true;
                     } else if (dual_inf) {
                         st = MPCQP_DUAL_INFEASIBLE_;
-                        obj = -OSQP_INFTY;
                         if (tid == 0) L.flag[2] = unscale;
                         done = true;
                     }
                 }
                 __syncthreads();
-                if (done && tid == 0) { L.flag[1] = st; L.res[14] = obj; }
+                // (the objective of an infeasible / non-convex status is set by finalize_ph)
+                if (done && tid == 0) L.flag[1] = st;
                 __syncthreads();
                 status = done ? st : MPCQP_UNSOLVED_;
                 stop = done;
@@ -1560,6 +1580,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
         PH(4)
         if (stop || iter >= p.max_iter) break;
     }
+    const double cval = cscal(0), cinv = cscal(1);
     if (!can_check && status == MPCQP_UNSOLVED_) {
         update_info_nl<T4>(p.self, b, cinv);
         info_iter = iter;
