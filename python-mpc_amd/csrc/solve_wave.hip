@@ -1285,7 +1285,8 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
             PH(1)
             // A: c_w = sum_{j<w} G_wj b_j (rows < 8), wave w only
             if (w > 0) {
-                double acc = 0.0;
+                // one accumulator per pair (wave 3: three 4-deep FMA chains instead of one 12-deep)
+                double acc[NB - 1] = {0.0, 0.0, 0.0};
 #pragma unroll
                 for (int j = 0; j < NB - 1; ++j) {
                     if (j < w) {
@@ -1293,10 +1294,10 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                         ld2(L.rb + j * S + 4 * ch, bj[0], bj[1]);
                         ld2(L.rb + j * S + 4 * ch + 2, bj[2], bj[3]);
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) acc += ga[j][e] * bj[e];
+                        for (int e = 0; e < 4; ++e) acc[j] += ga[j][e] * bj[e];
                     }
                 }
-                cw[rr] = reduce8(acc);
+                cw[rr] = reduce8((acc[0] + acc[1]) + acc[2]);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
