@@ -170,8 +170,9 @@ void *mpcqp_get_stream(const mpcqp_handle *h);
 /* Blocks until every call enqueued on the handle so far has finished, on the handle's
  * own stream(s) and on the caller stream the last *_device call used. */
 int mpcqp_synchronize(mpcqp_handle *h);
-/* hipEvent-bracketed timing of the ADMM kernel launches of the last *_device
- * solve on the handle's stream: milliseconds, or -1 when unavailable. */
+/* hipEvent-bracketed time of the last solve: milliseconds, or -1 when unavailable.
+ * The host-pointer mpcqp_solve_batch always records it; the *_device entry points
+ * only while mpcqp_timing is on (no event packet between their kernels otherwise). */
 double mpcqp_last_kernel_ms(mpcqp_handle *h);
 
 /* Kernel timing for bench.py's roofline: while enabled, every *_device solve
