@@ -255,6 +255,27 @@ def pmc_traffic(workload, batch, kernel):
     return t if t.get("kernel") == kernel else {}  # measured on another kernel: not this one's traffic
 
 
+def copy_peak(dev_index, nbytes=2 << 30, reps=10):
+    """Achievable HBM bandwidth of a device-to-device copy (torch's copy kernel): a 2 GiB
+    buffer copied `reps` times, (read + write) bytes / time, GB/s.  Outside the timed region."""
+    import torch
+    dev = torch.device("cuda", dev_index)
+    src = torch.empty(nbytes // 8, dtype=torch.float64, device=dev).fill_(1.0)
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    torch.cuda.synchronize(dev)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    b.record()
+    torch.cuda.synchronize(dev)
+    gbs = 2 * nbytes * reps / (a.elapsed_time(b) * 1e-3) / 1e9
+    del src, dst
+    torch.cuda.empty_cache()
+    return gbs
+
+
 def main(argv=None, solver_cls=None, device=None):
     """argv: the command line (default sys.argv[1:]).  solver_cls / device: a stand-in for
     osqp_amd.DeviceBatch and its torch device -- only tests/test_multiproc.py passes them,
@@ -378,7 +399,8 @@ def main(argv=None, solver_cls=None, device=None):
     # launch, which separates the solve kernel's time.
     span = None
     if not args.no_kernel_timing:
-        if fused and not args.assemble and on_gpu and hasattr(solver, "stream_handle"):
+        # (a batch past kOrderFuseMax = 16384 runs the order sort as a second kernel per step)
+        if fused and not args.assemble and B <= 16384 and on_gpu and hasattr(solver, "stream_handle"):
             ext = torch.cuda.ExternalStream(solver.stream_handle().value, device=torch.device("cuda", local))
             span = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True), ext)
         else:
@@ -452,6 +474,7 @@ def main(argv=None, solver_cls=None, device=None):
     fp64_tflops = flop_iter * float(iters_last.astype(np.float64).sum()) / (solve_ms * 1e-3) / 1e12
 
     traffic = pmc_traffic(spec["name"], B, solve_kernel_name(info, fused=fused))
+    copy_gbs = copy_peak(local) if (on_gpu and rank == 0 and not args.no_cpu) else None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -525,6 +548,10 @@ def main(argv=None, solver_cls=None, device=None):
                                 "kernel_variant": info["variant"], "threads_per_qp": info["threads_per_qp"]}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic.get("bytes_per_launch"),
+                         # the achievable peak of a plain device copy on this
+                         # GPU, beside the datasheet peak (diagnostic; `frac` uses the datasheet)
+                         "peak_copy_measured": copy_gbs,
+                         "frac_of_copy_peak": (achieved / copy_gbs) if copy_gbs else None,
                          "traffic_source": traffic.get("source"),
                          "kernel": kname,
                          "kernel_ms": solve_ms, "kernel_ms_method": kt.get("method"), "setup_kernel_ms": setup_ms,
