@@ -580,6 +580,52 @@ def test_calls_on_different_streams_are_ordered():
         assert torch.equal(a, c)
 
 
+def test_own_stream_calls_are_ordered_without_events():
+    """A call on the handle's own stream records no event (no packet between a single-stream
+    caller's kernels); moving to a caller's stream records the ordering event on the own
+    stream first (api.hip::stream_enter), and moving back waits for the caller stream's.
+    Own -> caller -> own with no synchronisation in between equals a single-stream run.
+    mpcqp_last_kernel_ms is -1 for a device solve without timing, a time with it."""
+    import torch
+    from osqp_amd import DeviceBatch, lib
+    B = 1024
+    bs = [mpc.make_batch(2, B=B, seed=41 + k) for k in range(3)]
+    s = {k: v for k, v in bs[0]["settings"].items() if k != "verbose"}
+    s.update(warm_start=False)
+    dev = torch.device("cuda", 0)
+    n, m = bs[0]["n"], bs[0]["m"]
+
+    def put(b):
+        return [torch.from_numpy(np.ascontiguousarray(b[k])).to(dev) for k in ("Px", "Ax", "q", "l", "u")]
+
+    def out():
+        return (torch.empty((B, n), dtype=torch.float64, device=dev), torch.empty((B, m), dtype=torch.float64, device=dev),
+                torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev))
+
+    ins = [put(b) for b in bs]
+    torch.cuda.synchronize()
+    sc = torch.cuda.Stream()
+    h = DeviceBatch(bs[0]["P"], bs[0]["A"], B, device=0, **s)
+    o = [out() for _ in range(3)]
+    h.setup_solve(*ins[0], *o[0])                          # own stream
+    assert lib().mpcqp_last_kernel_ms(h._h.ptr) == -1.0    # no event pair without timing
+    h.setup_solve(*ins[1], *o[1], stream=sc.cuda_stream)   # caller stream: waits for the own stream
+    h.setup_solve(*ins[2], *o[2])                          # own stream again: waits for the caller's
+    h.synchronize()
+    torch.cuda.synchronize()
+    ref = DeviceBatch(bs[0]["P"], bs[0]["A"], B, device=0, **s)
+    r = [out() for _ in range(3)]
+    for k in range(3):
+        ref.setup_solve(*ins[k], *r[k])
+    ref.synchronize()
+    for a, c in zip(sum(map(list, o), []), sum(map(list, r), [])):
+        assert torch.equal(a, c)
+    ref.timing(True)
+    ref.setup_solve(*ins[0], *r[0])
+    assert lib().mpcqp_last_kernel_ms(ref._h.ptr) > 0.0
+    ref.timing(False)
+
+
 @pytest.mark.parametrize("cfg,B", [(2, 512), (3, 512)])
 def test_register_list_setup_is_bit_identical(monkeypatch, cfg, B):
     """kernels.hip::k_setup_r (register-resident gather lists, one column / row per
