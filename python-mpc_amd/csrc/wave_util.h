@@ -62,13 +62,6 @@ __device__ __forceinline__ T* opaque_ptr(T* p) {
     asm volatile("" : "+s"(p));
     return p;
 }
-// The lane index as a value formed at the call (a fresh mbcnt pair through an empty asm):
-// per-lane addresses built from it are formed at the site, not once per kernel.
-__device__ __forceinline__ int opaque_lane() {
-    int l = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    asm volatile("" : "+v"(l));
-    return l;
-}
 // A per-lane int through an empty asm (see opaque_zero).
 __device__ __forceinline__ int opaque_v(int x) {
     asm volatile("" : "+v"(x));
@@ -80,12 +73,6 @@ __device__ __forceinline__ void lds_put(const double* arr, int idx, double v) {
     unsigned a = lds_addr(arr);
     asm volatile("" : "+s"(a));
     *(__attribute__((address_space(3))) double*)(unsigned long)(a + 8u * (unsigned)idx) = v;
-}
-// An LDS store at a byte address that passes through an empty asm (a rarely run store
-// whose address would otherwise be kept in a register across the solve loop).
-__device__ __forceinline__ void lds_store_opaque(unsigned byte_addr, double v) {
-    asm volatile("" : "+s"(byte_addr));
-    *(__attribute__((address_space(3))) double*)(unsigned long)byte_addr = v;
 }
 
 }  // namespace mpcqp
