@@ -85,6 +85,8 @@ def parse(argv=None):
                     help="diagnostic: no HIP events in the timed region (roofline kernel_ms from the untimed pass)")
     ap.add_argument("--no-dispatch-ab", action="store_true",
                     help="skip the identity-dispatch diagnostic (rocprof passes: one handle's launches only)")
+    ap.add_argument("--no-pcie", action="store_true",
+                    help="skip the PCIe-inclusive diagnostic (host buffers in, host buffers out)")
     return ap.parse_args(argv)
 
 
@@ -276,6 +278,72 @@ def copy_peak(dev_index, nbytes=2 << 30, reps=10):
     return gbs
 
 
+def pcie_leg(solver, dev, local, bufs, host_in, steps, pipelined):
+    """PCIe-inclusive rate (diagnostic, never `value`): every step copies
+    the batch's Px, Ax, q, l, u from pinned host memory to HBM, runs the same
+    mpcqp_setup_solve_device call as the timed step, and copies x, y, status, iters back to
+    pinned host memory.
+      serial:    all of it in order on one torch stream, passed to the library as the
+                 caller stream;
+      pipelined: two sets of device buffers, the kernels on the handle's own stream, the
+                 copies on one torch stream in the order H2D(i), D2H(i-1): step i's inputs
+                 go up while step i-1's kernel runs, and i-1's outputs come down while step
+                 i's kernel runs (the overlap a host-side caller of the batch API can get).
+    The copies always run on a torch stream: torch's host allocator records the pinned
+    blocks' events on the copy's stream, and the handle destroys its own stream when freed.
+    bufs: [(dPx, dAx, dq, dl, du, dx, dy, dst, dit)] x (1 or 2); host_in: [(hPx, hAx, hq, hl,
+    hu)] cycled over the steps.  Returns seconds per step."""
+    import torch
+    cs = torch.cuda.Stream(dev)
+    outs = [tuple(torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in bufs[0][5:]) for _ in range(2)]
+    if pipelined:
+        ks = torch.cuda.ExternalStream(solver.stream_handle().value, device=torch.device("cuda", local))
+        ready = [torch.cuda.Event() for _ in range(2)]
+        done = [torch.cuda.Event() for _ in range(2)]
+
+    def down(i):
+        for hh, dd in zip(outs[i % 2], bufs[i % len(bufs)][5:]):
+            hh.copy_(dd, non_blocking=True)
+
+    def run(i):
+        k = i % len(bufs)
+        d = bufs[k]
+        with torch.cuda.stream(cs):
+            for dd, hh in zip(d[:5], host_in[i % len(host_in)]):
+                dd.copy_(hh, non_blocking=True)
+            if not pipelined:
+                solver.setup_solve(*d[:5], *d[5:], stream=cs.cuda_stream)
+                down(i)
+                return
+            ready[k].record(cs)
+            if i > 0:
+                cs.wait_event(done[(i - 1) % 2])
+                down(i - 1)
+        ks.wait_event(ready[k])
+        solver.setup_solve(*d[:5], *d[5:])
+        done[k].record(ks)
+
+    def drain(i):
+        if pipelined and i > 0:
+            with torch.cuda.stream(cs):
+                cs.wait_event(done[(i - 1) % 2])
+                down(i - 1)
+
+    solver.synchronize()
+    for i in range(2):  # warmup
+        run(i)
+    drain(2)
+    torch.cuda.synchronize(dev)
+    solver.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        run(i)
+    drain(steps)
+    torch.cuda.synchronize(dev)
+    solver.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
 def main(argv=None, solver_cls=None, device=None):
     """argv: the command line (default sys.argv[1:]).  solver_cls / device: a stand-in for
     osqp_amd.DeviceBatch and its torch device -- only tests/test_multiproc.py passes them,
@@ -453,6 +521,30 @@ def main(argv=None, solver_cls=None, device=None):
         value_identity = B * args.steps / (time.perf_counter() - ta)
         del ident
 
+    # Diagnostic, outside the timed region and never `value`: the rate with the batch handed
+    # over in host memory (the PCIe-inclusive line of DESIGN.md §6)
+    pcie = None
+    if (rank == 0 and on_gpu and not args.no_pcie and not args.assemble and not warm and fused
+            and B <= 65536 and hasattr(solver, "stream_handle")):
+        import torch as _t
+        pin = lambda a: _t.from_numpy(np.ascontiguousarray(a)).pin_memory()  # noqa: E731
+        hPx, hAx, hq = pin(Px), pin(Ax), pin(b["q"])
+        host_in = [(hPx, hAx, hq, seq[t][0].cpu().pin_memory(), seq[t][1].cpu().pin_memory())
+                   for t in range(1 + args.warmup, 1 + args.warmup + min(4, args.steps))]
+        set0 = (dPx, dAx, dq, dl.clone(), du.clone(), dx, dy, dst, dit)
+        set1 = tuple(t.clone() for t in set0)
+        t_ser = pcie_leg(solver, dev, local, [set0], host_in, args.steps, pipelined=False)
+        t_pip = pcie_leg(solver, dev, local, [set0, set1], host_in, args.steps, pipelined=True)
+        h2d = 8 * (Px.shape[1] + Ax.shape[1] + n + 2 * m)
+        d2h = 8 * (n + m) + 8
+        pcie = {"value_serial": B / t_ser, "ms_per_step_serial": t_ser * 1e3,
+                "value_pipelined": B / t_pip, "ms_per_step_pipelined": t_pip * 1e3,
+                "h2d_bytes_per_solve": h2d, "d2h_bytes_per_solve": d2h,
+                "method": "pinned host buffers: H2D of Px, Ax, q, l, u, the same setup_solve call, D2H of "
+                          "x, y, status, iters every step; serial on one stream / pipelined over two buffer "
+                          "sets, copies on their own stream beside the kernels (bench.py::pcie_leg); never `value`"}
+        del set1
+
     value = B_global * args.steps / dt
     nnzP, nnzA = P.nnz, A.nnz
     # SURVEY.md §8d D3 counts the nonzeros of one instance's matrices: cfg 5's stored
@@ -558,6 +650,7 @@ def main(argv=None, solver_cls=None, device=None):
                          "bytes_per_solve": bytes_per_solve, "launch_instances": B,
                          "fp64_tflops_model": fp64_tflops, "fp64_peak_tflops": FP64_PEAK_TFLOPS},
             "cpu_baseline": cpu,
+            "pcie_inclusive": pcie,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
