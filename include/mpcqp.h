@@ -14,6 +14,8 @@
  *                            Control/MPC/mpc_incre_kine_func.py:179-180
  *   mpcqp_update_batch    <- prob.update(q=q_new, l=l_new, u=u_new)
  *                            vehicle_lateral_mpc_slack_increment.py:237,269
+ *   mpcqp_update_matrices_batch <- prob.update(Px=, Px_idx=, Ax=, Ax_idx=)
+ *                            vehicle_lateral_mpc_slack_increment.py:236 (commented out there)
  *   mpcqp_warm_start_batch<- prob.warm_start(x=..., y=...)   (osqp API; used for
  *                            the receding-horizon shift)
  *   mpcqp_solve_batch     <- res = prob.solve(); res.x, res.y, res.info.status, res.info.iter
@@ -120,6 +122,18 @@ int mpcqp_setup_batch(int32_t n, int32_t m,
 
 /* q, l, u may each be NULL (not updated). */
 int mpcqp_update_batch(mpcqp_handle *h, const double *q, const double *l, const double *u);
+/* osqp_update_P / osqp_update_A / osqp_update_P_A (OSQP 0.6): new values of P's upper
+ * triangle and / or A for every instance -- Px is B x nPx, Ax is B x nAx, row-major; each
+ * row holds the values at the indices Px_idx / Ax_idx (into the value arrays given to
+ * mpcqp_setup_batch, in its CSC order; a repeated index takes its last value), or all
+ * nnzP / nnzA values when the index array is NULL (n* then ignored).  Either matrix may be
+ * NULL.  As OSQP: the data is unscaled, updated, scaled afresh and refactored at the next
+ * solve; x, z, y, rho and the row classes are kept (the iterates stay in the previous
+ * scaling).  The sparsity pattern is fixed.  Handles of mpcqp_setup_batch only, not in
+ * shared-matrix mode.  Replaces prob.update(Px=, Px_idx=, Ax=, Ax_idx=), which the reference
+ * mentions at vehicle_lateral_mpc_slack_increment.py:236 (commented out). */
+int mpcqp_update_matrices_batch(mpcqp_handle *h, const double *Px, const int32_t *Px_idx, int32_t nPx,
+                                const double *Ax, const int32_t *Ax_idx, int32_t nAx);
 /* x, y may each be NULL (keeps the current iterate of that part). */
 int mpcqp_warm_start_batch(mpcqp_handle *h, const double *x, const double *y);
 /* any output may be NULL */

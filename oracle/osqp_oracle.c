@@ -407,11 +407,12 @@ static void scale_data(orc_work *w) {
         limit_scaling(Et, m);
         for (int j = 0; j < n; ++j) Dt[j] = 1.0 / sqrt(Dt[j]);
         for (int i = 0; i < m; ++i) Et[i] = 1.0 / sqrt(Et[i]);
-        /* P <- Dt P Dt ; A <- Et A Dt ; q <- Dt q */
+        /* P <- Dt P Dt ; A <- Et A Dt ; q <- Dt q  (mat_premult_diag, then mat_postmult_diag:
+         * two roundings per entry, in that order) */
         for (int j = 0; j < n; ++j)
-            for (int p = w->Pp[j]; p < w->Pp[j + 1]; ++p) w->Px[p] *= Dt[w->Pi[p]] * Dt[j];
+            for (int p = w->Pp[j]; p < w->Pp[j + 1]; ++p) { w->Px[p] *= Dt[w->Pi[p]]; w->Px[p] *= Dt[j]; }
         for (int j = 0; j < n; ++j)
-            for (int p = w->Ap[j]; p < w->Ap[j + 1]; ++p) w->Ax[p] *= Et[w->Ai[p]] * Dt[j];
+            for (int p = w->Ap[j]; p < w->Ap[j + 1]; ++p) { w->Ax[p] *= Et[w->Ai[p]]; w->Ax[p] *= Dt[j]; }
         for (int j = 0; j < n; ++j) w->q[j] *= Dt[j];
         for (int j = 0; j < n; ++j) w->D[j] *= Dt[j];
         for (int i = 0; i < m; ++i) w->E[i] *= Et[i];
@@ -611,10 +612,56 @@ int orc_warm_start(orc_work *w, const double *x, const double *y) {
     memcpy(w->y, y, sizeof(double) * w->m);
     if (w->set.scaling) {
         for (int j = 0; j < w->n; ++j) w->x[j] *= w->Dinv[j];
-        for (int i = 0; i < w->m; ++i) w->y[i] *= w->Einv[i] * w->c;
+        for (int i = 0; i < w->m; ++i) { w->y[i] *= w->Einv[i]; w->y[i] *= w->c; }  /* vec_ew_prod, vec_mult_scalar */
     }
     mat_vec(w->n, w->Ap, w->Ai, w->Ax, w->m, w->x, w->z, 0);
     return 0;
+}
+
+/* ---- scaling.c: unscale_data (OSQP 0.6), used by the matrix updates ----
+ * P <- cinv Dinv P Dinv (mat_mult_scalar, mat_premult_diag, mat_postmult_diag),
+ * q <- Dinv (cinv q), A <- Einv A Dinv, l <- Einv l, u <- Einv u: one rounding per
+ * factor, in OSQP's order. */
+static void unscale_data(orc_work *w) {
+    int n = w->n, m = w->m;
+    for (int p = 0; p < w->Pp[n]; ++p) w->Px[p] *= w->cinv;
+    for (int j = 0; j < n; ++j)
+        for (int p = w->Pp[j]; p < w->Pp[j + 1]; ++p) { w->Px[p] *= w->Dinv[w->Pi[p]]; w->Px[p] *= w->Dinv[j]; }
+    for (int j = 0; j < n; ++j) { w->q[j] *= w->cinv; w->q[j] *= w->Dinv[j]; }
+    for (int j = 0; j < n; ++j)
+        for (int p = w->Ap[j]; p < w->Ap[j + 1]; ++p) { w->Ax[p] *= w->Einv[w->Ai[p]]; w->Ax[p] *= w->Dinv[j]; }
+    for (int i = 0; i < m; ++i) { w->l[i] *= w->Einv[i]; w->u[i] *= w->Einv[i]; }
+}
+
+/* osqp_update_P / osqp_update_A / osqp_update_P_A (OSQP 0.6 osqp.c): unscale the data,
+ * write the new values (all of them, or those at the given indices of P's upper-triangular
+ * / A's CSC value arrays, in order), scale from scratch, refactor the KKT matrix with the
+ * rho vector as it is, reset the status.  x, z, y and the rho vector are left as they are
+ * (OSQP 0.6 keeps the iterates in the previous scaling).  Px / Ax NULL: that matrix is not
+ * updated; *_idx NULL: all nnz values. */
+int orc_update_P_A(orc_work *w, const double *Px, const int *Px_idx, int nP, const double *Ax,
+                   const int *Ax_idx, int nA) {
+    int nnzP = w->Pp[w->n], nnzA = w->Ap[w->n];
+    if ((Px && Px_idx && (nP < 0 || nP > nnzP)) || (Ax && Ax_idx && (nA < 0 || nA > nnzA)))
+        return ORC_DATA_VALIDATION_ERROR;
+    if (Px_idx) for (int k = 0; k < nP; ++k) if (Px_idx[k] < 0 || Px_idx[k] >= nnzP) return ORC_DATA_VALIDATION_ERROR;
+    if (Ax_idx) for (int k = 0; k < nA; ++k) if (Ax_idx[k] < 0 || Ax_idx[k] >= nnzA) return ORC_DATA_VALIDATION_ERROR;
+    if (w->set.scaling) unscale_data(w);
+    if (Px) {
+        if (Px_idx) for (int k = 0; k < nP; ++k) w->Px[Px_idx[k]] = Px[k];
+        else memcpy(w->Px, Px, sizeof(double) * nnzP);
+    }
+    if (Ax) {
+        if (Ax_idx) for (int k = 0; k < nA; ++k) w->Ax[Ax_idx[k]] = Ax[k];
+        else memcpy(w->Ax, Ax, sizeof(double) * nnzA);
+    }
+    if (w->set.scaling) scale_data(w);
+    kkt_free(w->kkt);
+    w->kkt = NULL;
+    int e = kkt_init(&w->kkt, w->n, w->m, w->Pp, w->Pi, w->Px, w->Ap, w->Ai, w->Ax, w->set.sigma,
+                     w->rho_inv_vec);
+    reset_info(w);
+    return e;
 }
 
 /* ---- auxil.c ---- */
@@ -882,7 +929,7 @@ static void store_solution(orc_work *w) {
         memcpy(w->sol_y, w->y, sizeof(double) * m);
         if (w->set.scaling) {
             for (int j = 0; j < n; ++j) w->sol_x[j] *= w->D[j];
-            for (int i = 0; i < m; ++i) w->sol_y[i] *= w->E[i] * w->cinv;
+            for (int i = 0; i < m; ++i) { w->sol_y[i] *= w->E[i]; w->sol_y[i] *= w->cinv; }  /* unscale_solution */
         }
     } else {
         for (int j = 0; j < n; ++j) w->sol_x[j] = NAN;
@@ -1001,6 +1048,12 @@ static void polish(orc_work *w) {
 int orc_solve(orc_work *w) {
     int iter, can_check = 0;
     int compute_cost = 0; /* verbose off */
+    if (!w->kkt) {  /* a matrix update whose refactorisation failed (orc_update_P_A) */
+        w->info.status_val = ORC_NON_CVX;
+        w->info.iter = 0;
+        store_solution(w);
+        return ORC_NONCVX_ERROR;
+    }
     if (!w->set.warm_start) cold_start(w);
     for (iter = 1; iter <= w->set.max_iter; ++iter) {
         swap_vectors(&w->x, &w->x_prev);

@@ -87,6 +87,10 @@ int orc_update_lin_cost(orc_work *w, const double *q);
 int orc_update_bounds(orc_work *w, const double *l, const double *u);
 int orc_update_lower_bound(orc_work *w, const double *l);
 int orc_update_upper_bound(orc_work *w, const double *u);
+/* osqp_update_P_A: new values of P (upper triangle) and / or A, all (idx NULL) or at the
+ * given value indices; NULL skips that matrix.  Unscale, update, rescale, refactor. */
+int orc_update_P_A(orc_work *w, const double *Px, const int *Px_idx, int nP, const double *Ax,
+                   const int *Ax_idx, int nA);
 int orc_warm_start(orc_work *w, const double *x, const double *y);
 int orc_solve(orc_work *w);
 /* x (n), y (m); certificates may be NULL */

@@ -80,6 +80,8 @@ def lib():
         for name in ("orc_update_lin_cost", "orc_update_lower_bound", "orc_update_upper_bound"):
             getattr(L, name).argtypes = [C.c_void_p, P(C.c_double)]
         L.orc_update_bounds.argtypes = [C.c_void_p, P(C.c_double), P(C.c_double)]
+        L.orc_update_P_A.argtypes = [C.c_void_p, P(C.c_double), P(C.c_int), C.c_int,
+                                     P(C.c_double), P(C.c_int), C.c_int]
         L.orc_warm_start.argtypes = [C.c_void_p, P(C.c_double), P(C.c_double)]
         L.orc_solve.argtypes = [C.c_void_p]
         L.orc_get_solution.argtypes = [C.c_void_p, P(C.c_double), P(C.c_double),
@@ -159,8 +161,11 @@ class OSQP:
         if e:
             raise ValueError(f"oracle setup failed (code {e})")
 
-    def update(self, q=None, l=None, u=None):
+    def update(self, q=None, l=None, u=None, Px=None, Px_idx=None, Ax=None, Ax_idx=None):
+        """osqp.OSQP.update in osqp-python 0.6's order: q, the bounds, then the matrices
+        (update_P / update_A / update_P_A; an empty or missing index array: all values)."""
         L = lib()
+        e = 0
         if q is not None:
             q = np.ascontiguousarray(q, np.float64)
             L.orc_update_lin_cost(self._w, _dp(q))
@@ -173,10 +178,22 @@ class OSQP:
         elif u is not None:
             u = np.ascontiguousarray(u, np.float64)
             e = L.orc_update_upper_bound(self._w, _dp(u))
-        else:
-            e = 0
         if e:
             raise ValueError(f"oracle update failed (code {e})")
+        if Px is not None or Ax is not None:
+            def prep(v, idx):
+                if v is None:
+                    return None, None, 0
+                v = np.ascontiguousarray(v, np.float64)
+                if idx is None or np.size(idx) == 0:
+                    return v, None, v.size
+                return v, np.ascontiguousarray(idx, np.int32), v.size
+            Pv, Pi, nP = prep(Px, Px_idx)
+            Av, Ai, nA = prep(Ax, Ax_idx)
+            e = L.orc_update_P_A(self._w, _dp(Pv), None if Pi is None else _ip(Pi), nP,
+                                 _dp(Av), None if Ai is None else _ip(Ai), nA)
+            if e:
+                raise ValueError(f"oracle matrix update failed (code {e})")
 
     def warm_start(self, x=None, y=None):
         x = np.ascontiguousarray(x, np.float64); y = np.ascontiguousarray(y, np.float64)

@@ -488,6 +488,83 @@ int mpcqp_update_batch(mpcqp_handle* h, const double* q, const double* l, const 
     return 0;
 }
 
+int mpcqp_update_matrices_batch(mpcqp_handle* h, const double* Px, const int32_t* Px_idx, int32_t nPx,
+                                const double* Ax, const int32_t* Ax_idx, int32_t nAx) {
+    if (!h) return fail(MPCQP_EINVAL, "NULL handle");
+    if (!Px && !Ax) return fail(MPCQP_EINVAL, "no matrix values given");
+    const Plan& pl = h->plan;
+    // the columns of the value arrays that are written: all, or per index its last
+    // occurrence (OSQP's sequential loop: a repeated index takes the last value)
+    auto pick_cols = [&](const int32_t* idx, int32_t k, int nnz, const char* name, std::vector<int>& col,
+                         std::vector<int>& dst) -> int {
+        if (!idx) {
+            col.resize(nnz);
+            for (int i = 0; i < nnz; ++i) col[i] = i;
+            dst = col;
+            return 0;
+        }
+        if (k < 0 || k > nnz)
+            return fail(MPCQP_EINVAL, "new number of elements (%d) greater than elements in %s (%d)", k, name, nnz);
+        std::vector<int> last(nnz, -1);
+        for (int i = 0; i < k; ++i) {
+            if (idx[i] < 0 || idx[i] >= nnz) return fail(MPCQP_EINVAL, "%s index %d out of range", name, idx[i]);
+            last[idx[i]] = i;
+        }
+        for (int v = 0; v < nnz; ++v)
+            if (last[v] >= 0) { col.push_back(last[v]); dst.push_back(v); }
+        return 0;
+    };
+    std::vector<int> pcol, pdst, acol, adst;
+    if (Px)
+        if (int e = pick_cols(Px_idx, nPx, pl.nnzP, "P", pcol, pdst)) return e;
+    if (Ax)
+        if (int e = pick_cols(Ax_idx, nAx, pl.nnzA, "A", acol, adst)) return e;
+    const int kP = Px ? (Px_idx ? nPx : pl.nnzP) : 0, kA = Ax ? (Ax_idx ? nAx : pl.nnzA) : 0;
+    const int nP = (int)pdst.size(), nA = (int)adst.size();
+    for (auto& s : h->shards) {
+        if (!s.in_Px) return fail(MPCQP_EINVAL, "matrix updates need a handle made by mpcqp_setup_batch");
+        if (s.kp.mat_shared) return fail(MPCQP_EINVAL, "matrix updates need per-instance matrices (shared mode is on)");
+    }
+    // per shard: the selected values (Bs x nP, Bs x nA) and their indices, in one staging
+    // allocation freed after the call
+    std::vector<void*> tmp(h->shards.size(), nullptr);
+    auto release = [&]() {
+        for (size_t i = 0; i < tmp.size(); ++i)
+            if (tmp[i]) { (void)hipSetDevice(h->shards[i].dev); (void)hipFree(tmp[i]); }
+    };
+    int err = 0;
+    std::vector<std::vector<double>> host(h->shards.size());
+    for (size_t si = 0; si < h->shards.size() && !err; ++si) {
+        Shard& s = h->shards[si];
+        const long Bs = s.B;
+        std::vector<double>& hv = host[si];
+        hv.resize((size_t)Bs * (nP + nA));
+        for (long b = 0; b < Bs; ++b) {
+            for (int k = 0; k < nP; ++k) hv[b * nP + k] = Px[(s.b0 + b) * kP + pcol[k]];
+            for (int k = 0; k < nA; ++k) hv[Bs * nP + b * nA + k] = Ax[(s.b0 + b) * kA + acol[k]];
+        }
+        const size_t vbytes = sizeof(double) * hv.size(), ibytes = sizeof(int) * (size_t)(nP + nA);
+        auto step = [&]() -> int {
+            HIPCHK(hipSetDevice(s.dev));
+            HIPCHK(hipMalloc(&tmp[si], vbytes + ibytes + 16));
+            double* dv = (double*)tmp[si];
+            int* di = (int*)((char*)tmp[si] + vbytes);
+            if (int e = stream_enter(s, s.stream)) return e;
+            if (vbytes) HIPCHK(hipMemcpyAsync(dv, hv.data(), vbytes, hipMemcpyHostToDevice, s.stream));
+            if (nP) HIPCHK(hipMemcpyAsync(di, pdst.data(), sizeof(int) * nP, hipMemcpyHostToDevice, s.stream));
+            if (nA) HIPCHK(hipMemcpyAsync(di + nP, adst.data(), sizeof(int) * nA, hipMemcpyHostToDevice, s.stream));
+            HIPCHK(launch_update_mat(s.kp, Bs, s.in_Px, s.in_Ax, s.in_q, s.in_l, s.in_u, Px ? dv : nullptr, di, nP,
+                                     Ax ? dv + Bs * nP : nullptr, di + nP, nA, s.stream));
+            return stream_leave(s, s.stream);
+        };
+        err = step();
+    }
+    if (!err) err = sync_all(h);
+    release();
+    if (err) return err;
+    return check_err_flags(h);
+}
+
 int mpcqp_warm_start_batch(mpcqp_handle* h, const double* x, const double* y) {
     if (!h) return fail(MPCQP_EINVAL, "NULL handle");
     const long n = h->n, m = h->m;

@@ -79,8 +79,15 @@ size_t lds_kernel_bytes(const KParams& p);     // what the chosen variant's kern
 // error text for mpcqp_last_error() (api.hip); returns code
 int set_error(int code, const char* fmt, ...);
 
+// keep: the rescaling of a matrix update (launch_update_mat) -- x, z, y, the row classes
+// and rho are left as they are
 hipError_t launch_setup(const KParams& p, long B, const double* Px, const double* Ax, const double* q,
-                        const double* l, const double* u, hipStream_t st);
+                        const double* l, const double* u, hipStream_t st, bool keep = false);
+// osqp_update_P_A: unscale the workspace's data into the *_io setup inputs (user order),
+// write the new values (B x nP / B x nA, at the given indices or all), scale afresh
+hipError_t launch_update_mat(const KParams& p, long B, double* Px_io, double* Ax_io, double* q_io, double* l_io,
+                             double* u_io, const double* Px_new, const int* Px_idx, int nP, const double* Ax_new,
+                             const int* Ax_idx, int nA, hipStream_t st);
 hipError_t launch_update(const KParams& p, long B, const double* q, const double* l, const double* u,
                          hipStream_t st);
 hipError_t launch_warm(const KParams& p, long B, const double* x, const double* y, hipStream_t st);

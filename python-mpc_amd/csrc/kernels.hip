@@ -33,7 +33,8 @@ namespace mpcqp {
 // LDS indices instead of dependent global loads.
 __host__ __device__ inline long setup_span(const KParams& p) { return (long)(p.asm_blk_ptr - p.pad_var); }
 
-template <bool STAGE>  // false: plans whose index span does not fit in LDS read it from the plan
+// KEEP: a matrix update (k_unscale_mat): scale afresh, leave x, z, y, the row classes and rho
+template <bool STAGE, bool KEEP>  // STAGE false: plans whose index span does not fit in LDS read it from the plan
 __global__ __launch_bounds__(T) void k_setup(KParams p, const double* __restrict__ Px_in,
                                              const double* __restrict__ Ax_in,
                                              const double* __restrict__ q_in,
@@ -143,9 +144,11 @@ __global__ __launch_bounds__(T) void k_setup(KParams p, const double* __restrict
         p.l[b * m + i] = li;
         p.u[b * m + i] = ui;
         p.E[b * m + i] = Ev[i];
-        p.ct[b * m + i] = t;
-        p.z[b * m + i] = 0.0;
-        p.y[b * m + i] = 0.0;
+        if (!KEEP) {
+            p.ct[b * m + i] = t;
+            p.z[b * m + i] = 0.0;
+            p.y[b * m + i] = 0.0;
+        }
     }
     bad = block_any<T>(bad, flag);
     for (int i = tid; i < nnzP; i += T) p.Px[b * nnzP + i] = Pv[i];
@@ -154,30 +157,101 @@ __global__ __launch_bounds__(T) void k_setup(KParams p, const double* __restrict
     for (int pc = tid; pc < npad; pc += T) {
         p.q[b * npad + pc] = qv[pc];
         p.D[b * npad + pc] = Dv[pc];
-        p.x[b * npad + pc] = 0.0;
+        if (!KEEP) p.x[b * npad + pc] = 0.0;
     }
     if (tid == 0) {
         p.scal[b * 4 + 0] = c;
         p.scal[b * 4 + 1] = 1.0 / c;
-        p.scal[b * 4 + 2] = rho;
         p.status[b] = MPCQP_UNSOLVED_;
         p.err[b] = bad ? 1 : 0;
-        p.iter[b] = 0;
-        p.rho_upd[b] = 0;
+        if (!KEEP) {
+            p.scal[b * 4 + 2] = rho;
+            p.iter[b] = 0;
+            p.rho_upd[b] = 0;
+        }
     }
 }
 
 // ------------------------------------------------- setup, register lists --
 // setup_r.h::setup_r_body with 256 threads: one padded column and one row per thread
-template <int K, int KP, int AS, int PS>
+template <int K, int KP, int AS, int PS, bool KEEP>
 __global__ __launch_bounds__(T) void k_setup_r(KParams p, const double* __restrict__ Px_in,
                                                const double* __restrict__ Ax_in,
                                                const double* __restrict__ q_in,
                                                const double* __restrict__ l_in,
                                                const double* __restrict__ u_in) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    setup_r_body<T, K, KP, 1, AS, PS>(p, (long)blockIdx.x, Px_in, Ax_in, q_in, l_in, u_in, sm);
+    setup_r_body<T, K, KP, 1, AS, PS, KEEP>(p, (long)blockIdx.x, Px_in, Ax_in, q_in, l_in, u_in, sm);
 }
+
+// ------------------------------------------------------- matrix update --
+// osqp_update_P / osqp_update_A / osqp_update_P_A (OSQP 0.6; the call the reference's
+// commented-out update(Px=, Px_idx=) at vehicle_lateral_mpc_slack_increment.py:236 would
+// make): unscale_data -- P <- cinv Dinv P Dinv, q <- Dinv (cinv q), A <- Einv A Dinv,
+// l, u <- Einv (l, u), one rounding per factor in OSQP's order -- into the setup inputs
+// (user order), then the new values at their indices (none: all nnz); launch_update_mat
+// then scales them afresh with k_setup(_r)<KEEP>, which leaves x, z, y, the row classes
+// and rho as OSQP 0.6 does.  Dinv / Einv as OSQP forms them (vec_ew_recipr: 1 / D).
+__global__ __launch_bounds__(T) void k_unscale_mat(KParams p, double* __restrict__ Px_o, double* __restrict__ Ax_o,
+                                                   double* __restrict__ q_o, double* __restrict__ l_o,
+                                                   double* __restrict__ u_o, const double* __restrict__ Px_new,
+                                                   const int* __restrict__ Px_idx, int nP,
+                                                   const double* __restrict__ Ax_new,
+                                                   const int* __restrict__ Ax_idx, int nA) {
+    const int tid = threadIdx.x;
+    const long b = blockIdx.x;
+    const int n = p.n, m = p.m, npad = p.npad, nnzP = p.nnzP, nnzA = p.nnzA;
+    const double* D = p.D + b * npad;
+    const double* E = p.E + b * m;
+    const bool sc = p.scaling != 0;
+    const double cinv = p.scal[b * 4 + 1];
+    for (int v = tid; v < nnzP; v += T) {
+        double x = p.Px[b * nnzP + v];
+        if (sc) {
+            x *= cinv;
+            x *= 1.0 / D[p.p_r[v]];
+            x *= 1.0 / D[p.p_c[v]];
+        }
+        Px_o[b * nnzP + v] = x;
+    }
+    for (int e = tid; e < nnzA; e += T) {  // the workspace keeps A in padded-CSC order
+        const int v = p.acsc_v[e];
+        double x = p.Ax[b * nnzA + e];
+        if (sc) {
+            x *= 1.0 / E[p.acsc_row[e]];
+            x *= 1.0 / D[p.a_c[v]];
+        }
+        Ax_o[b * nnzA + v] = x;
+    }
+    for (int pc = tid; pc < npad; pc += T) {
+        const int j = p.pad_var[pc];
+        if (j < 0) continue;
+        double x = p.q[b * npad + pc];
+        if (sc) {
+            x *= cinv;
+            x *= 1.0 / D[pc];
+        }
+        q_o[b * n + j] = x;
+    }
+    for (int i = tid; i < m; i += T) {
+        double li = p.l[b * m + i], ui = p.u[b * m + i];
+        if (sc) {
+            const double ei = 1.0 / E[i];
+            li *= ei;
+            ui *= ei;
+        }
+        l_o[b * m + i] = li;
+        u_o[b * m + i] = ui;
+    }
+    __syncthreads();
+    // the new values (indices unique: the host keeps the last of repeated ones, as OSQP's
+    // sequential loop does)
+    if (Px_new)
+        for (int k = tid; k < nP; k += T) Px_o[b * nnzP + (Px_idx ? Px_idx[k] : k)] = Px_new[b * nP + k];
+    if (Ax_new)
+        for (int k = tid; k < nA; k += T) Ax_o[b * nnzA + (Ax_idx ? Ax_idx[k] : k)] = Ax_new[b * nA + k];
+}
+
 
 // ----------------------------------------------------------------- update --
 __global__ __launch_bounds__(T) void k_update(KParams p, const double* __restrict__ q_in,
@@ -282,21 +356,31 @@ static int setup_r_variant(const KParams& p) {
 }
 
 hipError_t launch_setup(const KParams& p, long B, const double* Px, const double* Ax, const double* q,
-                        const double* l, const double* u, hipStream_t st) {
+                        const double* l, const double* u, hipStream_t st, bool keep) {
     if (const int v = setup_r_variant(p); v && !getenv_flag("MPCQP_SETUP_STAGED")) {
         const size_t lds = lds_setup_r_bytes(p.nnzP, p.nnzA, p.npad, p.m);
-        auto k = v == 1 ? k_setup_r<6, 4, 2, 1> : k_setup_r<8, 4, 3, 1>;
+        auto k = keep ? (v == 1 ? k_setup_r<6, 4, 2, 1, true> : k_setup_r<8, 4, 3, 1, true>)
+                      : (v == 1 ? k_setup_r<6, 4, 2, 1, false> : k_setup_r<8, 4, 3, 1, false>);
         hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(T), lds, st, p, Px, Ax, q, l, u);
         return hipGetLastError();
     }
     size_t lds = lds_setup_bytes(p);
-    auto k = setup_staged(p) ? k_setup<true> : k_setup<false>;
+    auto k = setup_staged(p) ? (keep ? k_setup<true, true> : k_setup<true, false>)
+                             : (keep ? k_setup<false, true> : k_setup<false, false>);
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(T), lds, st, p, Px, Ax, q, l, u);
     return hipGetLastError();
+}
+hipError_t launch_update_mat(const KParams& p, long B, double* Px_io, double* Ax_io, double* q_io, double* l_io,
+                             double* u_io, const double* Px_new, const int* Px_idx, int nP, const double* Ax_new,
+                             const int* Ax_idx, int nA, hipStream_t st) {
+    hipLaunchKernelGGL(k_unscale_mat, dim3((unsigned)B), dim3(T), 0, st, p, Px_io, Ax_io, q_io, l_io, u_io, Px_new,
+                       Px_idx, nP, Ax_new, Ax_idx, nA);
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+    return launch_setup(p, B, Px_io, Ax_io, q_io, l_io, u_io, st, true);
 }
 hipError_t launch_update(const KParams& p, long B, const double* q, const double* l, const double* u,
                          hipStream_t st) {

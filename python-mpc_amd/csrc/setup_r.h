@@ -15,6 +15,8 @@
 // 256-thread workgroup give the same sum): bit-identical output.
 //
 // K: gather-list length (>= gather_k), KP (>= p_k), AS / PS: A / P values per thread.
+// KEEP: a matrix update (kernels.hip::k_unscale_mat, OSQP 0.6 osqp_update_P_A) -- the data
+// is scaled afresh but the iterates x, z, y, the row classes and rho are left as they are.
 // sm: LDS, sizeof(double) * (nnzP + nnzA + npad + m + 10) + 16 bytes.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -28,7 +30,7 @@ __host__ __device__ inline size_t lds_setup_r_bytes(int nnzP, int nnzA, int npad
     return sizeof(double) * ((size_t)nnzP + 1 + nnzA + 1 + npad + m + 8) + 16;
 }
 
-template <int TT, int K, int KP, int RS, int AS, int PS>
+template <int TT, int K, int KP, int RS, int AS, int PS, bool KEEP = false>
 __device__ __forceinline__ void setup_r_body(const KParams& p, const long b, const double* __restrict__ Px_in,
                                              const double* __restrict__ Ax_in, const double* __restrict__ q_in,
                                              const double* __restrict__ l_in, const double* __restrict__ u_in,
@@ -178,9 +180,11 @@ __device__ __forceinline__ void setup_r_body(const KParams& p, const long b, con
             p.l[b * m + i] = li;
             p.u[b * m + i] = ui;
             p.E[b * m + i] = Ev[s];
-            p.ct[b * m + i] = t;
-            p.z[b * m + i] = 0.0;
-            p.y[b * m + i] = 0.0;
+            if (!KEEP) {
+                p.ct[b * m + i] = t;
+                p.z[b * m + i] = 0.0;
+                p.y[b * m + i] = 0.0;
+            }
         }
     }
     bad = block_any<TT>(bad, flag);
@@ -189,16 +193,18 @@ __device__ __forceinline__ void setup_r_body(const KParams& p, const long b, con
     if (pc < npad) {
         p.q[b * npad + pc] = qv;
         p.D[b * npad + pc] = Dv;
-        p.x[b * npad + pc] = 0.0;
+        if (!KEEP) p.x[b * npad + pc] = 0.0;
     }
     if (tid == 0) {
         p.scal[b * 4 + 0] = c;
         p.scal[b * 4 + 1] = 1.0 / c;
-        p.scal[b * 4 + 2] = rho;
         p.status[b] = MPCQP_UNSOLVED_;
         p.err[b] = bad ? 1 : 0;
-        p.iter[b] = 0;
-        p.rho_upd[b] = 0;
+        if (!KEEP) {
+            p.scal[b * 4 + 2] = rho;
+            p.iter[b] = 0;
+            p.rho_upd[b] = 0;
+        }
     }
 }
 

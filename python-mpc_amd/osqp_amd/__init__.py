@@ -121,6 +121,7 @@ def lib():
     L.mpcqp_setup_batch.argtypes = [C.c_int32, C.c_int32, i32p, i32p, i32p, i32p, C.c_int64,
                                     dp, dp, dp, dp, dp, _P(_Settings), C.c_uint32, hp]
     L.mpcqp_update_batch.argtypes = [vp, dp, dp, dp]
+    L.mpcqp_update_matrices_batch.argtypes = [vp, dp, i32p, C.c_int32, dp, i32p, C.c_int32]
     L.mpcqp_warm_start_batch.argtypes = [vp, dp, dp]
     L.mpcqp_solve_batch.argtypes = [vp, dp, dp, i32p, i32p]
     L.mpcqp_get_info_batch.argtypes = [vp, dp, dp, dp, dp, i32p]
@@ -217,6 +218,15 @@ def analyze(P, A, eliminate=False):
     return out + (ne.value,) if eliminate else out
 
 
+def _kept_index(V):
+    """Per value index of the user's pattern: its index once the entries zero in every
+    instance are dropped (_drop_common_zeros), or -1."""
+    keep = np.any(np.asarray(V) != 0, axis=0)
+    out = np.full(keep.size, -1, np.int64)
+    out[keep] = np.arange(int(keep.sum()))
+    return out
+
+
 def _drop_common_zeros(M, V):
     keep = np.any(V != 0, axis=0)
     if keep.all():
@@ -270,6 +280,10 @@ class OSQPBatch:
         # operation, so dropping them is bit-for-bit neutral; it keeps structural
         # zeros of the reference's assembly (e.g. C~'QC~ at mpc_dynamics.py:296-297)
         # out of the sparsity plan.
+        # user value index -> index in the kept pattern (-1: dropped), for update(Px_idx=, Ax_idx=)
+        self._pmap = _kept_index(Px)
+        self._amap = _kept_index(Ax)
+        self._nnz_user = (P.nnz, A.nnz)
         P, Px = _drop_common_zeros(P, Px)
         A, Ax = _drop_common_zeros(A, Ax)
         Px = np.ascontiguousarray(Px, np.float64)
@@ -293,12 +307,51 @@ class OSQPBatch:
             raise ValueError("Workspace not initialized!")
         return self._h.ptr
 
-    def update(self, q=None, l=None, u=None, Px=None, Ax=None, **kw):
+    def update(self, q=None, l=None, u=None, Px=None, Px_idx=None, Ax=None, Ax_idx=None):
+        """osqp-python 0.6's update order: q, the bounds, then the matrices.  Px: (B, k)
+        values of triu(P) at Px_idx (k indices into the setup's triu(P).tocsc() value array;
+        None or empty: all nnz), likewise Ax / Ax_idx (mpcqp_update_matrices_batch)."""
         h = self._need()
-        if Px is not None or Ax is not None or kw:
-            raise NotImplementedError("matrix updates (Px/Ax) are not supported; run setup() again")
-        if q is None and l is None and u is None:
+        if q is None and l is None and u is None and Px is None and Ax is None:
             raise ValueError("No updatable data has been specified!")
+        B, n, m = self.B, self.n, self.m
+        if q is not None or l is not None or u is not None:
+            self._update_vectors(h, q, l, u)
+        if Px is not None or Ax is not None:
+            P = self._matrix_values(Px, Px_idx, self._pmap, self._nnz_user[0], "P")
+            A = self._matrix_values(Ax, Ax_idx, self._amap, self._nnz_user[1], "A")
+            pv, pi = P if P else (None, None)
+            av, ai = A if A else (None, None)
+            _check(lib().mpcqp_update_matrices_batch(
+                h, _dp(pv), None if pi is None else _ip(pi), 0 if pi is None else len(pi),
+                _dp(av), None if ai is None else _ip(ai), 0 if ai is None else len(ai)), "update matrices")
+
+    def _matrix_values(self, V, idx, kmap, nnz_user, name):
+        """(values (B, k') in the kept pattern, kept indices (k',)) for the library, or None.
+        A value for an entry that was zero in every instance at setup (dropped from the
+        pattern) must stay zero: the pattern is fixed."""
+        if V is None:
+            return None
+        B = self.B
+        V = np.asarray(V, np.float64)
+        if idx is None or np.size(idx) == 0:
+            V = V.reshape(B, nnz_user)
+            idx = np.arange(nnz_user)
+        else:
+            idx = np.asarray(idx).ravel().astype(np.int64)
+            if idx.size > nnz_user:
+                raise ValueError(f"new number of elements ({idx.size}) greater than elements in {name} ({nnz_user})")
+            if idx.min() < 0 or idx.max() >= nnz_user:
+                raise ValueError(f"{name}x_idx out of range")
+            V = V.reshape(B, idx.size)
+        kept = kmap[idx]
+        dropped = kept < 0
+        if np.any(V[:, dropped] != 0):
+            raise ValueError(f"{name}x sets an entry that was zero in every instance at setup "
+                             "(not in the sparsity pattern); run setup() again")
+        return (np.ascontiguousarray(V[:, ~dropped]), np.ascontiguousarray(kept[~dropped], np.int32))
+
+    def _update_vectors(self, h, q, l, u):
         B, n, m = self.B, self.n, self.m
 
         def prep(v, k, clip):
@@ -393,7 +446,10 @@ class OSQP:
             if len(u) != m:
                 raise ValueError("u must have length m")
         t0 = time.perf_counter()
-        self._b.update(q=q, l=l, u=u, Px=Px, Ax=Ax)
+        self._b.update(q=None if q is None else np.asarray(q, np.float64)[None, :],
+                       l=None if l is None else l[None, :], u=None if u is None else u[None, :],
+                       Px=None if Px is None else np.asarray(Px, np.float64)[None, :], Px_idx=Px_idx,
+                       Ax=None if Ax is None else np.asarray(Ax, np.float64)[None, :], Ax_idx=Ax_idx)
         self._update_time = time.perf_counter() - t0
 
     def warm_start(self, x=None, y=None):

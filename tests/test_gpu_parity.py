@@ -854,3 +854,89 @@ def test_plan_and_kernel_per_config(cfg, nb, ne, variant):
              **{k: v for k, v in b["settings"].items() if k != "verbose"})
     info = bg.plan_info()
     assert (info["nb"], info["n_eliminated"], info["variant"]) == (nb, ne, variant)
+
+
+@pytest.mark.parametrize("warm", [False, True])
+def test_matrix_updates_match_oracle(warm):
+    """update(Px=, Ax=, Ax_idx=) -- mpcqp_update_matrices_batch, OSQP 0.6 osqp_update_P_A:
+    unscale, new values, rescale, refactor at the next solve, iterates kept -- on a cfg-2
+    batch: solved, then every P value scaled by 1.5 and solved, then a third of A's values
+    changed by index (with a repeated index) and solved, each against the oracle doing the
+    same calls."""
+    b = mpc.make_batch(2, B=64, seed=9)
+    s = dict(warm_start=warm)
+    P, A = b["P"], b["A"]
+    dev = OSQPBatch()
+    dev.setup(P, b["q"], A, b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
+    orc = []
+    for k in range(b["Px"].shape[0]):
+        o = pyoracle.OSQP()
+        Pk, Ak = P.copy(), A.copy()
+        Pk.data, Ak.data = b["Px"][k].copy(), b["Ax"][k].copy()
+        o.setup(Pk, b["q"][k], Ak, b["l"][k], b["u"][k], **s)
+        orc.append(o)
+    rng = np.random.default_rng(3)
+    idx = np.concatenate([np.arange(0, A.nnz, 3), [0]])
+    for step in range(3):
+        if step == 1:
+            Pn = b["Px"] * 1.5
+            dev.update(Px=Pn)
+            for k, o in enumerate(orc):
+                o.update(Px=Pn[k])
+        elif step == 2:
+            An = b["Ax"][:, idx] * rng.uniform(0.9, 1.1, (b["Ax"].shape[0], idx.size))
+            dev.update(Ax=An, Ax_idx=idx)
+            for k, o in enumerate(orc):
+                o.update(Ax=An[k], Ax_idx=idx)
+        rd = dev.solve()
+        ro = [o.solve() for o in orc]
+        st = np.array([r.info.status_val for r in ro])
+        it = np.array([r.info.iter for r in ro])
+        assert np.mean(rd.status_val == st) >= 0.99, step
+        assert np.mean(rd.iter == it) >= 0.99, step
+        same = (rd.iter == it) & (st == 1)
+        assert same.sum() >= 0.9 * len(ro), step
+        du = np.array([np.abs(rd.x[k, b["u_block"]] - ro[k].x[b["u_block"]]).max() for k in range(len(ro))])
+        assert np.all(du[same] < U_TOL), (step, du[same].max())
+
+
+def test_shim_matrix_update_demo():
+    """osqp.OSQP().update(Px=, Px_idx=, Ax=, Ax_idx=) through the shim on the osqp
+    documentation's demo problem and its update_P_A example, with an index update after
+    it: the same iteration counts as the oracle and x to 1e-9."""
+    import scipy.sparse as sps
+    P = sps.csc_matrix(np.array([[4.0, 1.0], [1.0, 2.0]]))
+    A = sps.csc_matrix(np.array([[1.0, 1.0], [1.0, 0.0], [0.0, 1.0]]))
+    q, l, u = np.array([1.0, 1.0]), np.array([1.0, 0.0, 0.0]), np.array([1.0, 0.7, 0.7])
+    s = dict(eps_abs=1e-6, eps_rel=1e-6, verbose=False)
+    g, o = OSQP(), pyoracle.OSQP()
+    g.setup(P, q, A, l, u, **s)
+    o.setup(P, q, A, l, u, **s)
+    calls = [dict(),
+             dict(Px=np.array([5.0, 1.5, 1.0]), Ax=np.array([1.2, 1.5, 1.1, 0.8])),
+             dict(Px=np.array([3.0]), Px_idx=np.array([0]), Ax=np.array([0.9, 1.0]), Ax_idx=np.array([2, 2]))]
+    for c in calls:
+        if c:
+            g.update(**c)
+            o.update(**c)
+        rg, ro = g.solve(), o.solve()
+        assert rg.info.status == ro.info.status == "solved"
+        assert rg.info.iter == ro.info.iter
+        assert np.abs(rg.x - ro.x).max() < 1e-9
+
+
+def test_matrix_update_keeps_the_pattern():
+    """An entry that is zero in every instance at setup is not in the device's pattern:
+    setting it nonzero is refused (run setup again), keeping it zero is fine."""
+    import scipy.sparse as sps
+    # triu(P) with an explicit zero at (0, 1): in osqp's pattern, dropped from the device's
+    P = sps.csc_matrix((np.array([4.0, 0.0, 2.0]), np.array([0, 0, 1]), np.array([0, 1, 3])), shape=(2, 2))
+    A = sps.csc_matrix(np.array([[1.0, 1.0], [1.0, 0.0], [0.0, 1.0]]))
+    q, l, u = np.array([1.0, 1.0]), np.array([1.0, 0.0, 0.0]), np.array([1.0, 0.7, 0.7])
+    g = OSQP()
+    g.setup(P, q, A, l, u, verbose=False)
+    g.solve()
+    with pytest.raises(ValueError):
+        g.update(Px=np.array([4.0, 1.0, 2.0]))
+    g.update(Px=np.array([5.0, 0.0, 2.0]))
+    assert g.solve().info.status == "solved"

@@ -208,3 +208,58 @@ def test_oracle_osqp_demo_known_answer(eps, tol):
     assert np.abs(r.x - xs).max() < tol
     assert np.abs(r.y - ys).max() < 10 * tol
     assert abs(r.info.obj_val - obj) < 10 * tol
+
+
+def _demo_update_values():
+    """The values of the osqp documentation's update_P_A example on the demo problem:
+    P = [[5, 1.5], [1.5, 1]], A = [[1.2, 1.1], [1.5, 0], [0, 0.8]] (triu(P) / A CSC order)."""
+    return np.array([5.0, 1.5, 1.0]), np.array([1.2, 1.5, 1.1, 0.8])
+
+
+@pytest.mark.parametrize("eps", [1e-3, 1e-9])
+def test_oracle_matrix_update_equals_fresh_setup(eps):
+    """orc_update_P_A (OSQP 0.6 osqp_update_P_A: unscale, new values, rescale, refactor)
+    from a cold start gives the fresh setup's solve on the new matrices: the same iteration
+    count, x within the unscale/rescale round trip's rounding.  Then an index update of two
+    A values, against a fresh setup of the matrix it makes.  (Fixed rho: an update keeps
+    the rho the previous solve adapted to, a fresh setup starts from the setting.)"""
+    P, q, A, l, u, *_ = osqp_demo_problem()
+    s = dict(eps_abs=eps, eps_rel=eps, warm_start=False, adaptive_rho=False)
+    o = pyoracle.OSQP()
+    o.setup(P, q, A, l, u, **s)
+    o.solve()
+    Pn, An = _demo_update_values()
+    o.update(Px=Pn, Ax=An)
+    r = o.solve()
+    Pf, Af = sp.triu(sp.csc_matrix(P), format="csc"), sp.csc_matrix(A)
+    Pf.data, Af.data = Pn.copy(), An.copy()
+    f = pyoracle.OSQP()
+    f.setup(Pf, q, Af, l, u, **s)
+    rf = f.solve()
+    assert r.info.status == rf.info.status == "solved"
+    assert r.info.iter == rf.info.iter
+    assert np.abs(r.x - rf.x).max() < 1e-12
+    # index update, a repeated index taking its last value (OSQP's sequential loop)
+    o.update(Ax=np.array([9.0, 0.5, 1.0]), Ax_idx=np.array([3, 0, 3]))
+    r2 = o.solve()
+    Af.data = np.array([0.5, 1.5, 1.1, 1.0])
+    f2 = pyoracle.OSQP()
+    f2.setup(Pf, q, Af, l, u, **s)
+    rf2 = f2.solve()
+    assert r2.info.iter == rf2.info.iter
+    assert np.abs(r2.x - rf2.x).max() < 1e-12
+
+
+def test_oracle_matrix_update_keeps_the_iterates():
+    """With warm starting, OSQP 0.6 keeps x, z, y through a matrix update: updating P to
+    its own values and solving again starts at the previous solution (one check interval),
+    where a cold start needs the full count."""
+    P, q, A, l, u, *_ = osqp_demo_problem()
+    o = pyoracle.OSQP()
+    o.setup(P, q, A, l, u, warm_start=True, eps_abs=1e-7, eps_rel=1e-7)
+    r0 = o.solve()
+    o.update(Px=np.array([4.0, 1.0, 2.0]))
+    r1 = o.solve()
+    assert r1.info.status == "solved"
+    assert r1.info.iter < r0.info.iter
+    assert np.abs(r1.x - r0.x).max() < 1e-6
