@@ -524,7 +524,7 @@ def main(argv=None, solver_cls=None, device=None):
     # Diagnostic, outside the timed region and never `value`: the rate with the batch handed
     # over in host memory (the PCIe-inclusive line of DESIGN.md §6)
     pcie = None
-    if (rank == 0 and on_gpu and not args.no_pcie and not args.assemble and not warm and fused
+    if (rank == 0 and world == 1 and on_gpu and not args.no_pcie and not args.assemble and not warm and fused
             and B <= 65536 and hasattr(solver, "stream_handle")):
         import torch as _t
         pin = lambda a: _t.from_numpy(np.ascontiguousarray(a)).pin_memory()  # noqa: E731
