@@ -624,6 +624,14 @@ def test_own_stream_calls_are_ordered_without_events():
     ref.setup_solve(*ins[0], *r[0])
     assert lib().mpcqp_last_kernel_ms(ref._h.ptr) > 0.0
     ref.timing(False)
+    # mask 2 alone: setup launches timed, solve launches not (mpcqp.h::mpcqp_timing)
+    lib().mpcqp_timing(ref._h.ptr, 2)
+    ref.setup(*ins[1])
+    ref.solve(*r[1])
+    ref.synchronize()
+    kt = ref.timing_read()
+    assert kt["n_setup"] == 1 and kt["setup_ms"] > 0.0 and kt["n_solve"] == 0, kt
+    ref.timing(False)
 
 
 @pytest.mark.parametrize("cfg,B", [(2, 512), (3, 512)])

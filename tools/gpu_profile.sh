@@ -20,8 +20,8 @@ step() {  # step <name> <timeout> <cmd...>: stdout+stderr to $out/<name>.log
     if [ $rc -ne 0 ]; then echo "$name failed ($rc)" | tee -a "$out/failed"; exit $rc; fi
 }
 timeout -k 10 300 python3 bench.py "${args[@]}" > $out/bench.json 2> $out/bench.err || { echo "bench failed"; exit 1; }
-short=(--no-cpu --no-dispatch-ab --steps 4 --warmup 1 "${args[@]}")
-step kt 240 rocprofv3 --kernel-trace --stats -d $out/kt -o kt --output-format csv -- python3 bench.py --no-cpu --no-dispatch-ab --steps 10 --warmup 2 "${args[@]}"
+short=(--no-cpu --no-dispatch-ab --no-pcie --steps 4 --warmup 1 "${args[@]}")
+step kt 240 rocprofv3 --kernel-trace --stats -d $out/kt -o kt --output-format csv -- python3 bench.py --no-cpu --no-dispatch-ab --no-pcie --steps 10 --warmup 2 "${args[@]}"
 step pmc_f 120 rocprofv3 --pmc FETCH_SIZE -d $out/pmc_f -o f --output-format csv -- python3 bench.py "${short[@]}"
 step pmc_w 120 rocprofv3 --pmc WRITE_SIZE -d $out/pmc_w -o w --output-format csv -- python3 bench.py "${short[@]}"
 step sq1 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS -d $out/sq1 -o sq1 --output-format csv -- python3 bench.py "${short[@]}"

@@ -15,6 +15,9 @@ import statistics
 import sys
 
 
+KT_STEPS = 10  # tools/gpu_profile.sh's kt run: --steps 10 unless its args override it (read from kt.log)
+
+
 def rows(pattern):
     out = []
     for f in glob.glob(pattern):
@@ -43,6 +46,23 @@ def main():
         if kernel.split("::")[-1] in r["Name"]:
             res["kernel_trace_mean_ms"] = float(r["AverageNs"]) / 1e6
             res["kernel_trace_calls"] = int(r["Calls"])
+    # the timed steps' launches: the last `steps` launches of the kernel in the kt run (no
+    # identity-dispatch or PCIe legs after the timed region), against the bench line's own
+    # in-region HIP-event time
+    tr = [r for r in rows(os.path.join(d, "kt", "*kernel_trace.csv")) if kernel.split("::")[-1] in r["Kernel_Name"]]
+    if tr:
+        tr.sort(key=lambda r: int(r["Start_Timestamp"]))
+        steps = KT_STEPS
+        ktlog = os.path.join(d, "kt.log")
+        if os.path.exists(ktlog):  # the kt run's own bench line says how many steps it timed
+            js = [ln for ln in open(ktlog) if ln.startswith("{")]
+            if js:
+                steps = json.loads(js[-1])["steps"]
+        dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in tr[-steps:]]
+        res["kernel_trace_timed_launches"] = len(dur)
+        res["kernel_trace_timed_mean_ms"] = statistics.mean(dur)
+        res["bench_kernel_ms"] = line["roofline"]["kernel_ms"]
+        res["timed_mean_over_bench"] = statistics.mean(dur) / line["roofline"]["kernel_ms"]
     f, nf = per_launch(rows(os.path.join(d, "pmc_f", "*counter_collection.csv")), kernel)
     w, nw = per_launch(rows(os.path.join(d, "pmc_w", "*counter_collection.csv")), kernel)
     if "FETCH_SIZE" in f and "WRITE_SIZE" in w:
