@@ -75,6 +75,7 @@ extern "C" {
 #define MPCQP_EUNSUPPORTED 2  /* sparsity structure or setting not supported */
 #define MPCQP_EDEVICE 3       /* HIP runtime error / no device */
 #define MPCQP_ENOMEM 4
+#define MPCQP_ENONCVX 5       /* mpcqp_setup_batch: an instance's P is not convex (OSQP_NONCVX_ERROR) */
 
 typedef struct {
     double rho, sigma, alpha;
@@ -120,6 +121,10 @@ int mpcqp_setup_batch(int32_t n, int32_t m,
                       const mpcqp_settings *settings, uint32_t device_mask,
                       mpcqp_handle **out);
 
+/* (mpcqp_setup_batch, as osqp_setup) returns MPCQP_ENONCVX when an instance's KKT matrix is
+ * not quasi-definite (P + sigma I + A' diag(rho) A not positive definite): one factor-only
+ * launch of the solve kernel checks every instance.  The device entry points do not check;
+ * their solve reports such an instance as non-convex (status -7). */
 /* q, l, u may each be NULL (not updated). */
 int mpcqp_update_batch(mpcqp_handle *h, const double *q, const double *l, const double *u);
 /* osqp_update_P / osqp_update_A / osqp_update_P_A (OSQP 0.6): new values of P's upper
@@ -130,7 +135,8 @@ int mpcqp_update_batch(mpcqp_handle *h, const double *q, const double *l, const 
  * NULL.  As OSQP: the data is unscaled, updated, scaled afresh and refactored at the next
  * solve; x, z, y, rho and the row classes are kept (the iterates stay in the previous
  * scaling).  The sparsity pattern is fixed.  Handles of mpcqp_setup_batch only, not in
- * shared-matrix mode.  Replaces prob.update(Px=, Px_idx=, Ax=, Ax_idx=), which the reference
+ * shared-matrix mode.  MPCQP_ENONCVX when the new matrices are not convex (OSQP's update
+ * refactors at once).  Replaces prob.update(Px=, Px_idx=, Ax=, Ax_idx=), which the reference
  * mentions at vehicle_lateral_mpc_slack_increment.py:236 (commented out). */
 int mpcqp_update_matrices_batch(mpcqp_handle *h, const double *Px, const int32_t *Px_idx, int32_t nPx,
                                 const double *Ax, const int32_t *Ax_idx, int32_t nAx);

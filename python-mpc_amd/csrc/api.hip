@@ -393,6 +393,31 @@ int check_err_flags(mpcqp_handle* h) {
     return 0;
 }
 
+// osqp_setup's convexity test (OSQP 0.6 init_linsys_solver: the quasi-definite KKT matrix
+// must have n positive pivots, which holds iff P + sigma I + A' diag(rho) A is positive
+// definite -- the reduced matrix the solve kernels factor): one factor-only launch of the
+// solve kernel per shard, which stops after the first factorisation and marks an instance
+// whose factorisation fails as non-convex.  The first such instance is reported.
+int check_convex(mpcqp_handle* h) {
+    for (auto& s : h->shards) {
+        HIPCHK(hipSetDevice(s.dev));
+        if (int e = stream_enter(s, s.stream)) return e;
+        HIPCHK(launch_solve(s.kp, s.B, s.out_x, s.out_y, 1, s.stream));
+        if (int e = stream_leave(s, s.stream)) return e;
+    }
+    if (int e = sync_all(h)) return e;
+    for (auto& s : h->shards) {
+        std::vector<int> st(s.B);
+        HIPCHK(hipSetDevice(s.dev));
+        HIPCHK(hipMemcpy(st.data(), s.kp.status, sizeof(int) * s.B, hipMemcpyDeviceToHost));
+        for (long i = 0; i < s.B; ++i)
+            if (st[i] == MPCQP_NON_CVX_)
+                return fail(MPCQP_ENONCVX, "instance %ld: P is not convex (the KKT matrix is not quasi-definite)",
+                            s.b0 + i);
+    }
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -465,6 +490,7 @@ int mpcqp_setup_batch(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi
         if (int e = upload(s)) { mpcqp_free(h); return e; }
     if (int e = sync_all(h)) { mpcqp_free(h); return e; }
     if (int e = check_err_flags(h)) { mpcqp_free(h); return e; }
+    if (int e = check_convex(h)) { mpcqp_free(h); return e; }
     *out = h;
     return 0;
 }
@@ -562,7 +588,8 @@ int mpcqp_update_matrices_batch(mpcqp_handle* h, const double* Px, const int32_t
     if (!err) err = sync_all(h);
     release();
     if (err) return err;
-    return check_err_flags(h);
+    if (int e = check_err_flags(h)) return e;
+    return check_convex(h);  // osqp_update_P_A refactors at once and reports a failed factorisation
 }
 
 int mpcqp_warm_start_batch(mpcqp_handle* h, const double* x, const double* y) {

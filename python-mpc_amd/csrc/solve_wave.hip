@@ -1037,8 +1037,11 @@ constexpr int T4 = 256;
 // which the rows phase reads from xt like any other column.  Its termination-check column
 // is pe (the lower half keeps the block column).
 // K: row-list length, KC: column-list length (even: the rhs splits it over the half-waves).
+// factor_only: return after the first factorisation (the setup-time convexity check of
+// api.hip::check_convex); the fused setup + solve kernel passes 0
 template <int K, int KPK, int QR, bool EL = false, int KC = K>
-__device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restrict__ xo, double* __restrict__ yo) {
+__device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restrict__ xo, double* __restrict__ yo,
+                                              int factor_only = 0) {
     const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int h = lane >> 5, r = lane & 31, rr = lane >> 3, ch = lane & 7;
     constexpr int NB = 4, NP = NB * (NB - 1) / 2;  // exactly four blocks (solve.hip::variant_fits)
@@ -1146,6 +1149,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 can_check = true;
                 break;
             }
+            if (factor_only) return;
             __syncthreads();
             const bool have_y = iter > 0 || warm;
             {
@@ -1615,10 +1619,12 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
 #undef PH
 }
 
-template <int K, int KPK, int QR, bool EL = false, int KC = K>
+// FO: the factor-only instantiation (api.hip::check_convex), so that the solve's own code
+// carries no factor_only test
+template <int K, int KPK, int QR, bool EL = false, int KC = K, bool FO = false>
 __global__ __launch_bounds__(T4, 2) void k_solve_w4(KParams p, double* __restrict__ xo, double* __restrict__ yo,
-                                                    int factor_only) {
-    solve_w4_body<K, KPK, QR, EL, KC>(p, xo, yo);
+                                                    int /*factor_only: FO*/) {
+    solve_w4_body<K, KPK, QR, EL, KC>(p, xo, yo, FO ? 1 : 0);
     extern __shared__ __attribute__((aligned(16))) double sm[];
     order_epilogue<T4>(p, (int*)sm);
 }
@@ -2227,7 +2233,11 @@ hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, i
         case 9: return go_w<8, 4>(p, B, xo, yo, factor_only, st, lds, ref);
 #endif
         case 17: {
-            auto k = p.ne ? k_solve_w4<6, 4, 8, true, 8> : (p.amax <= 5 ? k_solve_w4<6, 4, 5> : k_solve_w4<6, 4, 8>);
+            auto k = factor_only
+                         ? (p.ne ? k_solve_w4<6, 4, 8, true, 8, true>
+                                 : (p.amax <= 5 ? k_solve_w4<6, 4, 5, false, 6, true> : k_solve_w4<6, 4, 8, false, 6, true>))
+                         : (p.ne ? k_solve_w4<6, 4, 8, true, 8>
+                                 : (p.amax <= 5 ? k_solve_w4<6, 4, 5> : k_solve_w4<6, 4, 8>));
             const size_t lds = lds_w2_bytes(p);
             hipError_t e = lists_fit(p, 6, p.ne ? 8 : 6, 4, p.ne || p.amax > 5 ? 8 : 5);
             if (e != hipSuccess) return e;

@@ -166,7 +166,7 @@ def _ip(a):
 def _check(code, what):
     if code:
         msg = lib().mpcqp_last_error().decode()
-        if code == 1:
+        if code in (1, 5):  # invalid data; non-convex P (osqp-python raises ValueError at setup)
             raise ValueError(f"{what}: {msg}")
         if code == 2:
             raise NotImplementedError(f"{what}: {msg}")

@@ -948,3 +948,31 @@ def test_matrix_update_keeps_the_pattern():
         g.update(Px=np.array([4.0, 1.0, 2.0]))
     g.update(Px=np.array([5.0, 0.0, 2.0]))
     assert g.solve().info.status == "solved"
+
+
+def test_nonconvex_setup_raises_like_osqp():
+    """osqp_setup refuses a problem whose KKT matrix is not quasi-definite (a non-convex P):
+    osqp-python raises ValueError at setup, and so do the shim and OSQPBatch
+    (api.hip::check_convex, one factor-only launch) -- for a single QP, for one bad instance
+    in a cfg-2 batch (the four-wave kernel's factor-only instantiation), and for a matrix
+    update that makes P non-convex.  The oracle rejects the same problems."""
+    import scipy.sparse as sps
+    P = sps.csc_matrix(np.array([[-1.0, 0.0], [0.0, 1.0]]))
+    A = sps.csc_matrix(np.array([[1.0, 1.0]]))
+    q, l, u = np.zeros(2), np.array([-1.0]), np.array([1.0])
+    with pytest.raises(ValueError):
+        pyoracle.OSQP().setup(P, q, A, l, u)
+    with pytest.raises(ValueError, match="not convex"):
+        OSQP().setup(P, q, A, l, u, verbose=False)
+    b = mpc.make_batch(2, B=64, seed=12)
+    s = {k: v for k, v in b["settings"].items() if k != "verbose"}
+    Px = b["Px"].copy()
+    Px[37] *= -1.0
+    h = OSQPBatch()
+    with pytest.raises(ValueError, match="instance 37"):
+        h.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=Px, Ax=b["Ax"], **s)
+    h.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
+    assert h.plan_info()["variant"] == 17
+    assert (h.solve().status_val == 1).all()
+    with pytest.raises(ValueError, match="instance 37"):
+        h.update(Px=Px)
