@@ -1658,7 +1658,8 @@ __global__ __launch_bounds__(T4, 2) void k_setup_solve_w4(KParams p, const doubl
 constexpr int T8 = 512;
 
 template <int K, int KPK>
-__device__ __forceinline__ void solve_w8_body(const KParams& p, double* __restrict__ xo, double* __restrict__ yo) {
+__device__ __forceinline__ void solve_w8_body(const KParams& p, double* __restrict__ xo, double* __restrict__ yo,
+                                              int factor_only) {
     const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int h = lane >> 5, r = lane & 31, rr = lane >> 2, ch = lane & 3;
     constexpr int NB = 8, NP = NB * (NB - 1) / 2;  // exactly eight blocks (solve.hip::variant_fits)
@@ -1749,6 +1750,7 @@ __device__ __forceinline__ void solve_w8_body(const KParams& p, double* __restri
                 can_check = true;
                 break;
             }
+            if (factor_only) return;
             __syncthreads();
             {
                 const double* src = Sg + (long)w * SS + r * S + 16 * h;
@@ -2135,7 +2137,7 @@ __device__ __forceinline__ void solve_w8_body(const KParams& p, double* __restri
 template <int K, int KPK>
 __global__ __launch_bounds__(T8, 1) void k_solve_w8(KParams p, double* __restrict__ xo, double* __restrict__ yo,
                                                     int factor_only) {
-    solve_w8_body<K, KPK>(p, xo, yo);
+    solve_w8_body<K, KPK>(p, xo, yo, factor_only);
     extern __shared__ __attribute__((aligned(16))) double sm[];
     order_epilogue<T8>(p, (int*)sm);
 }
