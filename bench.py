@@ -357,6 +357,10 @@ def main(argv=None, solver_cls=None, device=None):
         raise SystemExit(launch(args.gpus, cmd))
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were started")
+    if os.environ.get("MPCQP_BENCH_SHARE_GPU") == "1":
+        # diagnostic: every rank on GPU 0, to rehearse the N > 1 path (ranks, gloo barriers,
+        # max over ranks, rank 0's line) on a one-GPU box; never for a measurement
+        local = 0
     import torch
     import torch.distributed as dist
     from osqp_amd import DeviceBatch, _drop_common_zeros
