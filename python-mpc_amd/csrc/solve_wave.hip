@@ -39,7 +39,7 @@
 
 namespace mpcqp {
 
-constexpr int TW = 64;
+[[maybe_unused]] constexpr int TW = 64;
 
 #ifdef MPCQP_EXPERIMENTAL  // the one-wave kernels (variants 8, 9): make exp / MPCQP_BUILD=exp
 // S^{-1} rows of the lane's two blocks, SB[e][c] = S_{kb_e}^{-1}[r][c] (128 VGPRs)
@@ -1043,7 +1043,7 @@ template <int K, int KPK, int QR, bool EL = false, int KC = K>
 __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restrict__ xo, double* __restrict__ yo,
                                               int factor_only = 0) {
     const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const int h = lane >> 5, r = lane & 31, rr = lane >> 3, ch = lane & 7;
+    const int h = lane >> 5, r = lane & 31;  // (rr, ch: per pass, below)
     constexpr int NB = 4, NP = NB * (NB - 1) / 2;  // exactly four blocks (solve.hip::variant_fits)
     static_assert(KC % 2 == 0, "the rhs splits the column list over the half-waves");
     constexpr int KH = KC / 2;                       // column-list entries per half in the rhs
@@ -2228,7 +2228,7 @@ size_t lds_w2_bytes(const KParams& p) {
 // Wave-kernel instantiations (solve.hip::variant_fits gives their preconditions).
 hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st,
                              KernelRef* ref) {
-    const size_t lds = lds_solve_bytes(p);
+    [[maybe_unused]] const size_t lds = lds_solve_bytes(p);  // (the experimental variants')
     switch (p.variant) {
 #ifdef MPCQP_EXPERIMENTAL
         case 8: return go_w<6, 3>(p, B, xo, yo, factor_only, st, lds, ref);
