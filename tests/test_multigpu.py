@@ -31,7 +31,10 @@ def _solve(b, monkeypatch, split, **s):
     u[:, :2] *= 0.9
     h.update(l=l, u=u)
     r2 = h.solve()
-    return r1, r2
+    # a matrix update (mpcqp_update_matrices_batch: each shard's slice of the values)
+    h.update(Px=b["Px"] * 1.25, Ax=b["Ax"][:, ::2] * 0.95, Ax_idx=np.arange(0, b["Ax"].shape[1], 2))
+    r3 = h.solve()
+    return r1, r2, r3
 
 
 @pytest.mark.parametrize("cfg,B,split", [(2, 1000, 3), (3, 257, 2), (5, 40, 4)])
