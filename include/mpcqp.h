@@ -14,6 +14,7 @@
  *                            Control/MPC/mpc_incre_kine_func.py:179-180
  *   mpcqp_update_batch    <- prob.update(q=q_new, l=l_new, u=u_new)
  *                            vehicle_lateral_mpc_slack_increment.py:237,269
+ *   mpcqp_update_settings <- prob.update_settings(**kwargs)   (osqp API; not called by the reference)
  *   mpcqp_update_matrices_batch <- prob.update(Px=, Px_idx=, Ax=, Ax_idx=)
  *                            vehicle_lateral_mpc_slack_increment.py:236 (commented out there)
  *   mpcqp_warm_start_batch<- prob.warm_start(x=..., y=...)   (osqp API; used for
@@ -142,6 +143,14 @@ int mpcqp_update_matrices_batch(mpcqp_handle *h, const double *Px, const int32_t
                                 const double *Ax, const int32_t *Ax_idx, int32_t nAx);
 /* x, y may each be NULL (keeps the current iterate of that part). */
 int mpcqp_warm_start_batch(mpcqp_handle *h, const double *x, const double *y);
+/* osqp_update_settings / osqp_update_rho (OSQP 0.6; osqp-python's update_settings): max_iter,
+ * eps_abs, eps_rel, eps_prim_inf, eps_dual_inf, rho (clipped to [1e-6, 1e6], every instance,
+ * refactored at the next solve), alpha, delta, polish, polish_refine_iter, scaled_termination,
+ * check_termination, warm_start take the new values; sigma, scaling and the adaptive-rho
+ * settings must be unchanged (MPCQP_EINVAL otherwise), as OSQP fixes them at setup.  Any
+ * handle.  polish = 1 on a handle whose plan eliminated variables (the slack layouts set up
+ * without polish) is MPCQP_EUNSUPPORTED. */
+int mpcqp_update_settings(mpcqp_handle *h, const mpcqp_settings *s);
 /* any output may be NULL */
 int mpcqp_solve_batch(mpcqp_handle *h, double *x, double *y, int32_t *status, int32_t *iters);
 /* info of the last solve; any output may be NULL */

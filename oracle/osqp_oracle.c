@@ -552,6 +552,15 @@ int orc_setup(orc_work **out, int n, int m, const int *Pp, const int *Pi, const 
     int e = kkt_init(&w->kkt, n, m, w->Pp, w->Pi, w->Px, w->Ap, w->Ai, w->Ax, w->set.sigma,
                      w->rho_inv_vec);
     if (e) { orc_cleanup(w); return e; }
+    /* non-profiling rule for adaptive_rho_interval == 0 (pinned, see header), resolved here as
+     * osqp_setup does in builds without profiling: a later update_settings(check_termination=)
+     * does not move it */
+    if (w->set.adaptive_rho && !w->set.adaptive_rho_interval) {
+        if (w->set.check_termination)
+            w->set.adaptive_rho_interval = ADAPTIVE_RHO_MULTIPLE_TERMINATION * w->set.check_termination;
+        else
+            w->set.adaptive_rho_interval = ADAPTIVE_RHO_FIXED;
+    }
     w->info.status_val = ORC_UNSOLVED;
     w->info.rho_updates = 0;
     w->info.rho_estimate = w->set.rho;
@@ -662,6 +671,40 @@ int orc_update_P_A(orc_work *w, const double *Px, const int *Px_idx, int nP, con
                      w->rho_inv_vec);
     reset_info(w);
     return e;
+}
+
+/* osqp_update_settings as osqp-python 0.6 exposes it (update_max_iter, update_eps_abs, ...,
+ * update_rho): the settings OSQP lets change after setup are copied; rho goes through
+ * osqp_update_rho (clipped, rho vector by row class, KKT refactored).  sigma, scaling and
+ * the adaptive-rho settings are fixed at setup: a different value is a validation error. */
+static int osqp_update_rho(orc_work *w, double rho_new);
+
+int orc_update_settings(orc_work *w, const orc_settings *s) {
+    const orc_settings *o = &w->set;
+    if (s->sigma != o->sigma || s->scaling != o->scaling || s->adaptive_rho != o->adaptive_rho ||
+        s->adaptive_rho_tolerance != o->adaptive_rho_tolerance ||
+        (s->adaptive_rho_interval && s->adaptive_rho_interval != o->adaptive_rho_interval))
+        return ORC_SETTINGS_VALIDATION_ERROR;
+    if (s->max_iter <= 0 || s->eps_abs < 0 || s->eps_rel < 0 || (s->eps_abs == 0 && s->eps_rel == 0) ||
+        s->eps_prim_inf <= 0 || s->eps_dual_inf <= 0 || s->alpha <= 0 || s->alpha >= 2 ||
+        s->check_termination < 0 || s->rho <= 0 || s->delta <= 0 || s->polish_refine_iter < 0)
+        return ORC_SETTINGS_VALIDATION_ERROR;
+    const double rho = s->rho;
+    const int rho_changed = rho != o->rho;
+    w->set.max_iter = s->max_iter;
+    w->set.eps_abs = s->eps_abs;
+    w->set.eps_rel = s->eps_rel;
+    w->set.eps_prim_inf = s->eps_prim_inf;
+    w->set.eps_dual_inf = s->eps_dual_inf;
+    w->set.alpha = s->alpha;
+    w->set.delta = s->delta;
+    w->set.polish = s->polish;
+    w->set.polish_refine_iter = s->polish_refine_iter;
+    w->set.scaled_termination = s->scaled_termination;
+    w->set.check_termination = s->check_termination;
+    w->set.warm_start = s->warm_start;
+    if (rho_changed && osqp_update_rho(w, rho)) return ORC_NONCVX_ERROR;
+    return 0;
 }
 
 /* ---- auxil.c ---- */
@@ -1066,13 +1109,6 @@ int orc_solve(orc_work *w) {
         if (can_check) {
             update_info(w, iter, compute_cost);
             if (check_termination(w, 0)) break;
-        }
-        /* non-profiling rule for adaptive_rho_interval == 0 (pinned, see header) */
-        if (iter == 1 && w->set.adaptive_rho && !w->set.adaptive_rho_interval) {
-            if (w->set.check_termination)
-                w->set.adaptive_rho_interval = ADAPTIVE_RHO_MULTIPLE_TERMINATION * w->set.check_termination;
-            else
-                w->set.adaptive_rho_interval = ADAPTIVE_RHO_FIXED;
         }
         if (w->set.adaptive_rho && w->set.adaptive_rho_interval &&
             (iter % w->set.adaptive_rho_interval == 0)) {

@@ -80,6 +80,7 @@ def lib():
         for name in ("orc_update_lin_cost", "orc_update_lower_bound", "orc_update_upper_bound"):
             getattr(L, name).argtypes = [C.c_void_p, P(C.c_double)]
         L.orc_update_bounds.argtypes = [C.c_void_p, P(C.c_double), P(C.c_double)]
+        L.orc_update_settings.argtypes = [C.c_void_p, P(_Settings)]
         L.orc_update_P_A.argtypes = [C.c_void_p, P(C.c_double), P(C.c_int), C.c_int,
                                      P(C.c_double), P(C.c_int), C.c_int]
         L.orc_warm_start.argtypes = [C.c_void_p, P(C.c_double), P(C.c_double)]
@@ -149,6 +150,7 @@ class OSQP:
         P, A = canon(P, A)
         self.n, self.m = P.shape[0], A.shape[0]
         s = make_settings(**settings)
+        self._settings = dict(settings)
         self._keep = []
         arrs = [np.ascontiguousarray(P.indptr, np.int32), np.ascontiguousarray(P.indices, np.int32),
                 np.ascontiguousarray(P.data, np.float64), np.ascontiguousarray(q, np.float64),
@@ -195,9 +197,19 @@ class OSQP:
             if e:
                 raise ValueError(f"oracle matrix update failed (code {e})")
 
+    def update_settings(self, **kw):
+        """osqp.OSQP.update_settings: the settings OSQP lets change after setup"""
+        new = dict(self._settings, **kw)
+        s = make_settings(**new)
+        e = lib().orc_update_settings(self._w, C.byref(s))
+        if e:
+            raise ValueError(f"oracle update_settings failed (code {e})")
+        self._settings = new
+
     def warm_start(self, x=None, y=None):
         x = np.ascontiguousarray(x, np.float64); y = np.ascontiguousarray(y, np.float64)
         lib().orc_warm_start(self._w, _dp(x), _dp(y))
+        self._settings["warm_start"] = True  # (osqp_warm_start turns the setting on)
 
     def solve(self):
         L = lib()

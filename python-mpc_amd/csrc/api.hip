@@ -592,6 +592,45 @@ int mpcqp_update_matrices_batch(mpcqp_handle* h, const double* Px, const int32_t
     return check_convex(h);  // osqp_update_P_A refactors at once and reports a failed factorisation
 }
 
+int mpcqp_update_settings(mpcqp_handle* h, const mpcqp_settings* s) {
+    if (!h || !s) return fail(MPCQP_EINVAL, "NULL argument");
+    const mpcqp_settings& o = h->set;
+    if (s->sigma != o.sigma || s->scaling != o.scaling || s->adaptive_rho != o.adaptive_rho ||
+        s->adaptive_rho_tolerance != o.adaptive_rho_tolerance || s->adaptive_rho_interval != o.adaptive_rho_interval)
+        return fail(MPCQP_EINVAL, "sigma, scaling and the adaptive-rho settings cannot be changed after setup");
+    if (int e = validate_settings(*s)) return e;
+    if (s->polish && !(s->delta > 0 && s->polish_refine_iter >= 0)) return fail(MPCQP_EINVAL, "invalid polish settings");
+    if (s->polish && h->plan.ne > 0)
+        return fail(MPCQP_EUNSUPPORTED, "polish needs the full factor: this layout's handle eliminated %d variables; "
+                                        "run setup with polish on", h->plan.ne);
+    const bool rho_changed = s->rho != o.rho;
+    const double rho = std::min(std::max(s->rho, 1e-6), 1e6);  // osqp_update_rho: RHO_MIN / RHO_MAX
+    for (auto& sh : h->shards) {
+        KParams& k = sh.kp;
+        k.alpha = s->alpha; k.eps_abs = s->eps_abs; k.eps_rel = s->eps_rel;
+        k.eps_pinf = s->eps_prim_inf; k.eps_dinf = s->eps_dual_inf; k.rho0 = s->rho;
+        k.max_iter = s->max_iter; k.check_term = s->check_termination; k.warm_start = s->warm_start;
+        k.scaled_term = s->scaled_termination; k.polish = s->polish; k.refine_iter = s->polish_refine_iter;
+        k.delta = s->delta;
+        // (rho_interval keeps the value setup resolved: OSQP resolves the automatic interval
+        // in osqp_setup, so check_termination set later does not move it)
+        HIPCHK(hipSetDevice(sh.dev));
+        if (int e = stream_enter(sh, sh.stream)) return e;
+        HIPCHK(hipMemcpyAsync((void*)k.self, &k, sizeof(KParams), hipMemcpyHostToDevice, sh.stream));
+        if (rho_changed) {  // every instance's current rho (scal[2]); the solve refactors with it
+            std::vector<double> r(sh.B, rho);
+            HIPCHK(hipMemcpy2DAsync(k.scal + 2, 4 * sizeof(double), r.data(), sizeof(double), sizeof(double), sh.B,
+                                    hipMemcpyHostToDevice, sh.stream));
+            HIPCHK(hipStreamSynchronize(sh.stream));  // r is a host temporary
+        }
+        if (int e = stream_leave(sh, sh.stream)) return e;
+    }
+    const int interval = h->set.adaptive_rho_interval;
+    h->set = *s;
+    h->set.adaptive_rho_interval = interval;
+    return sync_all(h);
+}
+
 int mpcqp_warm_start_batch(mpcqp_handle* h, const double* x, const double* y) {
     if (!h) return fail(MPCQP_EINVAL, "NULL handle");
     const long n = h->n, m = h->m;

@@ -690,7 +690,9 @@ static hipError_t go(const KParams& p, long B, double* xo, double* yo, int fo, h
 
 // Instantiations: NB = register-resident factor blocks (0: tiles read from the
 // workspace), A = coupling rows of F_k, K = gather-list length, CS / RS = columns /
-// rows per thread, W = waves per SIMD the register budget is sized for, TRI =
+// rows per thread, W = waves per SIMD the register budget is sized for (variants 0, 1, 7
+// were sized for 4 and spilled 47 / 161 / 39 VGPRs at the occupancy of 2 they ran at
+// anyway; sized for 2 they spill 0 / 19 / 0, round 3), TRI =
 // three-phase solve.  variant_fits() is the exact precondition of each.
 bool variant_fits(const KParams& p, int v) {
     const int cs = (p.npad + T - 1) / T, rs = (p.m + T - 1) / T;
@@ -784,14 +786,14 @@ static hipError_t launch_solve_only(const KParams& p, long B, double* xo, double
                                     hipStream_t st, KernelRef* ref = nullptr) {
     const size_t lds = lds_solve_bytes(p);
     switch (p.variant) {
-        case 0: return go<4, 8, 6, 1, 1, 4, true>(p, B, xo, yo, factor_only, st, lds, ref);
-        case 1: return go<8, 8, 8, 1, 1, 4>(p, B, xo, yo, factor_only, st, lds, ref);
+        case 0: return go<4, 8, 6, 1, 1, 2, true>(p, B, xo, yo, factor_only, st, lds, ref);
+        case 1: return go<8, 8, 8, 1, 1, 2>(p, B, xo, yo, factor_only, st, lds, ref);
         case 2: return go<8, 16, 8, 1, 1, 2>(p, B, xo, yo, factor_only, st, lds, ref);
         case 3: return go<8, 16, 8, 1, 2, 2>(p, B, xo, yo, factor_only, st, lds, ref);
         case 4: return go<0, 32, 8, 2, 4, 2>(p, B, xo, yo, factor_only, st, lds, ref);
         case 5: return go<0, 32, 8, 4, 4, 2>(p, B, xo, yo, factor_only, st, lds, ref);
         case 6: return go<0, 32, 16, 8, 8, 1>(p, B, xo, yo, factor_only, st, lds, ref);
-        case 7: return go<4, 8, 6, 1, 1, 4, false>(p, B, xo, yo, factor_only, st, lds, ref);
+        case 7: return go<4, 8, 6, 1, 1, 2, false>(p, B, xo, yo, factor_only, st, lds, ref);
         case 8: case 9: case 10: case 17: case 18: return launch_solve_wave(p, B, xo, yo, factor_only, st, ref);
 #ifdef MPCQP_EXPERIMENTAL
         case 16: return launch_solve_dense(p, B, xo, yo, factor_only, st, ref);

@@ -121,6 +121,7 @@ def lib():
     L.mpcqp_setup_batch.argtypes = [C.c_int32, C.c_int32, i32p, i32p, i32p, i32p, C.c_int64,
                                     dp, dp, dp, dp, dp, _P(_Settings), C.c_uint32, hp]
     L.mpcqp_update_batch.argtypes = [vp, dp, dp, dp]
+    L.mpcqp_update_settings.argtypes = [vp, _P(_Settings)]
     L.mpcqp_update_matrices_batch.argtypes = [vp, dp, i32p, C.c_int32, dp, i32p, C.c_int32]
     L.mpcqp_warm_start_batch.argtypes = [vp, dp, dp]
     L.mpcqp_solve_batch.argtypes = [vp, dp, dp, i32p, i32p]
@@ -175,6 +176,9 @@ def _check(code, what):
 
 _SETTING_NAMES = {f[0] for f in _Settings._fields_}
 _IGNORED = {"linsys_solver", "time_limit", "adaptive_rho_fraction"}
+# osqp-python 0.6 update_settings: what may change after setup (verbose / time_limit: accepted, no effect)
+_UPDATABLE = {"max_iter", "eps_abs", "eps_rel", "eps_prim_inf", "eps_dual_inf", "rho", "alpha", "delta", "polish",
+              "polish_refine_iter", "verbose", "scaled_termination", "check_termination", "warm_start", "time_limit"}
 
 
 def _make_settings(**kw) -> _Settings:
@@ -294,6 +298,7 @@ class OSQPBatch:
         Pp, Pi, Ap, Ai = self._pattern
         s = _make_settings(**settings)
         self._settings = s
+        self._settings_kw = dict(settings)
         h = C.c_void_p()
         _check(lib().mpcqp_setup_batch(n, m, _ip(Pp), _ip(Pi), _ip(Ap), _ip(Ai), B, _dp(Px), _dp(Ax),
                                        _dp(q), _dp(l), _dp(u), C.byref(s), int(device_mask), C.byref(h)),
@@ -365,11 +370,24 @@ class OSQPBatch:
         q = prep(q, n, None); l = prep(l, m, -1); u = prep(u, m, 1)
         _check(lib().mpcqp_update_batch(h, _dp(q), _dp(l), _dp(u)), "update")
 
+    def update_settings(self, **kw):
+        """osqp.OSQP.update_settings (mpcqp_update_settings): max_iter, eps_*, rho, alpha, delta,
+        polish, polish_refine_iter, scaled_termination, check_termination, warm_start."""
+        h = self._need()
+        bad = sorted(set(kw) - _UPDATABLE)
+        if bad:
+            raise ValueError(f"setting(s) {', '.join(bad)} cannot be changed after setup")
+        new = dict(self._settings_kw, **kw)
+        s = _make_settings(**new)
+        _check(lib().mpcqp_update_settings(h, C.byref(s)), "update_settings")
+        self._settings, self._settings_kw = s, new
+
     def warm_start(self, x=None, y=None):
         h = self._need()
         x = None if x is None else np.ascontiguousarray(np.asarray(x, np.float64).reshape(self.B, self.n))
         y = None if y is None else np.ascontiguousarray(np.asarray(y, np.float64).reshape(self.B, self.m))
         _check(lib().mpcqp_warm_start_batch(h, _dp(x), _dp(y)), "warm_start")
+        self._settings_kw["warm_start"] = True  # (osqp_warm_start turns the setting on)
 
     def solve(self):
         h = self._need()
@@ -451,6 +469,11 @@ class OSQP:
                        Px=None if Px is None else np.asarray(Px, np.float64)[None, :], Px_idx=Px_idx,
                        Ax=None if Ax is None else np.asarray(Ax, np.float64)[None, :], Ax_idx=Ax_idx)
         self._update_time = time.perf_counter() - t0
+
+    def update_settings(self, **kwargs):
+        if self._b is None:
+            raise ValueError("Workspace not initialized!")
+        self._b.update_settings(**kwargs)
 
     def warm_start(self, x=None, y=None):
         if self._b is None:

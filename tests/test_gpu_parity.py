@@ -321,12 +321,14 @@ def test_polish_batch_cfg2():
     assert np.all(du[same] < 1e-6), du.max()
 
 
-@pytest.mark.parametrize("variant,cfg,B", [(11, 3, 256), (12, 5, 64), (10, 2, 1024), (17, 2, 1024)])
+@pytest.mark.parametrize("variant,cfg,B", [(11, 3, 256), (12, 5, 64), (10, 2, 1024), (17, 2, 1024), (0, 2, 512),
+                                             (7, 2, 512)])
 def test_alternative_kernel_variants(monkeypatch, variant, cfg, B):
     """Kernel instantiations that are not the default choice for a plan stay exact:
     the 512-thread two-sided kernel on the slack layout (variant 11), the long-horizon
     kernel on cfg 5 (12), the two-wave kernel (10, the default before the four-wave one)
-    and the four-wave kernel (17) on cfg 2, selected with the MPCQP_VARIANT override."""
+    and the four-wave kernel (17) on cfg 2, the 256-thread register-factor kernels with the
+    three-phase (0) and the sweep (7) solve on cfg 2, selected with the MPCQP_VARIANT override."""
     monkeypatch.setenv("MPCQP_VARIANT", str(variant))
     b = mpc.make_batch(cfg, B=B)
     settings = dict(warm_start=True) if cfg == 3 else dict(polish=False, warm_start=False)
@@ -976,3 +978,64 @@ def test_nonconvex_setup_raises_like_osqp():
     assert (h.solve().status_val == 1).all()
     with pytest.raises(ValueError, match="instance 37"):
         h.update(Px=Px)
+
+
+def test_update_settings_match_oracle():
+    """update_settings (mpcqp_update_settings, osqp_update_settings / osqp_update_rho): on a
+    cfg-2 batch solved once, then tighter tolerances, a new rho (refactored, row classes
+    kept), alpha, max_iter and check interval, solved warm; then warm starting off, solved
+    cold -- each against the oracle doing the same calls.  Settings OSQP fixes at setup are
+    refused by both."""
+    b = mpc.make_batch(2, B=64, seed=21)
+    s = dict(warm_start=True)
+    P, A = b["P"], b["A"]
+    dev = OSQPBatch()
+    dev.setup(P, b["q"], A, b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
+    orc = []
+    for k in range(b["Px"].shape[0]):
+        o = pyoracle.OSQP()
+        Pk, Ak = P.copy(), A.copy()
+        Pk.data, Ak.data = b["Px"][k].copy(), b["Ax"][k].copy()
+        o.setup(Pk, b["q"][k], Ak, b["l"][k], b["u"][k], **s)
+        orc.append(o)
+    for step, kw in enumerate([{}, dict(eps_abs=1e-5, eps_rel=1e-5, rho=0.5, alpha=1.4, max_iter=3000,
+                                        check_termination=10),
+                               dict(warm_start=False)]):
+        if kw:
+            dev.update_settings(**kw)
+            for o in orc:
+                o.update_settings(**kw)
+        rd = dev.solve()
+        ro = [o.solve() for o in orc]
+        st = np.array([r.info.status_val for r in ro])
+        it = np.array([r.info.iter for r in ro])
+        assert np.mean(rd.status_val == st) >= 0.99, step
+        assert np.mean(rd.iter == it) >= 0.99, step
+        same = rd.iter == it
+        du = np.array([np.abs(rd.x[k, b["u_block"]] - ro[k].x[b["u_block"]]).max() for k in range(len(ro))])
+        assert np.all(du[same] < U_TOL), (step, du[same].max())
+        if step == 1:  # every 10 iterations now
+            assert np.all(rd.iter % 10 == 0)
+    with pytest.raises(ValueError):
+        dev.update_settings(sigma=1e-5)
+    with pytest.raises(ValueError):
+        orc[0].update_settings(sigma=1e-5)
+
+
+def test_shim_update_settings_polish_demo():
+    """osqp.OSQP().update_settings(polish=True, eps_abs=, eps_rel=) through the shim on the
+    osqp documentation's demo problem: polished like the oracle, the closed-form optimum."""
+    import scipy.sparse as sps
+    P = sps.csc_matrix(np.array([[4.0, 1.0], [1.0, 2.0]]))
+    A = sps.csc_matrix(np.array([[1.0, 1.0], [1.0, 0.0], [0.0, 1.0]]))
+    q, l, u = np.array([1.0, 1.0]), np.array([1.0, 0.0, 0.0]), np.array([1.0, 0.7, 0.7])
+    g, o = OSQP(), pyoracle.OSQP()
+    g.setup(P, q, A, l, u, verbose=False)
+    o.setup(P, q, A, l, u)
+    g.solve(); o.solve()
+    g.update_settings(polish=True, eps_abs=1e-4, eps_rel=1e-4)
+    o.update_settings(polish=True, eps_abs=1e-4, eps_rel=1e-4)
+    rg, ro = g.solve(), o.solve()
+    assert rg.info.iter == ro.info.iter and rg.info.status_polish == ro.info.status_polish == 1
+    assert np.abs(rg.x - np.array([0.3, 0.7])).max() < 1e-9
+    assert np.abs(rg.x - ro.x).max() < 1e-12

@@ -263,3 +263,25 @@ def test_oracle_matrix_update_keeps_the_iterates():
     assert r1.info.status == "solved"
     assert r1.info.iter < r0.info.iter
     assert np.abs(r1.x - r0.x).max() < 1e-6
+
+
+def test_oracle_update_settings_equals_fresh_setup():
+    """orc_update_settings: rho through osqp_update_rho (row classes kept, KKT refactored),
+    tolerances, alpha and the check interval; a cold solve afterwards equals a fresh setup
+    with those settings (same iterations, x to rounding).  sigma is fixed at setup."""
+    P, q, A, l, u, *_ = osqp_demo_problem()
+    base = dict(warm_start=False, adaptive_rho=False)
+    new = dict(rho=0.7, eps_abs=1e-7, eps_rel=1e-7, alpha=1.3, check_termination=5, max_iter=2000)
+    o = pyoracle.OSQP()
+    o.setup(P, q, A, l, u, **base)
+    o.solve()
+    o.update_settings(**new)
+    r = o.solve()
+    f = pyoracle.OSQP()
+    f.setup(P, q, A, l, u, **base, **new)
+    rf = f.solve()
+    assert r.info.status == rf.info.status == "solved"
+    assert r.info.iter == rf.info.iter and r.info.iter % 5 == 0
+    assert np.abs(r.x - rf.x).max() < 1e-13
+    with pytest.raises(ValueError):
+        o.update_settings(sigma=1e-4)
