@@ -144,13 +144,14 @@ int mpcqp_update_matrices_batch(mpcqp_handle *h, const double *Px, const int32_t
 /* x, y may each be NULL (keeps the current iterate of that part). */
 int mpcqp_warm_start_batch(mpcqp_handle *h, const double *x, const double *y);
 /* osqp_update_settings / osqp_update_rho (OSQP 0.6; osqp-python's update_settings): max_iter,
- * eps_abs, eps_rel, eps_prim_inf, eps_dual_inf, rho (clipped to [1e-6, 1e6], every instance,
- * refactored at the next solve), alpha, delta, polish, polish_refine_iter, scaled_termination,
+ * eps_abs, eps_rel, eps_prim_inf, eps_dual_inf, rho (with set_rho != 0 only, as osqp-python
+ * calls update_rho only when rho is passed: clipped to [1e-6, 1e6], every instance, refactored
+ * at the next solve; else each instance keeps the rho its solves adapted to), alpha, delta, polish, polish_refine_iter, scaled_termination,
  * check_termination, warm_start take the new values; sigma, scaling and the adaptive-rho
  * settings must be unchanged (MPCQP_EINVAL otherwise), as OSQP fixes them at setup.  Any
  * handle.  polish = 1 on a handle whose plan eliminated variables (the slack layouts set up
  * without polish) is MPCQP_EUNSUPPORTED. */
-int mpcqp_update_settings(mpcqp_handle *h, const mpcqp_settings *s);
+int mpcqp_update_settings(mpcqp_handle *h, const mpcqp_settings *s, int32_t set_rho);
 /* any output may be NULL */
 int mpcqp_solve_batch(mpcqp_handle *h, double *x, double *y, int32_t *status, int32_t *iters);
 /* info of the last solve; any output may be NULL */

@@ -676,10 +676,12 @@ int orc_update_P_A(orc_work *w, const double *Px, const int *Px_idx, int nP, con
 /* osqp_update_settings as osqp-python 0.6 exposes it (update_max_iter, update_eps_abs, ...,
  * update_rho): the settings OSQP lets change after setup are copied; rho goes through
  * osqp_update_rho (clipped, rho vector by row class, KKT refactored).  sigma, scaling and
- * the adaptive-rho settings are fixed at setup: a different value is a validation error. */
+ * the adaptive-rho settings are fixed at setup: a different value is a validation error.
+ * set_rho: only when the caller passes rho (osqp-python calls update_rho only then), so the
+ * rho a previous solve adapted to stays otherwise. */
 static int osqp_update_rho(orc_work *w, double rho_new);
 
-int orc_update_settings(orc_work *w, const orc_settings *s) {
+int orc_update_settings(orc_work *w, const orc_settings *s, int set_rho) {
     const orc_settings *o = &w->set;
     if (s->sigma != o->sigma || s->scaling != o->scaling || s->adaptive_rho != o->adaptive_rho ||
         s->adaptive_rho_tolerance != o->adaptive_rho_tolerance ||
@@ -690,7 +692,6 @@ int orc_update_settings(orc_work *w, const orc_settings *s) {
         s->check_termination < 0 || s->rho <= 0 || s->delta <= 0 || s->polish_refine_iter < 0)
         return ORC_SETTINGS_VALIDATION_ERROR;
     const double rho = s->rho;
-    const int rho_changed = rho != o->rho;
     w->set.max_iter = s->max_iter;
     w->set.eps_abs = s->eps_abs;
     w->set.eps_rel = s->eps_rel;
@@ -703,7 +704,7 @@ int orc_update_settings(orc_work *w, const orc_settings *s) {
     w->set.scaled_termination = s->scaled_termination;
     w->set.check_termination = s->check_termination;
     w->set.warm_start = s->warm_start;
-    if (rho_changed && osqp_update_rho(w, rho)) return ORC_NONCVX_ERROR;
+    if (set_rho && osqp_update_rho(w, rho)) return ORC_NONCVX_ERROR;
     return 0;
 }
 

@@ -92,7 +92,7 @@ int orc_update_upper_bound(orc_work *w, const double *u);
 int orc_update_P_A(orc_work *w, const double *Px, const int *Px_idx, int nP, const double *Ax,
                    const int *Ax_idx, int nA);
 /* osqp_update_settings (the settings OSQP lets change after setup; rho via osqp_update_rho) */
-int orc_update_settings(orc_work *w, const orc_settings *s);
+int orc_update_settings(orc_work *w, const orc_settings *s, int set_rho);
 int orc_warm_start(orc_work *w, const double *x, const double *y);
 int orc_solve(orc_work *w);
 /* x (n), y (m); certificates may be NULL */

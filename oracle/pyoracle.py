@@ -80,7 +80,7 @@ def lib():
         for name in ("orc_update_lin_cost", "orc_update_lower_bound", "orc_update_upper_bound"):
             getattr(L, name).argtypes = [C.c_void_p, P(C.c_double)]
         L.orc_update_bounds.argtypes = [C.c_void_p, P(C.c_double), P(C.c_double)]
-        L.orc_update_settings.argtypes = [C.c_void_p, P(_Settings)]
+        L.orc_update_settings.argtypes = [C.c_void_p, P(_Settings), C.c_int]
         L.orc_update_P_A.argtypes = [C.c_void_p, P(C.c_double), P(C.c_int), C.c_int,
                                      P(C.c_double), P(C.c_int), C.c_int]
         L.orc_warm_start.argtypes = [C.c_void_p, P(C.c_double), P(C.c_double)]
@@ -201,7 +201,7 @@ class OSQP:
         """osqp.OSQP.update_settings: the settings OSQP lets change after setup"""
         new = dict(self._settings, **kw)
         s = make_settings(**new)
-        e = lib().orc_update_settings(self._w, C.byref(s))
+        e = lib().orc_update_settings(self._w, C.byref(s), int("rho" in kw))
         if e:
             raise ValueError(f"oracle update_settings failed (code {e})")
         self._settings = new

@@ -592,7 +592,7 @@ int mpcqp_update_matrices_batch(mpcqp_handle* h, const double* Px, const int32_t
     return check_convex(h);  // osqp_update_P_A refactors at once and reports a failed factorisation
 }
 
-int mpcqp_update_settings(mpcqp_handle* h, const mpcqp_settings* s) {
+int mpcqp_update_settings(mpcqp_handle* h, const mpcqp_settings* s, int32_t set_rho) {
     if (!h || !s) return fail(MPCQP_EINVAL, "NULL argument");
     const mpcqp_settings& o = h->set;
     if (s->sigma != o.sigma || s->scaling != o.scaling || s->adaptive_rho != o.adaptive_rho ||
@@ -603,7 +603,7 @@ int mpcqp_update_settings(mpcqp_handle* h, const mpcqp_settings* s) {
     if (s->polish && h->plan.ne > 0)
         return fail(MPCQP_EUNSUPPORTED, "polish needs the full factor: this layout's handle eliminated %d variables; "
                                         "run setup with polish on", h->plan.ne);
-    const bool rho_changed = s->rho != o.rho;
+    const bool rho_changed = set_rho != 0;
     const double rho = std::min(std::max(s->rho, 1e-6), 1e6);  // osqp_update_rho: RHO_MIN / RHO_MAX
     for (auto& sh : h->shards) {
         KParams& k = sh.kp;

@@ -121,7 +121,7 @@ def lib():
     L.mpcqp_setup_batch.argtypes = [C.c_int32, C.c_int32, i32p, i32p, i32p, i32p, C.c_int64,
                                     dp, dp, dp, dp, dp, _P(_Settings), C.c_uint32, hp]
     L.mpcqp_update_batch.argtypes = [vp, dp, dp, dp]
-    L.mpcqp_update_settings.argtypes = [vp, _P(_Settings)]
+    L.mpcqp_update_settings.argtypes = [vp, _P(_Settings), C.c_int32]
     L.mpcqp_update_matrices_batch.argtypes = [vp, dp, i32p, C.c_int32, dp, i32p, C.c_int32]
     L.mpcqp_warm_start_batch.argtypes = [vp, dp, dp]
     L.mpcqp_solve_batch.argtypes = [vp, dp, dp, i32p, i32p]
@@ -379,7 +379,7 @@ class OSQPBatch:
             raise ValueError(f"setting(s) {', '.join(bad)} cannot be changed after setup")
         new = dict(self._settings_kw, **kw)
         s = _make_settings(**new)
-        _check(lib().mpcqp_update_settings(h, C.byref(s)), "update_settings")
+        _check(lib().mpcqp_update_settings(h, C.byref(s), int("rho" in kw)), "update_settings")
         self._settings, self._settings_kw = s, new
 
     def warm_start(self, x=None, y=None):

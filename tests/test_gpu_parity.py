@@ -998,9 +998,8 @@ def test_update_settings_match_oracle():
         Pk.data, Ak.data = b["Px"][k].copy(), b["Ax"][k].copy()
         o.setup(Pk, b["q"][k], Ak, b["l"][k], b["u"][k], **s)
         orc.append(o)
-    # (eps 1e-4: at 1e-5 the cold solves run ~3x longer and 2 of 64 stop one check interval
-    # apart from the oracle's -- the reduced-vs-quasi-definite linear-solver difference of
-    # DESIGN.md §3 -- which is not what this test is about)
+    # (the third call passes no rho: each instance keeps the rho its previous solve adapted to,
+    # on the device and in the oracle, as osqp-python calls update_rho only when rho is given)
     for step, kw in enumerate([{}, dict(eps_abs=1e-4, eps_rel=1e-4, rho=0.5, alpha=1.4, max_iter=3000,
                                         check_termination=10),
                                dict(warm_start=False)]):
