@@ -451,6 +451,8 @@ def main(argv=None, solver_cls=None, device=None):
     solver.synchronize()
     status = dst.cpu().numpy()
     iters = dit.cpu().numpy()
+    # the base batch's control block, for the CPU baseline's parity figure (rank 0, N = 1)
+    u_base = dx[:, b["u_block"]].cpu().numpy() if (rank == 0 and world == 1 and not args.no_cpu) else None
     for t in range(1, 1 + args.warmup):
         step(t)
     solver.synchronize()
@@ -603,7 +605,10 @@ def main(argv=None, solver_cls=None, device=None):
                "setup_thread_s": round(t_setup, 3), "solve_thread_s": round(t_solve, 3),
                "value_solve_only": done / tc * (t_setup + t_solve) / t_solve if t_solve > 0 else None,
                "status_match_gpu": float(np.mean(rc.status_val == status[:nc])),
-               "iter_match_gpu": float(np.mean(rc.iter == iters[:nc]))}
+               "iter_match_gpu": float(np.mean(rc.iter == iters[:nc])),
+               # north-star tolerance ||u* - u*_ref||_inf < 1e-4: the largest difference over
+               # the sampled instances' control blocks (GPU base-batch solve vs the oracle's)
+               "parity_max_du": float(np.nanmax(np.abs(u_base[:nc] - rc.x[:, b["u_block"]])))}
 
     if rank == 0:
         kname = solve_kernel_name(info, fused=fused)
