@@ -449,10 +449,11 @@ def main(argv=None, solver_cls=None, device=None):
 
     step(0)  # the base batch: its statuses / iterations are the ones the CPU baseline is compared with
     solver.synchronize()
-    status = dst.cpu().numpy()
-    iters = dit.cpu().numpy()
+    # (copies: on a CPU device .cpu() would alias the buffers the later steps overwrite)
+    status = dst.cpu().numpy().copy()
+    iters = dit.cpu().numpy().copy()
     # the base batch's control block, for the CPU baseline's parity figure (rank 0, N = 1)
-    u_base = dx[:, b["u_block"]].cpu().numpy() if (rank == 0 and world == 1 and not args.no_cpu) else None
+    u_base = dx[:, b["u_block"]].cpu().numpy().copy() if (rank == 0 and world == 1 and not args.no_cpu) else None
     for t in range(1, 1 + args.warmup):
         step(t)
     solver.synchronize()

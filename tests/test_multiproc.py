@@ -107,3 +107,21 @@ def test_cfg4_shards_tile_one_global_batch(monkeypatch):
             assert np.array_equal(np.concatenate([p[k] for p in parts]), full[k])
     with pytest.raises(SystemExit):
         bench.make_shard(4, 60, 2, 0)
+
+
+def test_bench_main_one_rank_cpu_baseline(tmp_path):
+    """`bench.py` at N = 1 on CPU with the oracle stand-in: the cpu_baseline object -- the
+    oracle timed on a bounded sample, its statuses / iterations / control blocks against the
+    base-batch solve (parity_max_du; exactly 0 here, the stand-in being the oracle)."""
+    out = tmp_path / "line.json"
+    with open(out, "w") as f:
+        rc = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "bench_rank_cpu.py"), "--config", "2",
+                             "--batch", "16", "--steps", "2", "--warmup", "1", "--no-dispatch-ab",
+                             "--cpu-seconds", "0.2"], stdout=f, timeout=240,
+                            env=dict(os.environ, OMP_NUM_THREADS="2")).returncode
+    assert rc == 0
+    d = json.loads([ln for ln in open(out).read().splitlines() if ln.startswith("{")][-1])
+    cb = d["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
+    assert cb["status_match_gpu"] == 1.0 and cb["iter_match_gpu"] == 1.0
+    assert cb["parity_max_du"] == 0.0
