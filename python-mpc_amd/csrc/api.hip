@@ -598,8 +598,7 @@ int mpcqp_update_settings(mpcqp_handle* h, const mpcqp_settings* s, int32_t set_
     if (s->sigma != o.sigma || s->scaling != o.scaling || s->adaptive_rho != o.adaptive_rho ||
         s->adaptive_rho_tolerance != o.adaptive_rho_tolerance || s->adaptive_rho_interval != o.adaptive_rho_interval)
         return fail(MPCQP_EINVAL, "sigma, scaling and the adaptive-rho settings cannot be changed after setup");
-    if (int e = validate_settings(*s)) return e;
-    if (s->polish && !(s->delta > 0 && s->polish_refine_iter >= 0)) return fail(MPCQP_EINVAL, "invalid polish settings");
+    if (int e = validate_settings(*s)) return e;  // (polish's delta / refinement steps included)
     if (s->polish && h->plan.ne > 0)
         return fail(MPCQP_EUNSUPPORTED, "polish needs the full factor: this layout's handle eliminated %d variables; "
                                         "run setup with polish on", h->plan.ne);
