@@ -75,6 +75,11 @@ struct Shard {
     void* dio = nullptr;    // staging for the host-pointer API
     double *in_Px = nullptr, *in_Ax = nullptr, *in_q = nullptr, *in_l = nullptr, *in_u = nullptr;
     double *out_x = nullptr, *out_y = nullptr;
+    // host-pointer API, small shards: pinned staging of everything a solve returns (x, y, the
+    // info, the certificates, the statuses), filled by mpcqp_solve_batch with one
+    // synchronisation; the info / certificate / polish getters then read it (mpcqp_handle::staged)
+    char* hstage = nullptr;
+    char* hin = nullptr;  // ... and of update()'s q, l, u and the error flags it reads back
     KParams kp{};
 };
 
@@ -92,6 +97,7 @@ struct mpcqp_handle {
     bool collect_setup = false;  // ... and around device setup launches
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_setup, ev_solve;
     std::pair<hipEvent_t, hipEvent_t> last_pair{nullptr, nullptr};  // events of the last device solve
+    bool staged = false;  // every shard's hstage holds the last mpcqp_solve_batch's results
 };
 
 namespace {
@@ -393,6 +399,29 @@ int check_err_flags(mpcqp_handle* h) {
     return 0;
 }
 
+// The staging layout of one shard (Bs instances): x (Bs n), y (Bs m), obj, pri, dua, rho_est
+// (Bs each), the certificates dxc (Bs n) and dyc (Bs m) as doubles, then status, iter,
+// rho_upd, pstat (Bs each) as ints.  Shards past kStageMax bytes copy straight into the
+// caller's buffers as before (the large throughput batches, where the copies dominate).
+constexpr size_t kStageMax = 16u << 20;
+size_t stage_bytes(const mpcqp_handle* h, long Bs) {
+    return sizeof(double) * (size_t)Bs * (2 * (size_t)h->n + 2 * (size_t)h->m + 4) + sizeof(int) * 4 * (size_t)Bs;
+}
+struct Stage {
+    double *x, *y, *obj, *pri, *dua, *rho_est, *dxc, *dyc;
+    int *status, *iter, *rho_upd, *pstat;
+};
+Stage stage_of(const mpcqp_handle* h, const Shard& s) {
+    Stage g;
+    double* d = (double*)s.hstage;
+    const long Bs = s.B, n = h->n, m = h->m;
+    g.x = d; g.y = g.x + Bs * n; g.obj = g.y + Bs * m; g.pri = g.obj + Bs; g.dua = g.pri + Bs;
+    g.rho_est = g.dua + Bs; g.dxc = g.rho_est + Bs; g.dyc = g.dxc + Bs * n;
+    int* q = (int*)(g.dyc + Bs * m);
+    g.status = q; g.iter = q + Bs; g.rho_upd = q + 2 * Bs; g.pstat = q + 3 * Bs;
+    return g;
+}
+
 // osqp_setup's convexity test (OSQP 0.6 init_linsys_solver: the quasi-definite KKT matrix
 // must have n positive pivots, which holds iff P + sigma I + A' diag(rho) A is positive
 // definite -- the reduced matrix the solve kernels factor): one factor-only launch of the
@@ -497,26 +526,65 @@ int mpcqp_setup_batch(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi
 
 int mpcqp_update_batch(mpcqp_handle* h, const double* q, const double* l, const double* u) {
     if (!h) return fail(MPCQP_EINVAL, "NULL handle");
+    h->staged = false;  // (device work: the staged results of the last solve are stale)
     if (l && u)
         if (int e = check_bounds_host(h, l, u, h->B)) return e;
     const long n = h->n, m = h->m;
+    // small shards go through pinned staging: the copies and the error flags' read-back are
+    // asynchronous and the call synchronises once (osqp's per-step update of one problem)
+    auto in_bytes = [&](long Bs) { return sizeof(double) * (size_t)Bs * (n + 2 * m) + sizeof(int) * (size_t)Bs; };
     for (auto& s : h->shards) {
         HIPCHK(hipSetDevice(s.dev));
         if (int e = stream_enter(s, s.stream)) return e;
-        if (q) HIPCHK(hipMemcpyAsync(s.in_q, q + s.b0 * n, sizeof(double) * s.B * n, hipMemcpyHostToDevice, s.stream));
-        if (l) HIPCHK(hipMemcpyAsync(s.in_l, l + s.b0 * m, sizeof(double) * s.B * m, hipMemcpyHostToDevice, s.stream));
-        if (u) HIPCHK(hipMemcpyAsync(s.in_u, u + s.b0 * m, sizeof(double) * s.B * m, hipMemcpyHostToDevice, s.stream));
-        HIPCHK(launch_update(s.kp, s.B, q ? s.in_q : nullptr, l ? s.in_l : nullptr, u ? s.in_u : nullptr, s.stream));
+        const long Bs = s.B;
+        if (in_bytes(Bs) <= kStageMax) {
+            if (!s.hin) HIPCHK(hipHostMalloc((void**)&s.hin, in_bytes(Bs), hipHostMallocDefault));
+            double *hq = (double*)s.hin, *hl = hq + Bs * n, *hu = hl + Bs * m;
+            int* herr = (int*)(hu + Bs * m);
+            if (q) {
+                std::copy(q + s.b0 * n, q + (s.b0 + Bs) * n, hq);
+                HIPCHK(hipMemcpyAsync(s.in_q, hq, sizeof(double) * Bs * n, hipMemcpyHostToDevice, s.stream));
+            }
+            if (l) {
+                std::copy(l + s.b0 * m, l + (s.b0 + Bs) * m, hl);
+                HIPCHK(hipMemcpyAsync(s.in_l, hl, sizeof(double) * Bs * m, hipMemcpyHostToDevice, s.stream));
+            }
+            if (u) {
+                std::copy(u + s.b0 * m, u + (s.b0 + Bs) * m, hu);
+                HIPCHK(hipMemcpyAsync(s.in_u, hu, sizeof(double) * Bs * m, hipMemcpyHostToDevice, s.stream));
+            }
+            HIPCHK(launch_update(s.kp, Bs, q ? s.in_q : nullptr, l ? s.in_l : nullptr, u ? s.in_u : nullptr, s.stream));
+            if (l || u) HIPCHK(hipMemcpyAsync(herr, s.kp.err, sizeof(int) * Bs, hipMemcpyDeviceToHost, s.stream));
+        } else {
+            if (q) HIPCHK(hipMemcpyAsync(s.in_q, q + s.b0 * n, sizeof(double) * Bs * n, hipMemcpyHostToDevice, s.stream));
+            if (l) HIPCHK(hipMemcpyAsync(s.in_l, l + s.b0 * m, sizeof(double) * Bs * m, hipMemcpyHostToDevice, s.stream));
+            if (u) HIPCHK(hipMemcpyAsync(s.in_u, u + s.b0 * m, sizeof(double) * Bs * m, hipMemcpyHostToDevice, s.stream));
+            HIPCHK(launch_update(s.kp, Bs, q ? s.in_q : nullptr, l ? s.in_l : nullptr, u ? s.in_u : nullptr, s.stream));
+        }
         if (int e = stream_leave(s, s.stream)) return e;
     }
     if (int e = sync_all(h)) return e;
-    if (l || u) return check_err_flags(h);
+    if (!(l || u)) return 0;
+    for (auto& s : h->shards) {
+        if (in_bytes(s.B) > kStageMax) {
+            std::vector<int> err(s.B);
+            HIPCHK(hipSetDevice(s.dev));
+            HIPCHK(hipMemcpy(err.data(), s.kp.err, sizeof(int) * s.B, hipMemcpyDeviceToHost));
+            for (long i = 0; i < s.B; ++i)
+                if (err[i]) return fail(MPCQP_EINVAL, "instance %ld: invalid data (l > u or NaN bounds)", s.b0 + i);
+        } else {
+            const int* herr = (const int*)((const double*)s.hin + s.B * (n + 2 * m));
+            for (long i = 0; i < s.B; ++i)
+                if (herr[i]) return fail(MPCQP_EINVAL, "instance %ld: invalid data (l > u or NaN bounds)", s.b0 + i);
+        }
+    }
     return 0;
 }
 
 int mpcqp_update_matrices_batch(mpcqp_handle* h, const double* Px, const int32_t* Px_idx, int32_t nPx,
                                 const double* Ax, const int32_t* Ax_idx, int32_t nAx) {
     if (!h) return fail(MPCQP_EINVAL, "NULL handle");
+    h->staged = false;  // (device work: the staged results of the last solve are stale)
     if (!Px && !Ax) return fail(MPCQP_EINVAL, "no matrix values given");
     const Plan& pl = h->plan;
     // the columns of the value arrays that are written: all, or per index its last
@@ -594,6 +662,7 @@ int mpcqp_update_matrices_batch(mpcqp_handle* h, const double* Px, const int32_t
 
 int mpcqp_update_settings(mpcqp_handle* h, const mpcqp_settings* s, int32_t set_rho) {
     if (!h || !s) return fail(MPCQP_EINVAL, "NULL argument");
+    h->staged = false;  // (device work: the staged results of the last solve are stale)
     const mpcqp_settings& o = h->set;
     if (s->sigma != o.sigma || s->scaling != o.scaling || s->adaptive_rho != o.adaptive_rho ||
         s->adaptive_rho_tolerance != o.adaptive_rho_tolerance || s->adaptive_rho_interval != o.adaptive_rho_interval)
@@ -632,6 +701,7 @@ int mpcqp_update_settings(mpcqp_handle* h, const mpcqp_settings* s, int32_t set_
 
 int mpcqp_warm_start_batch(mpcqp_handle* h, const double* x, const double* y) {
     if (!h) return fail(MPCQP_EINVAL, "NULL handle");
+    h->staged = false;  // (device work: the staged results of the last solve are stale)
     const long n = h->n, m = h->m;
     for (auto& s : h->shards) {
         HIPCHK(hipSetDevice(s.dev));
@@ -661,15 +731,55 @@ int mpcqp_solve_batch(mpcqp_handle* h, double* x, double* y, int32_t* status, in
         HIPCHK(launch_order(s.kp, s.B, s.stream));
         if (int e = stream_leave(s, s.stream)) return e;
     }
-    // the host-side gather: each shard's slice of the caller's buffers, in shard order
+    // the host-side gather: each shard's slice of the caller's buffers, in shard order; a
+    // small shard stages everything its solve returns in pinned memory (one synchronisation
+    // for the solve and the getters that follow it, instead of one per array)
+    bool all_staged = true;
     for (auto& s : h->shards) {
         HIPCHK(hipSetDevice(s.dev));
-        if (x) HIPCHK(hipMemcpyAsync(x + s.b0 * n, s.out_x, sizeof(double) * s.B * n, hipMemcpyDeviceToHost, s.stream));
-        if (y) HIPCHK(hipMemcpyAsync(y + s.b0 * m, s.out_y, sizeof(double) * s.B * m, hipMemcpyDeviceToHost, s.stream));
-        if (status) HIPCHK(hipMemcpyAsync(status + s.b0, s.kp.status, sizeof(int) * s.B, hipMemcpyDeviceToHost, s.stream));
-        if (iters) HIPCHK(hipMemcpyAsync(iters + s.b0, s.kp.iter, sizeof(int) * s.B, hipMemcpyDeviceToHost, s.stream));
+        const size_t sb = stage_bytes(h, s.B);
+        if (sb <= kStageMax) {
+            if (!s.hstage) HIPCHK(hipHostMalloc((void**)&s.hstage, sb, hipHostMallocDefault));
+            const Stage g = stage_of(h, s);
+            const long Bs = s.B;
+            auto cp = [&](void* dst, const void* src, size_t bytes) -> int {
+                HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s.stream));
+                return 0;
+            };
+            if (int e = cp(g.x, s.out_x, sizeof(double) * Bs * n)) return e;
+            if (int e = cp(g.y, s.out_y, sizeof(double) * Bs * m)) return e;
+            if (int e = cp(g.obj, s.kp.obj, sizeof(double) * Bs)) return e;
+            if (int e = cp(g.pri, s.kp.pri, sizeof(double) * Bs)) return e;
+            if (int e = cp(g.dua, s.kp.dua, sizeof(double) * Bs)) return e;
+            if (int e = cp(g.rho_est, s.kp.rho_est, sizeof(double) * Bs)) return e;
+            if (int e = cp(g.dxc, s.kp.dxc, sizeof(double) * Bs * n)) return e;
+            if (int e = cp(g.dyc, s.kp.dyc, sizeof(double) * Bs * m)) return e;
+            if (int e = cp(g.status, s.kp.status, sizeof(int) * Bs)) return e;
+            if (int e = cp(g.iter, s.kp.iter, sizeof(int) * Bs)) return e;
+            if (int e = cp(g.rho_upd, s.kp.rho_upd, sizeof(int) * Bs)) return e;
+            if (h->set.polish) {
+                if (int e = cp(g.pstat, s.kp.pstat, sizeof(int) * Bs)) return e;
+            } else {
+                std::fill(g.pstat, g.pstat + Bs, 0);
+            }
+        } else {
+            all_staged = false;
+            if (x) HIPCHK(hipMemcpyAsync(x + s.b0 * n, s.out_x, sizeof(double) * s.B * n, hipMemcpyDeviceToHost, s.stream));
+            if (y) HIPCHK(hipMemcpyAsync(y + s.b0 * m, s.out_y, sizeof(double) * s.B * m, hipMemcpyDeviceToHost, s.stream));
+            if (status) HIPCHK(hipMemcpyAsync(status + s.b0, s.kp.status, sizeof(int) * s.B, hipMemcpyDeviceToHost, s.stream));
+            if (iters) HIPCHK(hipMemcpyAsync(iters + s.b0, s.kp.iter, sizeof(int) * s.B, hipMemcpyDeviceToHost, s.stream));
+        }
     }
     if (int e = sync_all(h)) return e;
+    for (auto& s : h->shards) {
+        if (stage_bytes(h, s.B) > kStageMax) continue;
+        const Stage g = stage_of(h, s);
+        if (x) std::copy(g.x, g.x + s.B * n, x + s.b0 * n);
+        if (y) std::copy(g.y, g.y + s.B * m, y + s.b0 * m);
+        if (status) std::copy(g.status, g.status + s.B, status + s.b0);
+        if (iters) std::copy(g.iter, g.iter + s.B, iters + s.b0);
+    }
+    h->staged = all_staged;
     float ms = 0.f;
     h->last_ms = -1.0;
     if (h->shards.size() == 1 && hipEventElapsedTime(&ms, h->shards[0].ev0, h->shards[0].ev1) == hipSuccess) {
@@ -682,6 +792,17 @@ int mpcqp_solve_batch(mpcqp_handle* h, double* x, double* y, int32_t* status, in
 int mpcqp_get_info_batch(mpcqp_handle* h, double* obj_val, double* pri_res, double* dua_res,
                          double* rho_estimate, int32_t* rho_updates) {
     if (!h) return fail(MPCQP_EINVAL, "NULL handle");
+    if (h->staged) {
+        for (auto& s : h->shards) {
+            const Stage g = stage_of(h, s);
+            if (obj_val) std::copy(g.obj, g.obj + s.B, obj_val + s.b0);
+            if (pri_res) std::copy(g.pri, g.pri + s.B, pri_res + s.b0);
+            if (dua_res) std::copy(g.dua, g.dua + s.B, dua_res + s.b0);
+            if (rho_estimate) std::copy(g.rho_est, g.rho_est + s.B, rho_estimate + s.b0);
+            if (rho_updates) std::copy(g.rho_upd, g.rho_upd + s.B, rho_updates + s.b0);
+        }
+        return 0;
+    }
     for (auto& s : h->shards) {
         HIPCHK(hipSetDevice(s.dev));
         if (obj_val) HIPCHK(hipMemcpy(obj_val + s.b0, s.kp.obj, sizeof(double) * s.B, hipMemcpyDeviceToHost));
@@ -695,6 +816,13 @@ int mpcqp_get_info_batch(mpcqp_handle* h, double* obj_val, double* pri_res, doub
 
 int mpcqp_get_polish_status(mpcqp_handle* h, int32_t* status_polish) {
     if (!h || !status_polish) return fail(MPCQP_EINVAL, "NULL argument");
+    if (h->staged) {
+        for (auto& s : h->shards) {
+            const Stage g = stage_of(h, s);
+            std::copy(g.pstat, g.pstat + s.B, status_polish + s.b0);
+        }
+        return 0;
+    }
     for (auto& s : h->shards) {
         HIPCHK(hipSetDevice(s.dev));
         if (h->set.polish)
@@ -707,6 +835,14 @@ int mpcqp_get_polish_status(mpcqp_handle* h, int32_t* status_polish) {
 
 int mpcqp_get_certificates(mpcqp_handle* h, double* prim_inf_cert, double* dual_inf_cert) {
     if (!h) return fail(MPCQP_EINVAL, "NULL handle");
+    if (h->staged) {
+        for (auto& s : h->shards) {
+            const Stage g = stage_of(h, s);
+            if (prim_inf_cert) std::copy(g.dyc, g.dyc + s.B * h->m, prim_inf_cert + s.b0 * h->m);
+            if (dual_inf_cert) std::copy(g.dxc, g.dxc + s.B * h->n, dual_inf_cert + s.b0 * h->n);
+        }
+        return 0;
+    }
     for (auto& s : h->shards) {
         HIPCHK(hipSetDevice(s.dev));
         if (prim_inf_cert)
@@ -745,6 +881,7 @@ static int ev_end(bool on, std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, hi
 int mpcqp_setup_device(mpcqp_handle* h, const double* dPx, const double* dAx, const double* dq,
                        const double* dl, const double* du, void* stream) {
     if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "device entry points need a single-device handle");
+    h->staged = false;  // (device work: the staged results of the last solve are stale)
     Shard& s = h->shards[0];
     hipStream_t st = pick(s, stream);
     HIPCHK(hipSetDevice(s.dev));
@@ -759,6 +896,7 @@ int mpcqp_setup_device(mpcqp_handle* h, const double* dPx, const double* dAx, co
 
 int mpcqp_update_device(mpcqp_handle* h, const double* dq, const double* dl, const double* du, void* stream) {
     if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "device entry points need a single-device handle");
+    h->staged = false;  // (device work: the staged results of the last solve are stale)
     Shard& s = h->shards[0];
     hipStream_t st = pick(s, stream);
     HIPCHK(hipSetDevice(s.dev));
@@ -769,6 +907,7 @@ int mpcqp_update_device(mpcqp_handle* h, const double* dq, const double* dl, con
 
 int mpcqp_warm_start_device(mpcqp_handle* h, const double* dx, const double* dy, void* stream) {
     if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "device entry points need a single-device handle");
+    h->staged = false;  // (device work: the staged results of the last solve are stale)
     Shard& s = h->shards[0];
     hipStream_t st = pick(s, stream);
     HIPCHK(hipSetDevice(s.dev));
@@ -781,6 +920,7 @@ int mpcqp_warm_start_device(mpcqp_handle* h, const double* dx, const double* dy,
 
 int mpcqp_solve_device(mpcqp_handle* h, double* dx, double* dy, int32_t* dstatus, int32_t* diters, void* stream) {
     if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "device entry points need a single-device handle");
+    h->staged = false;  // (device work: the staged results of the last solve are stale)
     Shard& s = h->shards[0];
     hipStream_t st = pick(s, stream);
     HIPCHK(hipSetDevice(s.dev));
@@ -805,6 +945,7 @@ int mpcqp_setup_solve_device(mpcqp_handle* h, const double* dPx, const double* d
                              const double* dl, const double* du, double* dx, double* dy, int32_t* dstatus,
                              int32_t* diters, void* stream) {
     if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "device entry points need a single-device handle");
+    h->staged = false;  // (device work: the staged results of the last solve are stale)
     Shard& s = h->shards[0];
     hipStream_t st = pick(s, stream);
     HIPCHK(hipSetDevice(s.dev));
@@ -833,6 +974,7 @@ void* mpcqp_get_stream(const mpcqp_handle* h) {
 
 int mpcqp_set_shared_matrices(mpcqp_handle* h, int32_t shared) {
     if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "device entry points need a single-device handle");
+    h->staged = false;  // (device work: the staged results of the last solve are stale)
     h->shards[0].kp.mat_shared = shared ? 1 : 0;
     return 0;
 }
@@ -945,6 +1087,8 @@ void mpcqp_free(mpcqp_handle* h) {
         if (s.stream) (void)hipStreamSynchronize(s.stream);
         if (s.dws) (void)hipFree(s.dws);
         if (s.dplan) (void)hipFree(s.dplan);
+        if (s.hstage) (void)hipHostFree(s.hstage);
+        if (s.hin) (void)hipHostFree(s.hin);
         if (s.ev0) (void)hipEventDestroy(s.ev0);
         if (s.ev1) (void)hipEventDestroy(s.ev1);
         if (s.last_ev) (void)hipEventDestroy(s.last_ev);
