@@ -3,7 +3,8 @@
 
 The reference's closed loop (vehicle_lateral_mpc_slack_increment.py:237,248) calls
 update(q=, l=, u=) then solve() on ONE problem per control step; this times both calls on the
-slack layout at N = 20 (configs[0]) and prints the mean and median microseconds per call.
+slack layout at N = 20 (configs[0]) and prints the mean and median microseconds per call,
+then a fresh object's setup() + solve() per call (the Control/MPC scripts' pattern).
 
   python tools/shim_latency.py [--steps 300]
 """
@@ -45,6 +46,18 @@ def main():
         its.append(r.info.iter)
     f = lambda v: f"mean {1e6 * np.mean(v):.0f} us, median {1e6 * np.median(v):.0f} us"  # noqa: E731
     print(f"config {a.config}, one QP, warm: update(q,l,u) {f(tu)}; solve() {f(ts)}; iterations {np.mean(its):.0f}")
+    # a fresh object per call (Control/MPC/mpc_kinematics.py:194-198: setup + solve every step)
+    tsu, tso = [], []
+    for _ in range(max(10, a.steps // 6)):
+        t0 = time.perf_counter()
+        p2 = OSQP()
+        p2.setup(P, q, A, l, u, warm_start=True, verbose=False)
+        t1 = time.perf_counter()
+        p2.solve()
+        t2 = time.perf_counter()
+        tsu.append(t1 - t0)
+        tso.append(t2 - t1)
+    print(f"config {a.config}, fresh object per call: setup() {f(tsu)}; solve() {f(tso)}")
 
 
 if __name__ == "__main__":
