@@ -1,3 +1,10 @@
+#!/usr/bin/env python3
+"""Where a small setup's time goes (GPU only, diagnostic): osqp-python's data
+canonicalisation, mpcqp_setup_batch + mpcqp_free, mpcqp_create + mpcqp_free (allocation
+only), and the shim's whole OSQP().setup(), in microseconds per call, on one cfg-2 QP.
+
+  python tools/setup_latency_probe.py
+"""
 import sys, time, os
 sys.path.insert(0, os.path.join(os.environ.get("GRAFT_REPO_ROOT", "/root/repo"), "python-mpc_amd"))
 import ctypes as C
