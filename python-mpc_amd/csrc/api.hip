@@ -81,7 +81,6 @@ struct Shard {
     // synchronisation; the info / certificate / polish getters then read it (mpcqp_handle::staged)
     char* hstage = nullptr;
     char* hin = nullptr;  // ... and of update()'s q, l, u and the error flags it reads back
-    size_t dws_bytes = 0, dplan_bytes = 0, hstage_bytes = 0, hin_bytes = 0;  // (resource pool keys)
     KParams kp{};
 };
 
@@ -123,92 +122,6 @@ void shape_params(const Plan& pl, KParams& k) {
     k.gkr = pl.max_row_nnz; k.gkc = pl.max_col_nnz;
 }
 
-// ---- resource pool ----
-// Device blocks, pinned host blocks and streams (with their three events) of freed handles,
-// kept for the next handle of the same shape: the Control/MPC scripts set up a fresh osqp
-// object every control step, and creating / destroying these costs most of a small setup
-// (~0.4 ms).  A reused block is cleared exactly as a new one (alloc_shard's memset), a reused
-// stream is idle (mpcqp_free synchronises it first).  Bounded: 256 MiB of device blocks,
-// 64 MiB pinned, 8 streams; past that, resources are released as before.  The pool is never
-// torn down (process exit reclaims it; no HIP call runs from a static destructor).
-struct ResPool {
-    struct Blk { int dev; size_t bytes; void* p; };
-    struct Str { int dev; hipStream_t st; hipEvent_t e0, e1, el; };
-    std::mutex mu;
-    std::vector<Blk> dev, pin;
-    std::vector<Str> str;
-    size_t dev_total = 0, pin_total = 0;
-};
-ResPool& respool() {
-    static ResPool* p = new ResPool;
-    return *p;
-}
-constexpr size_t kPoolDev = 256u << 20, kPoolPin = 64u << 20;
-constexpr size_t kPoolStreams = 8;
-
-hipError_t pool_malloc(int dev, size_t bytes, void** out, bool pinned) {
-    ResPool& r = respool();
-    {
-        std::lock_guard<std::mutex> lk(r.mu);
-        auto& v = pinned ? r.pin : r.dev;
-        for (size_t i = v.size(); i-- > 0;)
-            if (v[i].dev == dev && v[i].bytes == bytes) {
-                *out = v[i].p;
-                (pinned ? r.pin_total : r.dev_total) -= bytes;
-                v.erase(v.begin() + i);
-                return hipSuccess;
-            }
-    }
-    return pinned ? hipHostMalloc(out, bytes, hipHostMallocDefault) : hipMalloc(out, bytes);
-}
-void pool_free(int dev, size_t bytes, void* p, bool pinned) {
-    if (!p) return;
-    ResPool& r = respool();
-    {
-        std::lock_guard<std::mutex> lk(r.mu);
-        size_t& tot = pinned ? r.pin_total : r.dev_total;
-        if (tot + bytes <= (pinned ? kPoolPin : kPoolDev)) {
-            (pinned ? r.pin : r.dev).push_back({dev, bytes, p});
-            tot += bytes;
-            return;
-        }
-    }
-    if (pinned) (void)hipHostFree(p);
-    else (void)hipFree(p);
-}
-int pool_stream(Shard& s) {
-    ResPool& r = respool();
-    {
-        std::lock_guard<std::mutex> lk(r.mu);
-        for (size_t i = r.str.size(); i-- > 0;)
-            if (r.str[i].dev == s.dev) {
-                s.stream = r.str[i].st; s.ev0 = r.str[i].e0; s.ev1 = r.str[i].e1; s.last_ev = r.str[i].el;
-                r.str.erase(r.str.begin() + i);
-                return 0;
-            }
-    }
-    HIPCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-    HIPCHK(hipEventCreate(&s.ev0));
-    HIPCHK(hipEventCreate(&s.ev1));
-    HIPCHK(hipEventCreateWithFlags(&s.last_ev, hipEventDisableTiming));
-    return 0;
-}
-void pool_stream_release(Shard& s) {
-    if (!s.stream) return;
-    ResPool& r = respool();
-    {
-        std::lock_guard<std::mutex> lk(r.mu);
-        if (r.str.size() < kPoolStreams && s.ev0 && s.ev1 && s.last_ev) {
-            r.str.push_back({s.dev, s.stream, s.ev0, s.ev1, s.last_ev});
-            return;
-        }
-    }
-    if (s.ev0) (void)hipEventDestroy(s.ev0);
-    if (s.ev1) (void)hipEventDestroy(s.ev1);
-    if (s.last_ev) (void)hipEventDestroy(s.last_ev);
-    (void)hipStreamDestroy(s.stream);
-}
-
 int upload_plan(const Plan& pl, Shard& s) {
     std::vector<const std::vector<int>*> parts = {
         &pl.pad_var, &pl.acsc_ptr, &pl.acsc_row, &pl.acsc_v, &pl.acsr_ptr, &pl.acsr_col, &pl.acsr_v,
@@ -222,8 +135,7 @@ int upload_plan(const Plan& pl, Shard& s) {
         flat.insert(flat.end(), v->begin(), v->end());
         flat.push_back(0);  // never allocate zero-length parts
     }
-    s.dplan_bytes = flat.size() * sizeof(int);
-    HIPCHK(pool_malloc(s.dev, s.dplan_bytes, (void**)&s.dplan, false));
+    HIPCHK(hipMalloc(&s.dplan, flat.size() * sizeof(int)));
     HIPCHK(hipMemcpy(s.dplan, flat.data(), flat.size() * sizeof(int), hipMemcpyHostToDevice));
     const int** dst[] = {&s.kp.pad_var, &s.kp.acsc_ptr, &s.kp.acsc_row, &s.kp.acsc_v, &s.kp.acsr_ptr,
                          &s.kp.acsr_col, &s.kp.acsr_v, &s.kp.psym_ptr, &s.kp.psym_col, &s.kp.psym_v,
@@ -263,13 +175,15 @@ size_t workspace_bytes(const Plan& pl, long B, bool with_io) {
 int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
     const Plan& pl = h->plan;
     HIPCHK(hipSetDevice(s.dev));
-    if (int e = pool_stream(s)) return e;
+    HIPCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreate(&s.ev0));
+    HIPCHK(hipEventCreate(&s.ev1));
+    HIPCHK(hipEventCreateWithFlags(&s.last_ev, hipEventDisableTiming));
     if (int e = upload_plan(pl, s)) return e;
     const long B = s.B, n = pl.n, m = pl.m, np = pl.npad, nb = pl.nb;
     const long SS = (long)kS * kS;
     size_t total = workspace_bytes(pl, B, with_io);
-    hipError_t e = pool_malloc(s.dev, total, &s.dws, false);
-    if (e == hipSuccess) s.dws_bytes = total;
+    hipError_t e = hipMalloc(&s.dws, total);
     if (e != hipSuccess)
         return fail(MPCQP_ENOMEM, "hipMalloc(%zu bytes) failed: %s", total, hipGetErrorString(e));
     HIPCHK(hipMemset(s.dws, 0, total));
@@ -676,10 +590,7 @@ int mpcqp_update_batch(mpcqp_handle* h, const double* q, const double* l, const 
         if (int e = stream_enter(s, s.stream)) return e;
         const long Bs = s.B;
         if (in_bytes(Bs) <= kStageMax) {
-            if (!s.hin) {
-                HIPCHK(pool_malloc(s.dev, in_bytes(Bs), (void**)&s.hin, true));
-                s.hin_bytes = in_bytes(Bs);
-            }
+            if (!s.hin) HIPCHK(hipHostMalloc((void**)&s.hin, in_bytes(Bs), hipHostMallocDefault));
             double *hq = (double*)s.hin, *hl = hq + Bs * n, *hu = hl + Bs * m;
             int* herr = (int*)(hu + Bs * m);
             if (q) {
@@ -880,10 +791,7 @@ int mpcqp_solve_batch(mpcqp_handle* h, double* x, double* y, int32_t* status, in
         HIPCHK(hipSetDevice(s.dev));
         const size_t sb = stage_bytes(h, s.B);
         if (sb <= kStageMax) {
-            if (!s.hstage) {
-                HIPCHK(pool_malloc(s.dev, sb, (void**)&s.hstage, true));
-                s.hstage_bytes = sb;
-            }
+            if (!s.hstage) HIPCHK(hipHostMalloc((void**)&s.hstage, sb, hipHostMallocDefault));
             const Stage g = stage_of(h, s);
             const long Bs = s.B;
             auto cp = [&](void* dst, const void* src, size_t bytes) -> int {
@@ -1229,12 +1137,14 @@ void mpcqp_free(mpcqp_handle* h) {
     for (auto& s : h->shards) {
         (void)hipSetDevice(s.dev);
         if (s.stream) (void)hipStreamSynchronize(s.stream);
-        if (s.last_st && s.last_st != s.stream) (void)hipEventSynchronize(s.last_ev);  // a caller stream's last call
-        pool_free(s.dev, s.dws_bytes, s.dws, false);
-        pool_free(s.dev, s.dplan_bytes, s.dplan, false);
-        pool_free(s.dev, s.hstage_bytes, s.hstage, true);
-        pool_free(s.dev, s.hin_bytes, s.hin, true);
-        pool_stream_release(s);
+        if (s.dws) (void)hipFree(s.dws);
+        if (s.dplan) (void)hipFree(s.dplan);
+        if (s.hstage) (void)hipHostFree(s.hstage);
+        if (s.hin) (void)hipHostFree(s.hin);
+        if (s.ev0) (void)hipEventDestroy(s.ev0);
+        if (s.ev1) (void)hipEventDestroy(s.ev1);
+        if (s.last_ev) (void)hipEventDestroy(s.last_ev);
+        if (s.stream) (void)hipStreamDestroy(s.stream);
     }
     delete h;
 }
