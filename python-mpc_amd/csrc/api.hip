@@ -16,7 +16,6 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
-#include <mutex>
 #include <string>
 #include <vector>
 
@@ -296,57 +295,6 @@ std::string choose_plan(int32_t n, int32_t m, const int32_t* Pp, const int32_t* 
     return build_plan(n, m, Pp, Pi, Ap, Ai, pl, false);
 }
 
-// Plans by sparsity pattern: the Control/MPC scripts set up a fresh osqp object, with the same
-// pattern, every control step (mpc_kinematics.py:194-198), and planning is most of a small
-// setup's host time (~0.8 ms at N = 20).  A few recent plans are kept; a hit compares the whole
-// pattern, the polish flag and the plan-choice overrides, so it returns exactly the plan
-// choose_plan would build.
-struct PlanKey {
-    int32_t n = 0, m = 0;
-    bool polish = false;
-    std::string env;
-    std::vector<int32_t> pat;
-    bool operator==(const PlanKey& o) const {
-        return n == o.n && m == o.m && polish == o.polish && env == o.env && pat == o.pat;
-    }
-};
-std::mutex g_plan_mu;
-std::vector<std::pair<PlanKey, Plan>> g_plans;  // most recently used last
-constexpr size_t kPlanCache = 8;
-
-std::string cached_plan(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
-                        const int32_t* Ai, const mpcqp_settings& st, Plan& pl) {
-    if (n <= 0 || m < 0 || Pp[n] < 0 || Ap[n] < 0) return choose_plan(n, m, Pp, Pi, Ap, Ai, st, pl);
-    PlanKey k;
-    k.n = n;
-    k.m = m;
-    k.polish = st.polish != 0;
-    const char* ev = getenv("MPCQP_ELIM");
-    const char* vv = getenv("MPCQP_VARIANT");
-    k.env = std::string(ev ? ev : "") + "|" + (vv ? vv : "");
-    k.pat.reserve(2 * ((size_t)n + 1) + (size_t)Pp[n] + (size_t)Ap[n]);
-    k.pat.insert(k.pat.end(), Pp, Pp + n + 1);
-    k.pat.insert(k.pat.end(), Pi, Pi + Pp[n]);
-    k.pat.insert(k.pat.end(), Ap, Ap + n + 1);
-    k.pat.insert(k.pat.end(), Ai, Ai + Ap[n]);
-    {
-        std::lock_guard<std::mutex> lk(g_plan_mu);
-        for (size_t i = g_plans.size(); i-- > 0;)
-            if (g_plans[i].first == k) {
-                pl = g_plans[i].second;
-                std::rotate(g_plans.begin() + i, g_plans.begin() + i + 1, g_plans.end());
-                return std::string();
-            }
-    }
-    std::string err = choose_plan(n, m, Pp, Pi, Ap, Ai, st, pl);
-    if (err.empty()) {
-        std::lock_guard<std::mutex> lk(g_plan_mu);
-        g_plans.emplace_back(std::move(k), pl);
-        if (g_plans.size() > kPlanCache) g_plans.erase(g_plans.begin());
-    }
-    return err;
-}
-
 int validate_settings(const mpcqp_settings& s) {
     if (!(s.rho > 0) || !(s.sigma > 0) || s.max_iter <= 0 || s.eps_abs < 0 || s.eps_rel < 0 ||
         (s.eps_abs == 0 && s.eps_rel == 0) || !(s.eps_prim_inf > 0) || !(s.eps_dual_inf > 0) ||
@@ -368,7 +316,7 @@ int make_handle(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi, cons
     if (settings) h->set = *settings;
     else mpcqp_default_settings(&h->set);
     if (int e = validate_settings(h->set)) return e;
-    std::string err = cached_plan(n, m, Pp, Pi, Ap, Ai, h->set, h->plan);
+    std::string err = choose_plan(n, m, Pp, Pi, Ap, Ai, h->set, h->plan);
     if (!err.empty()) {
         bool unsup = err.rfind("unsupported", 0) == 0;
         return fail(unsup ? MPCQP_EUNSUPPORTED : MPCQP_EINVAL, "%s", err.c_str());
