@@ -180,3 +180,28 @@ def test_elimination_schur_complement_solves_the_full_system():
         p, ec = coup.get(j, (None, 0.0))
         x[j] = rhs[j] / K[j, j] - (ec * x[p] if p is not None else 0.0)
     assert np.allclose(x, x_ref, rtol=1e-9, atol=1e-12)
+
+
+def test_null_handle_is_einval():
+    """Every handle entry point refuses a NULL handle with MPCQP_EINVAL (no device needed),
+    the matrix-update and update-settings entries included."""
+    import ctypes as C
+    L = osqp_amd.lib()
+    s = osqp_amd._make_settings()
+    null = C.c_void_p()
+    calls = [
+        lambda: L.mpcqp_update_batch(null, None, None, None),
+        lambda: L.mpcqp_update_matrices_batch(null, None, None, 0, None, None, 0),
+        lambda: L.mpcqp_update_settings(null, C.byref(s), 0),
+        lambda: L.mpcqp_warm_start_batch(null, None, None),
+        lambda: L.mpcqp_solve_batch(null, None, None, None, None),
+        lambda: L.mpcqp_get_info_batch(null, None, None, None, None, None),
+        lambda: L.mpcqp_get_certificates(null, None, None),
+        lambda: L.mpcqp_synchronize(null),
+    ]
+    for c in calls:
+        assert c() == 1  # MPCQP_EINVAL (include/mpcqp.h)
+    with pytest.raises(ValueError, match="not initialized"):
+        osqp_amd.OSQP().update_settings(eps_abs=1e-4)
+    with pytest.raises(ValueError, match="not initialized"):
+        osqp_amd.OSQPBatch().update(Px=np.ones((1, 3)))
