@@ -205,3 +205,24 @@ def test_null_handle_is_einval():
         osqp_amd.OSQP().update_settings(eps_abs=1e-4)
     with pytest.raises(ValueError, match="not initialized"):
         osqp_amd.OSQPBatch().update(Px=np.ones((1, 3)))
+
+
+def test_matrix_update_index_mapping_on_host():
+    """OSQPBatch.update(Px=, Px_idx=) maps osqp's value indices (triu(P) CSC, explicit zeros
+    included) to the device pattern, which drops entries zero in every instance: kept
+    entries keep their order, a dropped one may only be set to zero (host logic, no device)."""
+    b = osqp_amd.OSQPBatch()
+    b.B = 2
+    Px = np.array([[4.0, 0.0, 2.0, 1.0], [5.0, 0.0, 3.0, 0.0]])  # entry 1 zero in both instances
+    kmap = osqp_amd._kept_index(Px)
+    assert kmap.tolist() == [0, -1, 1, 2]
+    vals, idx = b._matrix_values(np.array([[7.0, 0.0], [8.0, 0.0]]), np.array([3, 1]), kmap, 4, "P")
+    assert idx.tolist() == [2] and vals.tolist() == [[7.0], [8.0]]
+    vals, idx = b._matrix_values(np.arange(8.0).reshape(2, 4) * np.array([1, 0, 1, 1]), None, kmap, 4, "P")
+    assert idx.tolist() == [0, 1, 2] and vals.shape == (2, 3)
+    with pytest.raises(ValueError, match="zero in every instance"):
+        b._matrix_values(np.array([[1.0], [0.0]]), np.array([1]), kmap, 4, "P")
+    with pytest.raises(ValueError, match="greater than"):
+        b._matrix_values(np.ones((2, 5)), np.arange(5), kmap, 4, "P")
+    with pytest.raises(ValueError, match="out of range"):
+        b._matrix_values(np.ones((2, 1)), np.array([4]), kmap, 4, "P")
