@@ -53,6 +53,67 @@ __device__ __forceinline__ void put16(double (&v)[16], int j, double x) {
     }
 }
 
+// Row i's columns [0, 16) at src (a row of a row-major S x S tile, from column 16 h) into
+// v, read as 8 ds_read_b128 in the order column pair s ^ (i & 7) and put back in column
+// order by a three-stage conditional-swap network.  In column order every lane of a 16-lane
+// group of one read hits the same four banks (the rows are 256 bytes apart: 16-way, 512
+// LDS cycles per wave for the 8 reads); rotated, the group's rows spread over the eight
+// pairs' bank quads (2-way, 64 cycles; tools/lds_banks.py --swizzle).  The tile layout
+// is unchanged.  st_row16 is the same for the store-back.
+// The network's swaps are explicit v_cndmask_b32 on the lane mask (the compiler, given
+// selects between the values, turned them into a scratch array indexed by m)
+__device__ __forceinline__ unsigned sel32(const unsigned long long mk, const unsigned a, const unsigned b) {
+    unsigned r;
+    asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(mk));
+    return r;  // mk's lane bit ? b : a
+}
+__device__ __forceinline__ double seld(const unsigned long long mk, const double a, const double b) {
+    const unsigned lo = sel32(mk, (unsigned)__double2loint(a), (unsigned)__double2loint(b));
+    const unsigned hi = sel32(mk, (unsigned)__double2hiint(a), (unsigned)__double2hiint(b));
+    return __hiloint2double((int)hi, (int)lo);
+}
+#define MPCQP_CSW(mk, a, b)                \
+    {                                      \
+        const double2 t_ = a;              \
+        a.x = seld(mk, a.x, b.x);          \
+        a.y = seld(mk, a.y, b.y);          \
+        b.x = seld(mk, b.x, t_.x);         \
+        b.y = seld(mk, b.y, t_.y);         \
+    }
+#define MPCQP_XOR_PERM8(m, q0, q1, q2, q3, q4, q5, q6, q7)                                           \
+    {                                                                                              \
+        const unsigned long long s1_ = __builtin_amdgcn_ballot_w64(((m) & 1) != 0);                \
+        const unsigned long long s2_ = __builtin_amdgcn_ballot_w64(((m) & 2) != 0);                \
+        const unsigned long long s4_ = __builtin_amdgcn_ballot_w64(((m) & 4) != 0);                \
+        MPCQP_CSW(s1_, q0, q1) MPCQP_CSW(s1_, q2, q3) MPCQP_CSW(s1_, q4, q5) MPCQP_CSW(s1_, q6, q7) \
+        MPCQP_CSW(s2_, q0, q2) MPCQP_CSW(s2_, q1, q3) MPCQP_CSW(s2_, q4, q6) MPCQP_CSW(s2_, q5, q7) \
+        MPCQP_CSW(s4_, q0, q4) MPCQP_CSW(s4_, q1, q5) MPCQP_CSW(s4_, q2, q6) MPCQP_CSW(s4_, q3, q7) \
+    }
+__device__ __forceinline__ void ld_row16(const double* __restrict__ src, const int i, double (&v)[16]) {
+    const int m = i & 7;
+    double2 q0 = *(const double2*)(src + 2 * (0 ^ m)), q1 = *(const double2*)(src + 2 * (1 ^ m));
+    double2 q2 = *(const double2*)(src + 2 * (2 ^ m)), q3 = *(const double2*)(src + 2 * (3 ^ m));
+    double2 q4 = *(const double2*)(src + 2 * (4 ^ m)), q5 = *(const double2*)(src + 2 * (5 ^ m));
+    double2 q6 = *(const double2*)(src + 2 * (6 ^ m)), q7 = *(const double2*)(src + 2 * (7 ^ m));
+    MPCQP_XOR_PERM8(m, q0, q1, q2, q3, q4, q5, q6, q7)  // q_s held pair s ^ m; now pair s
+    v[0] = q0.x, v[1] = q0.y, v[2] = q1.x, v[3] = q1.y, v[4] = q2.x, v[5] = q2.y, v[6] = q3.x, v[7] = q3.y;
+    v[8] = q4.x, v[9] = q4.y, v[10] = q5.x, v[11] = q5.y, v[12] = q6.x, v[13] = q6.y, v[14] = q7.x, v[15] = q7.y;
+}
+// sc * v to dst
+__device__ __forceinline__ void st_row16(double* __restrict__ dst, const int i, const double sc, const double (&v)[16]) {
+    const int m = i & 7;
+    double2 q0 = make_double2(sc * v[0], sc * v[1]), q1 = make_double2(sc * v[2], sc * v[3]);
+    double2 q2 = make_double2(sc * v[4], sc * v[5]), q3 = make_double2(sc * v[6], sc * v[7]);
+    double2 q4 = make_double2(sc * v[8], sc * v[9]), q5 = make_double2(sc * v[10], sc * v[11]);
+    double2 q6 = make_double2(sc * v[12], sc * v[13]), q7 = make_double2(sc * v[14], sc * v[15]);
+    MPCQP_XOR_PERM8(m, q0, q1, q2, q3, q4, q5, q6, q7)  // q_s = pair s ^ m
+#define MPCQP_ST(s) *(double2*)(dst + 2 * ((s) ^ m)) = q##s;
+    MPCQP_ST(0) MPCQP_ST(1) MPCQP_ST(2) MPCQP_ST(3) MPCQP_ST(4) MPCQP_ST(5) MPCQP_ST(6) MPCQP_ST(7)
+#undef MPCQP_ST
+}
+#undef MPCQP_XOR_PERM8
+#undef MPCQP_CSW
+
 // Gauss-Jordan inverse of the SPD tile T (32 x 32 in LDS) by ONE wave, in place, with a
 // copy to Sgk.  Lane (i, h) = (lane % 32, lane / 32) keeps row i, columns [16 h, 16 h + 16)
 // in registers.  The in-place Gauss-Jordan matrix of a symmetric input stays symmetric up
@@ -200,16 +261,21 @@ __device__ __forceinline__ bool gj_wave(double* __restrict__ T, double* __restri
 // pivot order only changes which rows count as pivoted in the sign rule M_ij = -M_ji.
 // T (LDS or the workspace) holds true values between the segments (sc = 1 on entry).
 // buf: 2 S doubles of LDS.  a <= 16 (a <= 8 for the unrolled SEG 2).
-template <int SEG, bool Compact = false>
+// Rot (unrolled form only): the tile rows are read and written in ld_row16's rotated order.
+template <int SEG, bool Compact = false, bool Rot = false>
 __device__ __forceinline__ bool gj_seg(double* __restrict__ T, double* __restrict__ buf, const int a, const int npiv,
                                        const double* __restrict__ dl) {
     const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
     double v[16];
+    if constexpr (!Rot || Compact) {
 #pragma unroll
-    for (int jj = 0; jj < 16; jj += 2) {
-        const double2 t2 = *(const double2*)(T + i * S + 16 * h + jj);
-        v[jj] = t2.x;
-        v[jj + 1] = t2.y;
+        for (int jj = 0; jj < 16; jj += 2) {
+            const double2 t2 = *(const double2*)(T + i * S + 16 * h + jj);
+            v[jj] = t2.x;
+            v[jj + 1] = t2.y;
+        }
+    } else {
+        ld_row16(T + i * S + 16 * h, i, v);
     }
     if (SEG == 2 && h == 0 && i < a) {
 #pragma unroll
@@ -280,8 +346,12 @@ __device__ __forceinline__ bool gj_seg(double* __restrict__ T, double* __restric
         for (int p = 0; p < 8; ++p)
             if (p < a) step(p, p, done || i < p);
     }
+    if constexpr (!Rot || Compact) {
 #pragma unroll
-    for (int jj = 0; jj < 16; jj += 2) *(double2*)(T + i * S + 16 * h + jj) = make_double2(sc * v[jj], sc * v[jj + 1]);
+        for (int jj = 0; jj < 16; jj += 2) *(double2*)(T + i * S + 16 * h + jj) = make_double2(sc * v[jj], sc * v[jj + 1]);
+    } else {
+        st_row16(T + i * S + 16 * h, i, sc, v);
+    }
     return minpiv > 0.0;
 }
 
@@ -403,7 +473,7 @@ __device__ __forceinline__ void assemble_targets(const KP& p, const SLds& L, con
 //     pivots rows [0, amax) of S_k (gj_seg<2>).
 // The critical path is 32 + 3 amax pivot steps instead of 4 x 32.  Outputs as mode 2 of
 // factorize: S_k^{-1} in Sg (LDS here), G_kj in Hg at pair k(k-1)/2 + j.
-template <class KP>
+template <bool ROT = false, class KP>
 __device__ __forceinline__ bool factorize_w2(const KP& p, SLds& L, const double rho, double* __restrict__ Hg,
                                              double* __restrict__ Sg) {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -435,7 +505,7 @@ __device__ __forceinline__ bool factorize_w2(const KP& p, SLds& L, const double 
         assemble_block<false, true>(p, L, rho, k, Sg + (long)k * SS, Ek(k), lane, 64, wave_sync);
         wave_sync();
         FPH(8)
-        okw = gj_seg<1>(Sg + (long)k * SS, bufw, k ? amax : 0, p.bsize[k], nullptr) && okw;
+        okw = gj_seg<1, false, ROT>(Sg + (long)k * SS, bufw, k ? amax : 0, p.bsize[k], nullptr) && okw;
         FPH(10)
     }
     __syncthreads();
@@ -483,7 +553,7 @@ __device__ __forceinline__ bool factorize_w2(const KP& p, SLds& L, const double 
         }
         __syncthreads();
         FPH(9)
-        if (w == 0) okw = gj_seg<2>(Sg + (long)k * SS, bufw, amax, p.bsize[k], dl) && okw;
+        if (w == 0) okw = gj_seg<2, false, ROT>(Sg + (long)k * SS, bufw, amax, p.bsize[k], dl) && okw;
         __syncthreads();
         FPH(11)
     }
@@ -499,7 +569,7 @@ __device__ __forceinline__ bool factorize_w2(const KP& p, SLds& L, const double 
 // k assembles D_k and pre-pivots it (block 0: the whole inverse), all four at once --
 // then the same k = 1..3 chain (F_k, the corner, the G blocks, wave 0's corner pivots).
 // The critical path of stage 1 is one block's pivots instead of two.  Same outputs.
-template <class KP>
+template <bool ROT = false, class KP>
 __device__ __forceinline__ bool factorize_w4(const KP& p, SLds& L, const double rho, double* __restrict__ Hg,
                                              double* __restrict__ Sg, double* __restrict__ Fo) {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -548,7 +618,7 @@ __device__ __forceinline__ bool factorize_w4(const KP& p, SLds& L, const double 
         wave_sync();
     }
     FPH(8)
-    bool okw = gj_seg<1>(Sg + (long)w * SS, bufw, w ? amax : 0, p.bsize[w], nullptr);
+    bool okw = gj_seg<1, false, ROT>(Sg + (long)w * SS, bufw, w ? amax : 0, p.bsize[w], nullptr);
     FPH(10)
     __syncthreads();
     FPH(11)
@@ -579,7 +649,7 @@ __device__ __forceinline__ bool factorize_w4(const KP& p, SLds& L, const double 
                 dl[r * 16 + c] = -sacc;
             }
             wave_sync();
-            okw = gj_seg<2>(Sg + (long)k * SS, bufw, amax, p.bsize[k], dl) && okw;
+            okw = gj_seg<2, false, ROT>(Sg + (long)k * SS, bufw, amax, p.bsize[k], dl) && okw;
         } else {
             // waves 1-3 meanwhile: G_kj = -F_k G_{k-1,j} (j < k-1), off the chain's path
 #pragma unroll 1
@@ -618,7 +688,7 @@ __host__ __device__ inline double* w8_gpair(double* Fg, double* Hg, int amax, in
 // exceed 8) while waves 1-7 form G_kj = -F_k G_{k-1,j}, j < k-1, reading G_{k-1,j} back
 // from Hg (written by this workgroup one step earlier).  Outputs as factorize's mode 2;
 // the tiles Sg lie in V past the scratch (w8_toff).
-template <class KP>
+template <bool ROT = false, class KP>
 __device__ __forceinline__ bool factorize_w8(const KP& p, SLds& L, const double rho, double* __restrict__ Fg,
                                              double* __restrict__ Hg, double* __restrict__ Sg) {
     constexpr int NB = 8, TT = 512;
@@ -645,7 +715,7 @@ __device__ __forceinline__ bool factorize_w8(const KP& p, SLds& L, const double 
     assemble_block<false, true>(p, L, rho, w, Sg + (long)w * SS, Ek(w), lane, 64, wave_sync);
     wave_sync();
     FPH(8)
-    bool okw = gj_seg<1>(Sg + (long)w * SS, bufw, w ? amax : 0, p.bsize[w], nullptr);
+    bool okw = gj_seg<1, false, ROT>(Sg + (long)w * SS, bufw, w ? amax : 0, p.bsize[w], nullptr);
     FPH(10)
     __syncthreads();
     FPH(11)
@@ -715,7 +785,7 @@ __device__ __forceinline__ bool factorize_w8(const KP& p, SLds& L, const double 
 //     rows [0, amax) of S_k (gj_seg<2>).
 // The Gauss-Jordan critical path is 32 + (nb - 1) amax pivot steps instead of 32 nb,
 // and the assembly runs on four waves at once.  Same outputs as factorize's mode 1.
-template <class KP>
+template <bool ROT = false, class KP>
 __device__ __forceinline__ bool factorize_g(const KP& p, SLds& L, const double rho, double* __restrict__ Fg,
                                             double* __restrict__ Sg) {
     constexpr int TT = 256;
@@ -811,18 +881,18 @@ __device__ __forceinline__ bool factorize_g(const KP& p, SLds& L, const double r
 // POL: the polish system P + delta I + A' diag(w) A instead (solve.hip::k_polish): row
 // weights w_i = (number of active copies of row i, from ct bits 0/1) * rho with
 // rho = 1 / delta, diagonal delta, factor stored as in mode 1.
-template <int TT, class KP, bool POL = false>
+template <int TT, class KP, bool POL = false, bool ROT = false>
 __device__ __forceinline__ bool factorize(const KP& p, SLds& L, double rho, double* __restrict__ Fg,
                                           double* __restrict__ Hg, double* __restrict__ Sg) {
     if constexpr (TT == 128 && !POL) {  // the two-wave kernel (variant 10: nb = 4, amax <= 8)
-        if (p.mode == 2 && p.nb == 4 && p.amax <= 8) return factorize_w2(p, L, rho, Hg, Sg);
+        if (p.mode == 2 && p.nb == 4 && p.amax <= 8) return factorize_w2<ROT>(p, L, rho, Hg, Sg);
     }
     if constexpr (TT == 256 && !POL) {  // the register-sweep kernels (variants 1-3), the four-wave kernel (17)
-        if (p.mode == 1 && p.amax <= 16) return factorize_g(p, L, rho, Fg, Sg);
-        if (p.variant == 17 && p.mode == 2 && p.nb == 4 && p.amax <= 8) return factorize_w4(p, L, rho, Hg, Sg, Fg);
+        if (p.mode == 1 && p.amax <= 16) return factorize_g<ROT>(p, L, rho, Fg, Sg);
+        if (p.variant == 17 && p.mode == 2 && p.nb == 4 && p.amax <= 8) return factorize_w4<ROT>(p, L, rho, Hg, Sg, Fg);
     }
     if constexpr (TT == 512 && !POL) {  // the eight-wave kernel (18)
-        if (p.variant == 18 && p.mode == 2 && p.nb == 8 && p.amax <= 12) return factorize_w8(p, L, rho, Fg, Hg, Sg);
+        if (p.variant == 18 && p.mode == 2 && p.nb == 8 && p.amax <= 12) return factorize_w8<ROT>(p, L, rho, Fg, Hg, Sg);
     }
     const int tid = threadIdx.x;
     const int nb = p.nb, amax = p.amax, mode = POL ? 1 : p.mode;
@@ -1446,16 +1516,17 @@ __device__ __noinline__ bool factorize_pol_nl(const KParams* gp, long b) {
 }
 // sdst: where the S_k^{-1} tiles go (default: the workspace; the two-wave kernel keeps
 // them in LDS)
-template <int TT>
+template <int TT, bool ROT = false>
 __device__ __forceinline__ bool factorize_ph(const KParams* gp, long b, double rho, double* sdst) {
     KPc& p = kconst(gp);
     SL2 c = carve(p);
-    return factorize<TT>(p, c.L, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
+    return factorize<TT, KPc, false, ROT>(p, c.L, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
                      sdst ? sdst : p.Si + b * (long)p.nb * SS);
 }
-template <int TT>
+// ROT: the Gauss-Jordan steps read and write the tile rows in rotated order (ld_row16)
+template <int TT, bool ROT = false>
 __device__ __noinline__ bool factorize_nl(const KParams* gp, long b, double rho, double* sdst = nullptr) {
-    return factorize_ph<TT>(gp, b, rho, sdst);
+    return factorize_ph<TT, ROT>(gp, b, rho, sdst);
 }
 
 

@@ -1137,7 +1137,10 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 for (int i = tid; i < m; i += T4) yp[i] = L.ys[i];
                 __syncthreads();  // every ys read is done before factorize_w4's E tiles overwrite it
             }
-            const bool ok = factorize_nl<T4>(p.self, b, rho, Sg);
+            // the slack layouts' (EL) factorisation with rotated tile rows: cfg 3
+            // 43.38 -> 43.16 ms; cfg 2's build lost 1.6 % to the register assignment it moved
+            // (profiles/r3s3_ab/ab_swz*.json)
+            const bool ok = factorize_nl<T4, EL>(p.self, b, rho, Sg);
             if (!ok) {
                 if (iter == 0) {
                     if (xo) for (int j = tid; j < n; j += T4) opaque_ptr(xo + b * n)[j] = __builtin_nan("");
