@@ -226,3 +226,31 @@ def test_matrix_update_index_mapping_on_host():
         b._matrix_values(np.ones((2, 5)), np.arange(5), kmap, 4, "P")
     with pytest.raises(ValueError, match="out of range"):
         b._matrix_values(np.ones((2, 1)), np.array([4]), kmap, 4, "P")
+
+
+def test_rotated_tile_row_network_round_trips():
+    """ld_row16 / st_row16 (csrc/solve_phases.h): lane i reads column pair s ^ (i & 7) at step
+    s and a three-stage conditional swap (bits 1, 2, 4 of i & 7) restores column order; the
+    store applies the same involution before writing pair s ^ (i & 7).  The index model here
+    checks that every row lands in column order and that a 16-lane group's reads of one step
+    fall on distinct column pairs for distinct i & 7 (the 2-way bound of tools/lds_banks.py)."""
+    def network(q, m):
+        q = list(q)
+        for bit in (1, 2, 4):
+            if m & bit:
+                for s in range(8):
+                    if not s & bit:
+                        q[s], q[s | bit] = q[s | bit], q[s]
+        return q
+
+    for i in range(32):
+        m = i & 7
+        row = [(i, 2 * c) for c in range(8)]            # pair c of row i
+        loaded = [row[s ^ m] for s in range(8)]          # step s reads pair s ^ m
+        assert network(loaded, m) == row
+        out = [None] * 8
+        for s, v in enumerate(network(row, m)):          # st_row16: q_s = pair s ^ m
+            out[s ^ m] = v
+        assert out == row
+    for s in range(8):
+        assert len({s ^ (i & 7) for i in range(8)}) == 8
