@@ -100,6 +100,11 @@ typedef struct {
     int32_t threads_per_qp;     /* workgroup size of that kernel */
     int32_t n_eliminated;       /* variables taken out of the block system by a scalar Schur
                                    complement (degree <= 1 vertices of K: slack columns) */
+    int32_t plan_choice;        /* 0 plain plan (elimination not tried: polish, MPCQP_ELIM=0, a
+                                   variant override), 1 eliminated plan, 2 an eliminated plan was
+                                   built but did not fit the four-wave kernel (the reason:
+                                   mpcqp_plan_preview's note; MPCQP_PLAN_LOG=1 prints it),
+                                   3 nothing to eliminate */
 } mpcqp_plan_info;
 
 typedef struct mpcqp_handle mpcqp_handle;
@@ -150,7 +155,9 @@ int mpcqp_warm_start_batch(mpcqp_handle *h, const double *x, const double *y);
  * check_termination, warm_start take the new values; sigma, scaling and the adaptive-rho
  * settings must be unchanged (MPCQP_EINVAL otherwise), as OSQP fixes them at setup.  Any
  * handle.  polish = 1 on a handle whose plan eliminated variables (the slack layouts set up
- * without polish) is MPCQP_EUNSUPPORTED. */
+ * without polish) moves the handle onto the plain plan first (polish factors all of K): its
+ * data, scaling, iterates, rho and row classes are kept, so the next solve continues exactly
+ * as on a handle set up with polish on. */
 int mpcqp_update_settings(mpcqp_handle *h, const mpcqp_settings *s, int32_t set_rho);
 /* any output may be NULL */
 int mpcqp_solve_batch(mpcqp_handle *h, double *x, double *y, int32_t *status, int32_t *iters);
@@ -244,6 +251,15 @@ int mpcqp_analyze(int32_t n, int32_t m, const int32_t *Pp, const int32_t *Pi,
 int mpcqp_analyze_ex(int32_t n, int32_t m, const int32_t *Pp, const int32_t *Pi,
                      const int32_t *Ap, const int32_t *Ai, int32_t eliminate, int32_t *nb,
                      int32_t *block, int32_t *var_pad, int32_t *bsize, int32_t *n_eliminated);
+
+/* Host-only (no device needed): the plan and solve-kernel variant a handle created with
+ * this pattern and these settings (NULL: defaults) would take -- the shape fields of
+ * mpcqp_plan_info (batch, n_devices = 0) -- and, in note[note_cap] (may be NULL), why an
+ * eliminated plan was rejected ("" otherwise).  Used by the CPU test-suite to pin the
+ * kernel shape of each workload (e.g. the slack layout's reduced system: 4 blocks, amax <= 8). */
+int mpcqp_plan_preview(int32_t n, int32_t m, const int32_t *Pp, const int32_t *Pi,
+                       const int32_t *Ap, const int32_t *Ai, const mpcqp_settings *settings,
+                       mpcqp_plan_info *info, char *note, int32_t note_cap);
 
 /* ======================================================================
  * The MPC data path around the solver, on the device.

@@ -87,6 +87,7 @@ struct Shard {
 
 struct mpcqp_handle {
     Plan plan;
+    std::vector<int32_t> Pp, Pi, Ap, Ai;  // the user's pattern (a re-plan: replan_plain)
     mpcqp_settings set{};
     int n = 0, m = 0;
     long B = 0;
@@ -279,20 +280,69 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
 // configs 1, 3, 4: 230 variables, 8 blocks -> 125 in 4) -- else the plain plan.  Polish
 // factors the full system (factorize<POL>), so it keeps the plain plan; MPCQP_ELIM=0 (A/B)
 // and an MPCQP_VARIANT override other than 17 do too.
+// The plan's choice and, when an eliminated plan is rejected, why (Plan::choice /
+// choice_note; MPCQP_PLAN_LOG=1 prints it): a regression in the level ordering or the
+// greedy packing (e.g. amax > 8) then shows up in plan_info instead of as a quiet 2x
+// slowdown on the plain plan.
+std::string w4_misfit(const KParams& k) {
+    char buf[256];
+    const bool el = k.ne > 0;
+    std::string r;
+    auto need = [&](bool ok, const char* what, long have, long lim) {
+        if (ok) return;
+        snprintf(buf, sizeof buf, "%s%s = %ld > %ld", r.empty() ? "" : ", ", what, have, lim);
+        r += buf;
+    };
+    if (k.nb != 4) {
+        snprintf(buf, sizeof buf, "nb = %d (needs 4)", k.nb);
+        r += buf;
+    }
+    need(k.amax <= 8, "amax", k.amax, 8);
+    need(k.gkr <= 6, "longest A row", k.gkr, 6);
+    need(k.gkc <= (el ? 8 : 6), "longest A column", k.gkc, el ? 8 : 6);
+    need(k.pk <= 4, "longest P column", k.pk, 4);
+    need(k.m <= 256, "m", k.m, 256);
+    need(k.npad <= (el ? 256 : 128), "npad", k.npad, el ? 256 : 128);
+    need(k.nnzA <= (el ? 768 : 512), "nnzA", k.nnzA, el ? 768 : 512);
+    need(k.nnzP <= 256, "nnzP", k.nnzP, 256);
+    if (el) need(k.ecnt <= 2, "A nonzeros of an eliminated column", k.ecnt, 2);
+    if (el) need(k.ne <= 128, "eliminated columns", k.ne, 128);
+    KParams q2 = k;
+    q2.mode = 2;
+    need(lds_w2_bytes(q2) <= 80 * 1024, "LDS bytes", (long)lds_w2_bytes(q2), 80 * 1024);
+    return r.empty() ? "does not fit variant 17" : r;
+}
+
 std::string choose_plan(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
                         const int32_t* Ai, const mpcqp_settings& st, Plan& pl) {
     const char* ev = getenv("MPCQP_ELIM");
     const char* vv = getenv("MPCQP_VARIANT");
+    int choice = 0;
+    std::string note;
     if (!st.polish && !(ev && ev[0] == '0') && !(vv && *vv && atoi(vv) != 17)) {
         std::string err = build_plan(n, m, Pp, Pi, Ap, Ai, pl, true);
         if (err.empty() && pl.ne > 0) {  // (nothing eliminated: the plain plan, level-merged blocks)
             KParams k{};
             shape_params(pl, k);
             k.mode = 2;
-            if (variant_fits(k, 17)) return err;
+            if (variant_fits(k, 17)) {
+                pl.choice = 1;
+                return err;
+            }
+            choice = 2;
+            note = "eliminated plan (" + std::to_string(pl.ne) + " columns, " + std::to_string(pl.nb) +
+                   " blocks) rejected: " + w4_misfit(k);
+        } else {
+            choice = err.empty() ? 3 : 2;
+            if (!err.empty()) note = "eliminated plan failed: " + err;
         }
     }
-    return build_plan(n, m, Pp, Pi, Ap, Ai, pl, false);
+    std::string err = build_plan(n, m, Pp, Pi, Ap, Ai, pl, false);
+    pl.choice = choice;
+    pl.choice_note = note;
+    if (const char* lg = getenv("MPCQP_PLAN_LOG"); lg && lg[0] == '1' && !note.empty())
+        fprintf(stderr, "mpcqp: %s; using the plain plan\n", note.c_str());
+    return err;
 }
 
 int validate_settings(const mpcqp_settings& s) {
@@ -322,6 +372,8 @@ int make_handle(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi, cons
         return fail(unsup ? MPCQP_EUNSUPPORTED : MPCQP_EINVAL, "%s", err.c_str());
     }
     h->n = n; h->m = m; h->B = B;
+    h->Pp.assign(Pp, Pp + n + 1); h->Pi.assign(Pi, Pi + Pp[n]);
+    h->Ap.assign(Ap, Ap + n + 1); h->Ai.assign(Ai, Ai + Ap[n]);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
         return fail(MPCQP_EDEVICE, "no HIP device available (the solver has no CPU fallback)");
@@ -444,6 +496,107 @@ int check_convex(mpcqp_handle* h) {
                 return fail(MPCQP_ENONCVX, "instance %ld: P is not convex (the KKT matrix is not quasi-definite)",
                             s.b0 + i);
     }
+    return 0;
+}
+
+void free_shard(Shard& s) {
+    (void)hipSetDevice(s.dev);
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    if (s.dws) (void)hipFree(s.dws);
+    if (s.dplan) (void)hipFree(s.dplan);
+    if (s.hstage) (void)hipHostFree(s.hstage);
+    if (s.hin) (void)hipHostFree(s.hin);
+    if (s.ev0) (void)hipEventDestroy(s.ev0);
+    if (s.ev1) (void)hipEventDestroy(s.ev1);
+    if (s.last_ev) (void)hipEventDestroy(s.last_ev);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    s = Shard{};
+}
+
+// Move a handle whose plan eliminated variables (choose_plan: the slack layouts) onto the
+// plain plan, keeping its state, so that polish -- whose factorisation covers all of K
+// (factorize<POL>) -- can run (osqp-python's update_settings(polish=True) at any time).
+// Everything a solve carries from call to call moves over unchanged: the scaled data and
+// the scaling, the iterates x, z, y, each instance's rho and row classes, its last status,
+// info and certificates, the setup inputs; the per-column arrays (q, D, x: padded order)
+// are permuted from the old padded index to the new one.  The factor is formed at the start
+// of every solve, so nothing of it is kept.  The dispatch order restarts in identity order.
+int replan_plain(mpcqp_handle* h) {
+    if (int e = sync_all(h)) return e;
+    mpcqp_settings st = h->set;
+    st.polish = 1;
+    Plan npl;
+    std::string err = choose_plan(h->n, h->m, h->Pp.data(), h->Pi.data(), h->Ap.data(), h->Ai.data(), st, npl);
+    if (!err.empty()) return fail(MPCQP_EUNSUPPORTED, "re-plan for polish: %s", err.c_str());
+    Plan old = std::move(h->plan);
+    h->plan = std::move(npl);
+    const long n = h->n, m = h->m, npo = old.npad, npn = h->plan.npad;
+    std::vector<Shard> fresh;
+    int rc = 0;
+    for (auto& os : h->shards) {
+        Shard s;
+        s.dev = os.dev; s.b0 = os.b0; s.B = os.B;
+        fresh.push_back(s);
+        if ((rc = alloc_shard(h, fresh.back(), os.in_Px != nullptr))) break;
+        Shard& ns = fresh.back();
+        KParams &a = os.kp, &b = ns.kp;
+        b.mat_shared = a.mat_shared;
+        b.polish = a.polish; b.refine_iter = a.refine_iter; b.delta = a.delta;
+        b.alpha = a.alpha; b.eps_abs = a.eps_abs; b.eps_rel = a.eps_rel; b.eps_pinf = a.eps_pinf;
+        b.eps_dinf = a.eps_dinf; b.rho0 = a.rho0; b.max_iter = a.max_iter; b.check_term = a.check_term;
+        b.warm_start = a.warm_start; b.scaled_term = a.scaled_term;
+        const long B = s.B;
+        auto cp = [&](void* d, const void* src, size_t bytes) -> int {
+            if (bytes) HIPCHK(hipMemcpy(d, src, bytes, hipMemcpyDeviceToDevice));
+            return 0;
+        };
+        const size_t D8 = sizeof(double), I4 = sizeof(int);
+        if ((rc = cp(b.Px, a.Px, D8 * B * old.nnzP)) || (rc = cp(b.Ax, a.Ax, D8 * B * old.nnzA)) ||
+            (rc = cp(b.l, a.l, D8 * B * m)) || (rc = cp(b.u, a.u, D8 * B * m)) || (rc = cp(b.E, a.E, D8 * B * m)) ||
+            (rc = cp(b.z, a.z, D8 * B * m)) || (rc = cp(b.y, a.y, D8 * B * m)) || (rc = cp(b.scal, a.scal, D8 * B * 4)) ||
+            (rc = cp(b.dyc, a.dyc, D8 * B * m)) || (rc = cp(b.dxc, a.dxc, D8 * B * n)) ||
+            (rc = cp(b.obj, a.obj, D8 * B)) || (rc = cp(b.pri, a.pri, D8 * B)) || (rc = cp(b.dua, a.dua, D8 * B)) ||
+            (rc = cp(b.rho_est, a.rho_est, D8 * B)) || (rc = cp(b.ct, a.ct, (size_t)B * m)) ||
+            (rc = cp(b.status, a.status, I4 * B)) || (rc = cp(b.iter, a.iter, I4 * B)) ||
+            (rc = cp(b.rho_upd, a.rho_upd, I4 * B)) || (rc = cp(b.pstat, a.pstat, I4 * B)) ||
+            (rc = cp(b.err, a.err, I4 * B)))
+            break;
+        if (os.in_Px &&
+            ((rc = cp(ns.in_Px, os.in_Px, D8 * B * old.nnzP)) || (rc = cp(ns.in_Ax, os.in_Ax, D8 * B * old.nnzA)) ||
+             (rc = cp(ns.in_q, os.in_q, D8 * B * n)) || (rc = cp(ns.in_l, os.in_l, D8 * B * m)) ||
+             (rc = cp(ns.in_u, os.in_u, D8 * B * m)) || (rc = cp(ns.out_x, os.out_x, D8 * B * n)) ||
+             (rc = cp(ns.out_y, os.out_y, D8 * B * m))))
+            break;
+        // q, D, x: padded order -> the new padded order (padding: q = 0, D = 1, x = 0, as setup leaves it)
+        double* cols_old[3] = {a.q, a.D, a.x};
+        double* cols_new[3] = {b.q, b.D, b.x};
+        std::vector<double> ho((size_t)B * npo), hn((size_t)B * npn);
+        for (int t = 0; t < 3 && !rc; ++t) {
+            if (hipMemcpy(ho.data(), cols_old[t], D8 * B * npo, hipMemcpyDeviceToHost) != hipSuccess) {
+                rc = fail(MPCQP_EDEVICE, "re-plan: copy-out failed");
+                break;
+            }
+            std::fill(hn.begin(), hn.end(), t == 1 ? 1.0 : 0.0);
+            for (long i = 0; i < B; ++i)
+                for (long j = 0; j < n; ++j) hn[i * npn + h->plan.var_pad[j]] = ho[i * npo + old.var_pad[j]];
+            if (hipMemcpy(cols_new[t], hn.data(), D8 * B * npn, hipMemcpyHostToDevice) != hipSuccess)
+                rc = fail(MPCQP_EDEVICE, "re-plan: copy-in failed");
+        }
+        if (rc) break;
+        (void)hipSetDevice(ns.dev);
+        if (hipMemcpy((void*)b.self, &b, sizeof(KParams), hipMemcpyHostToDevice) != hipSuccess) {
+            rc = fail(MPCQP_EDEVICE, "re-plan: parameter copy failed");
+            break;
+        }
+    }
+    if (rc) {  // the handle keeps its old plan and workspace
+        for (auto& s : fresh) free_shard(s);
+        h->plan = std::move(old);
+        return rc;
+    }
+    for (auto& s : h->shards) free_shard(s);
+    h->shards.swap(fresh);
+    h->staged = false;
     return 0;
 }
 
@@ -668,9 +821,8 @@ int mpcqp_update_settings(mpcqp_handle* h, const mpcqp_settings* s, int32_t set_
         s->adaptive_rho_tolerance != o.adaptive_rho_tolerance || s->adaptive_rho_interval != o.adaptive_rho_interval)
         return fail(MPCQP_EINVAL, "sigma, scaling and the adaptive-rho settings cannot be changed after setup");
     if (int e = validate_settings(*s)) return e;  // (polish's delta / refinement steps included)
-    if (s->polish && h->plan.ne > 0)
-        return fail(MPCQP_EUNSUPPORTED, "polish needs the full factor: this layout's handle eliminated %d variables; "
-                                        "run setup with polish on", h->plan.ne);
+    if (s->polish && h->plan.ne > 0)  // polish factors all of K: the plain plan, state kept
+        if (int e = replan_plain(h)) return e;
     const bool rho_changed = set_rho != 0;
     const double rho = std::min(std::max(s->rho, 1e-6), 1e6);  // osqp_update_rho: RHO_MIN / RHO_MAX
     for (auto& sh : h->shards) {
@@ -1044,6 +1196,34 @@ int mpcqp_get_plan_info(const mpcqp_handle* h, mpcqp_plan_info* info) {
     info->variant = h->shards.empty() ? -1 : h->shards[0].kp.variant;
     info->threads_per_qp = h->shards.empty() ? 0 : solve_threads(h->shards[0].kp.variant);
     info->n_eliminated = h->plan.ne;
+    info->plan_choice = h->plan.choice;
+    return 0;
+}
+
+int mpcqp_plan_preview(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
+                       const int32_t* Ai, const mpcqp_settings* settings, mpcqp_plan_info* info, char* note,
+                       int32_t note_cap) {
+    if (!info || !Pp || !Pi || !Ap || !Ai) return fail(MPCQP_EINVAL, "NULL argument");
+    mpcqp_settings st;
+    if (settings) st = *settings;
+    else mpcqp_default_settings(&st);
+    if (int e = validate_settings(st)) return e;
+    Plan pl;
+    std::string err = choose_plan(n, m, Pp, Pi, Ap, Ai, st, pl);
+    if (note && note_cap > 0) snprintf(note, (size_t)note_cap, "%s", pl.choice_note.c_str());
+    if (!err.empty()) return fail(err.rfind("unsupported", 0) == 0 ? MPCQP_EUNSUPPORTED : MPCQP_EINVAL, "%s", err.c_str());
+    KParams k{};
+    shape_params(pl, k);
+    k.variant = solve_variant(k);
+    k.mode = k.variant >= 0 ? solve_mode(k.variant) : 0;
+    *info = mpcqp_plan_info{};
+    info->n = n; info->m = m; info->nb = pl.nb; info->block = kS; info->npad = pl.npad;
+    info->max_level = pl.max_level;
+    info->lds_bytes_solve = k.variant >= 0 ? (int64_t)lds_kernel_bytes(k) : 0;
+    info->bytes_per_instance = (int64_t)workspace_bytes(pl, 1, false);
+    info->amax = pl.amax; info->gather_k = pl.gather_k; info->variant = k.variant;
+    info->threads_per_qp = k.variant >= 0 ? solve_threads(k.variant) : 0;
+    info->n_eliminated = pl.ne; info->plan_choice = pl.choice;
     return 0;
 }
 
@@ -1082,18 +1262,7 @@ void mpcqp_free(mpcqp_handle* h) {
         drain(h->ev_setup, &t);
         drain(h->ev_solve, &t);
     }
-    for (auto& s : h->shards) {
-        (void)hipSetDevice(s.dev);
-        if (s.stream) (void)hipStreamSynchronize(s.stream);
-        if (s.dws) (void)hipFree(s.dws);
-        if (s.dplan) (void)hipFree(s.dplan);
-        if (s.hstage) (void)hipHostFree(s.hstage);
-        if (s.hin) (void)hipHostFree(s.hin);
-        if (s.ev0) (void)hipEventDestroy(s.ev0);
-        if (s.ev1) (void)hipEventDestroy(s.ev1);
-        if (s.last_ev) (void)hipEventDestroy(s.last_ev);
-        if (s.stream) (void)hipStreamDestroy(s.stream);
-    }
+    for (auto& s : h->shards) free_shard(s);
     delete h;
 }
 

@@ -82,6 +82,12 @@ struct Plan {
     // tterm's format: slot j of target t at (j * 2 ne + t)
     int eterm_max = 0;
     std::vector<int> etterm;
+    // Which plan a handle took (api.hip::choose_plan): 0 the plain plan (elimination not
+    // tried: polish, MPCQP_ELIM=0, an MPCQP_VARIANT override), 1 the eliminated plan, 2 an
+    // eliminated plan was built but the four-wave kernel's shape did not fit it (choice_note
+    // says which precondition failed), 3 nothing to eliminate
+    int choice = 0;
+    std::string choice_note;
 };
 
 // Returns "" on success, otherwise an error message.  eliminate: take degree <= 1

@@ -595,6 +595,10 @@ __device__ __forceinline__ bool factorize_w4(const KP& p, SLds& L, const double 
 #endif
     assemble_block<false, true>(p, L, rho, w, Sg + (long)w * SS, Ek(w), lane, 64, wave_sync);
     wave_sync();
+    // an eliminated column's pivot K_jj is a pivot of the full KKT factorisation too: a
+    // non-positive (or NaN) one makes the instance non-convex, as OSQP's LDL' of the
+    // quasi-definite matrix would find, even though the reduced blocks may still factor
+    bool oke = true;
     if (p.ne && lane < S) {
         // eliminated columns (plan.h Plan::eown): the owner lane of block column w S + lane
         // forms K_jj, K_pj of its column j, folds the Schur complement -K_pj^2 / K_jj into its
@@ -611,6 +615,7 @@ __device__ __forceinline__ bool factorize_w4(const KP& p, SLds& L, const double 
                 kpj += c.y < 0 ? L.Pv[c.x] : rho_of(L.ct[c.y], rho) * L.Acsc[c.x & 0xFFFF] * L.Acsc[(unsigned)c.x >> 16];
             }
             const double ed = 1.0 / kjj, ec = kpj * ed;
+            oke = kjj > 0.0 && ed < __builtin_huge_val();
             Sg[(long)w * SS + lane * S + lane] -= kpj * ec;
             Fo[2 * e] = ec;
             Fo[2 * e + 1] = ed;
@@ -619,6 +624,7 @@ __device__ __forceinline__ bool factorize_w4(const KP& p, SLds& L, const double 
     }
     FPH(8)
     bool okw = gj_seg<1, false, ROT>(Sg + (long)w * SS, bufw, w ? amax : 0, p.bsize[w], nullptr);
+    okw = okw && __builtin_amdgcn_ballot_w64(!oke) == 0;
     FPH(10)
     __syncthreads();
     FPH(11)

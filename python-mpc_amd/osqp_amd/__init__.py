@@ -86,7 +86,7 @@ class _PlanInfo(C.Structure):
         ("npad", C.c_int32), ("max_level", C.c_int32), ("batch", C.c_int64),
         ("n_devices", C.c_int32), ("lds_bytes_solve", C.c_int64), ("bytes_per_instance", C.c_int64),
         ("amax", C.c_int32), ("gather_k", C.c_int32), ("variant", C.c_int32), ("threads_per_qp", C.c_int32),
-        ("n_eliminated", C.c_int32),
+        ("n_eliminated", C.c_int32), ("plan_choice", C.c_int32),
     ]
 
 
@@ -152,6 +152,8 @@ def lib():
                                 i32p, i32p, i32p, i32p]
     L.mpcqp_analyze_ex.argtypes = [C.c_int32, C.c_int32, i32p, i32p, i32p, i32p, C.c_int32,
                                    i32p, i32p, i32p, i32p, i32p]
+    L.mpcqp_plan_preview.argtypes = [C.c_int32, C.c_int32, i32p, i32p, i32p, i32p, _P(_Settings),
+                                     _P(_PlanInfo), C.c_char_p, C.c_int32]
     _lib = L
     return L
 
@@ -220,6 +222,24 @@ def analyze(P, A, eliminate=False):
                                   C.byref(blk), _ip(vp), _ip(bs), C.byref(ne)), "analyze")
     out = (nb.value, blk.value, vp, bs[: nb.value].copy())
     return out + (ne.value,) if eliminate else out
+
+
+def plan_preview(P, A, **settings):
+    """Host-only (no GPU): the plan and solve-kernel variant a batch with this pattern and
+    these settings would take (mpcqp_plan_preview) -- plan_info's shape fields, plus
+    "note": why an eliminated plan was rejected ("" when it was not)."""
+    P, A = canonical_data(P, A)
+    n, m = P.shape[0], A.shape[0]
+    Pp = np.ascontiguousarray(P.indptr, np.int32); Pi = np.ascontiguousarray(P.indices, np.int32)
+    Ap = np.ascontiguousarray(A.indptr, np.int32); Ai = np.ascontiguousarray(A.indices, np.int32)
+    s = _make_settings(**{k: v for k, v in settings.items() if k != "verbose"})
+    info = _PlanInfo()
+    note = C.create_string_buffer(512)
+    _check(lib().mpcqp_plan_preview(n, m, _ip(Pp), _ip(Pi), _ip(Ap), _ip(Ai), C.byref(s), C.byref(info),
+                                    note, 512), "plan_preview")
+    out = {f[0]: getattr(info, f[0]) for f in _PlanInfo._fields_}
+    out["note"] = note.value.decode()
+    return out
 
 
 def _kept_index(V):

@@ -143,6 +143,39 @@ def test_elimination_plan_slack_layout(cfg):
     assert np.bincount(r[off & elim[r]], minlength=n).max() <= 1
 
 
+@pytest.mark.parametrize("cfg,nb,amax_max,variant,choice,ne", [
+    (1, 4, 8, 17, 1, 105),   # slack N = 20: the reduced system in the four-wave kernel
+    (3, 4, 8, 17, 1, 105),
+    (2, 4, 8, 17, 3, 0),     # vanilla N = 20: nothing to eliminate, four-wave kernel
+    (5, 17, 16, 12, 3, 0),   # incremental dynamic N = 50: the long-horizon kernel
+])
+def test_plan_preview_pins_each_workloads_kernel(cfg, nb, amax_max, variant, choice, ne):
+    """mpcqp_plan_preview (host only): the plan and kernel variant a handle would take.  The
+    slack layouts' eliminated plan must keep amax <= 8 (the four-wave kernel's coupling rows);
+    a regression in the level ordering or the greedy packing would otherwise fall back to
+    the plain 8-block plan quietly (2x slower) -- here it fails, and plan_choice / note say
+    why (plan.cpp greedy packing)."""
+    b = mpc.make_batch(cfg, B=2, seed=3)
+    P, _ = osqp_amd._drop_common_zeros(b["P"], b["Px"])
+    A, _ = osqp_amd._drop_common_zeros(b["A"], b["Ax"])
+    info = osqp_amd.plan_preview(P, A, **b["settings"])
+    assert info["note"] == "", info["note"]
+    assert (info["nb"], info["variant"], info["plan_choice"], info["n_eliminated"]) == (nb, variant, choice, ne)
+    assert info["amax"] <= amax_max
+    # polish factors the full system: the plain plan, elimination not tried
+    pol = osqp_amd.plan_preview(P, A, **dict(b["settings"], polish=True))
+    assert pol["plan_choice"] == 0 and pol["n_eliminated"] == 0
+
+
+def test_plan_preview_reports_a_rejected_elimination():
+    """An eliminated plan the four-wave kernel cannot take (the slack layout at N = 30: 6
+    blocks) is rejected with the failed preconditions named, and the plain plan is used."""
+    P, q, A, l, u = mpc.slack_qp(30, np.zeros(5))
+    info = osqp_amd.plan_preview(P, A, warm_start=True)
+    assert info["plan_choice"] == 2 and info["n_eliminated"] == 0
+    assert "nb = 6 (needs 4)" in info["note"] and "rejected" in info["note"]
+
+
 def test_elimination_schur_complement_solves_the_full_system():
     """The algebra the four-wave kernel runs for an eliminated column j with parent p
     (factorize_w4, solve_w4_body): K_pp -= K_pj^2 / K_jj, b_p -= (K_pj / K_jj) b_j, then

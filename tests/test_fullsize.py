@@ -103,3 +103,60 @@ def test_cfg3_full_batch_meets_the_termination_test():
     same = bo.iter == r1.iter[idx]
     du = np.abs(r1.x[idx][:, b["u_block"]] - bo.x[:, b["u_block"]]).max(axis=1)
     assert np.all(du[same] < 1e-4), du.max()
+
+
+def _stage_shift(v, N, nxa, nu, groups):
+    """One-stage shift of incremental-layout iterates (mpcqp_incr_warm_shift_device; the
+    reference's horizon shift, mpc_dynamics.py:589-610)."""
+    B = v.shape[0]
+    out = []
+    for g in range(groups):
+        blk = v[:, g * (N + 1) * nxa:(g + 1) * (N + 1) * nxa].reshape(B, N + 1, nxa)
+        out.append(np.concatenate([blk[:, 1:], blk[:, -1:]], 1).reshape(B, -1))
+    du = v[:, groups * (N + 1) * nxa:].reshape(B, N, nu)
+    out.append(np.concatenate([du[:, 1:], du[:, -1:]], 1).reshape(B, -1))
+    return np.concatenate(out, 1)
+
+
+def test_cfg5_full_batch_warm_meets_the_termination_test():
+    """configs[4] at full size (B = 8192 incremental dynamic QPs, N = 50), as bench.py times
+    it: a cold solve, then the solution shifted one stage (the warm start of SURVEY.md §8d
+    D2) and the next step's QP -- initial states jittered +-2 % of the D2 ranges, as
+    bench.py::bound_sequence -- solved from it, dispatched longest-previous-first from the
+    cold solve's iteration counts.  Every instance of both solves: status solved (the oracle
+    solves a 512-instance sample of this batch cold and warm with no other status) and OSQP's
+    termination test recomputed on the host.  An oracle sample of 128 pins the warm solve's
+    iteration counts and du."""
+    import bench
+    b = mpc.make_batch(5)
+    B, N = b["Px"].shape[0], b["N"]
+    assert B == 8192
+    s = {k: v for k, v in b["settings"].items() if k != "verbose"}
+    h = OSQPBatch()
+    h.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
+    r1 = h.solve()
+    assert (r1.status_val == 1).all(), np.unique(r1.status_val, return_counts=True)
+    ok_d, ok_p, fd, fp = _termination_holds(b, r1.x, r1.y)
+    assert ok_d.all(), (np.flatnonzero(~ok_d)[:10], fd.max())
+    assert ok_p.all(), (np.flatnonzero(~ok_p)[:10], fp.max())
+    xs, ys = _stage_shift(r1.x, N, 8, 2, 1), _stage_shift(r1.y, N, 8, 2, 2)
+    x0 = bench.x0_sequence(b, 2, bench.instance_seed(5, 0))[1]
+    l, u = b["l"].copy(), b["u"].copy()
+    l[:, :x0.shape[1]] = -x0
+    u[:, :x0.shape[1]] = -x0
+    h.update(l=l, u=u)
+    h.warm_start(x=xs, y=ys)
+    r2 = h.solve()
+    assert (r2.status_val == 1).all(), np.unique(r2.status_val, return_counts=True)
+    assert r2.iter.mean() < r1.iter.mean()
+    b2 = dict(b, l=l, u=u)
+    ok_d, ok_p, fd, fp = _termination_holds(b2, r2.x, r2.y)
+    assert ok_d.all(), (np.flatnonzero(~ok_d)[:10], fd.max())
+    assert ok_p.all(), (np.flatnonzero(~ok_p)[:10], fp.max())
+    idx = np.random.default_rng(2).choice(B, 128, replace=False)
+    bo = pyoracle.solve_batch(b["P"], b["A"], b["Px"][idx], b["q"][idx], b["Ax"][idx], l[idx], u[idx],
+                              nthreads=16, x0=xs[idx], y0=ys[idx], **s)
+    same = bo.iter == r2.iter[idx]
+    assert (bo.status_val == 1).all() and same.mean() >= 0.97, (bo.iter[~same], r2.iter[idx][~same])
+    du = np.abs(r2.x[idx][:, b["u_block"]] - bo.x[:, b["u_block"]]).max(axis=1)
+    assert np.all(du[same] < 1e-4), du.max()

@@ -985,6 +985,34 @@ def test_nonconvex_setup_raises_like_osqp():
         h.update(Px=Px)
 
 
+def test_nonconvex_eliminated_slack_raises_like_osqp():
+    """The slack layout's plan eliminates the slack columns (plan.h Plan::eown): their pivot
+    K_jj = P_jj + sigma + rho a^2 never enters the reduced block factor, so a negative slack
+    weight is caught by factorize_w4's own check of K_jj (the reduced blocks alone would still
+    factor: subtracting a negative Schur term raises the parent's diagonal).  A live slack's
+    weight -10 (the e_y slack of stage 3, P column 143): the oracle rejects it, and so must
+    setup() and update(Px=) -- ValueError naming the instance."""
+    b = mpc.make_batch(3, B=48, seed=12)
+    s = {k: v for k, v in b["settings"].items() if k != "verbose"}
+    P = b["P"]
+    pos = P.indptr[143]
+    assert P.indices[pos] == 143 and P.indptr[144] - pos == 1
+    Px = b["Px"].copy()
+    Px[5, pos] = -10.0
+    Pk = P.copy()
+    Pk.data = Px[5].copy()
+    with pytest.raises(ValueError):
+        pyoracle.OSQP().setup(Pk, b["q"][5], b["A"], b["l"][5], b["u"][5], verbose=False)
+    h = OSQPBatch()
+    with pytest.raises(ValueError, match="instance 5"):
+        h.setup(P, b["q"], b["A"], b["l"], b["u"], Px=Px, Ax=b["Ax"], **s)
+    h.setup(P, b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
+    assert h.plan_info()["n_eliminated"] > 0
+    assert (h.solve().status_val == 1).all()
+    with pytest.raises(ValueError, match="instance 5"):
+        h.update(Px=Px)
+
+
 @pytest.mark.parametrize("cfg,B", [(2, 64), (3, 48), (5, 12)])
 def test_update_settings_match_oracle(cfg, B):
     """update_settings (mpcqp_update_settings, osqp_update_settings / osqp_update_rho): on a
@@ -1029,6 +1057,65 @@ def test_update_settings_match_oracle(cfg, B):
         dev.update_settings(sigma=1e-5)
     with pytest.raises(ValueError):
         orc[0].update_settings(sigma=1e-5)
+
+
+def test_update_settings_polish_on_eliminated_plan(golden):
+    """update_settings(polish=True) on a slack-layout handle set up without polish, whose plan
+    eliminated the 105 slack columns (api.hip::replan_plain moves it onto the plain plan,
+    state kept): the warm re-solve after it matches the oracle doing the same calls -- the
+    reference's own slack QP through the shim, and a cfg-3 batch (status, iterations, polish
+    decision, x)."""
+    g = golden("slack_n20.npz")
+    P, A, q, l, u = g["P"], g["A"], g["q"], g["l"], g["u"]
+    d, o = OSQP(), pyoracle.OSQP()
+    d.setup(P, q, A, l, u, warm_start=True, verbose=False)
+    o.setup(P, q, A, l, u, warm_start=True)
+    d.solve(); o.solve()
+    d.update_settings(polish=True)
+    o.update_settings(polish=True)
+    # the reference's own update of step 401 (bound regime 1; the script's update, :237)
+    q2, l2, u2 = g["upd_q"][1], g["upd_l"][1], g["upd_u"][1]
+    d.update(q=q2, l=l2, u=u2); o.update(q=q2, l=l2, u=u2)
+    rd, ro = d.solve(), o.solve()
+    assert rd.info.status == ro.info.status and rd.info.iter == ro.info.iter
+    assert rd.info.status_polish == ro.info.status_polish
+    tol = 1e-8 if ro.info.status_polish == 1 else 1e-6
+    assert np.abs(rd.x - ro.x).max() < tol * max(1.0, np.abs(ro.x).max())
+
+    b = mpc.make_batch(3, B=48, seed=31)
+    s = dict(warm_start=True)
+    dev = OSQPBatch()
+    dev.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
+    assert dev.plan_info()["n_eliminated"] == 105
+    r0 = dev.solve()
+    orc = []
+    for k in range(b["Px"].shape[0]):
+        ok = pyoracle.OSQP()
+        Pk, Ak = b["P"].copy(), b["A"].copy()
+        Pk.data, Ak.data = b["Px"][k].copy(), b["Ax"][k].copy()
+        ok.setup(Pk, b["q"][k], Ak, b["l"][k], b["u"][k], **s)
+        ok.solve()
+        ok.update_settings(polish=True)
+        orc.append(ok)
+    dev.update_settings(polish=True)
+    info = dev.plan_info()
+    assert info["n_eliminated"] == 0 and info["plan_choice"] == 0
+    lb, ub = b["l"].copy(), b["u"].copy()
+    lb[:, :5] = ub[:, :5] = b["l"][:, :5] * 0.95
+    dev.update(l=lb, u=ub)
+    rd = dev.solve()
+    ros = []
+    for k, ok in enumerate(orc):
+        ok.update(l=lb[k], u=ub[k])
+        ros.append(ok.solve())
+    it = np.array([r.info.iter for r in ros])
+    ps = np.array([r.info.status_polish for r in ros])
+    assert (rd.status_val == 1).all() and (r0.status_val == 1).all()
+    assert (rd.iter == it).mean() >= 0.97, (rd.iter, it)
+    same = rd.iter == it
+    assert (rd.status_polish[same] == ps[same]).all()
+    xo = np.stack([r.x for r in ros])
+    assert np.abs(rd.x[same] - xo[same]).max() < 1e-6 * max(1.0, np.abs(xo).max())
 
 
 def test_shim_update_settings_polish_demo():
