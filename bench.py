@@ -365,7 +365,13 @@ def main(argv=None, solver_cls=None, device=None):
     import torch.distributed as dist
     from osqp_amd import DeviceBatch, _drop_common_zeros
 
+    json_fd = 1
     if world > 1:
+        # gloo prints its "[Gloo] Rank r is connected to ..." lines on stdout (from C++): send
+        # the ranks' stdout to stderr and keep the original for rank 0's one JSON line
+        sys.stdout.flush()
+        json_fd = os.dup(1)
+        os.dup2(2, 1)
         dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
     if device is None:
         torch.cuda.set_device(local)
@@ -662,7 +668,11 @@ def main(argv=None, solver_cls=None, device=None):
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
         }
-        print(json.dumps(line), flush=True)
+        if json_fd == 1:
+            print(json.dumps(line), flush=True)
+        else:
+            sys.stdout.flush()
+            os.write(json_fd, (json.dumps(line) + "\n").encode())
     if world > 1:
         dist.destroy_process_group()
 

@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -80,6 +81,7 @@ struct Shard {
     // synchronisation; the info / certificate / polish getters then read it (mpcqp_handle::staged)
     char* hstage = nullptr;
     char* hin = nullptr;  // ... and of update()'s q, l, u and the error flags it reads back
+    size_t dws_bytes = 0, dplan_bytes = 0, hstage_bytes = 0, hin_bytes = 0;  // (resource pool keys)
     KParams kp{};
 };
 
@@ -122,6 +124,92 @@ void shape_params(const Plan& pl, KParams& k) {
     k.gkr = pl.max_row_nnz; k.gkc = pl.max_col_nnz;
 }
 
+// ---- resource pool ----
+// Device blocks, pinned host blocks and streams (with their three events) of freed handles,
+// kept for the next handle of the same shape: the Control/MPC scripts set up a fresh osqp
+// object every control step, and creating / destroying these costs most of a small setup
+// (~0.4 ms).  A reused block is cleared exactly as a new one (alloc_shard's memset), a reused
+// stream is idle (mpcqp_free synchronises it first).  Bounded: 256 MiB of device blocks,
+// 64 MiB pinned, 8 streams; past that, resources are released as before.  The pool is never
+// torn down (process exit reclaims it; no HIP call runs from a static destructor).
+struct ResPool {
+    struct Blk { int dev; size_t bytes; void* p; };
+    struct Str { int dev; hipStream_t st; hipEvent_t e0, e1, el; };
+    std::mutex mu;
+    std::vector<Blk> dev, pin;
+    std::vector<Str> str;
+    size_t dev_total = 0, pin_total = 0;
+};
+ResPool& respool() {
+    static ResPool* p = new ResPool;
+    return *p;
+}
+constexpr size_t kPoolDev = 256u << 20, kPoolPin = 64u << 20;
+constexpr size_t kPoolStreams = 8;
+
+hipError_t pool_malloc(int dev, size_t bytes, void** out, bool pinned) {
+    ResPool& r = respool();
+    {
+        std::lock_guard<std::mutex> lk(r.mu);
+        auto& v = pinned ? r.pin : r.dev;
+        for (size_t i = v.size(); i-- > 0;)
+            if (v[i].dev == dev && v[i].bytes == bytes) {
+                *out = v[i].p;
+                (pinned ? r.pin_total : r.dev_total) -= bytes;
+                v.erase(v.begin() + i);
+                return hipSuccess;
+            }
+    }
+    return pinned ? hipHostMalloc(out, bytes, hipHostMallocDefault) : hipMalloc(out, bytes);
+}
+void pool_free(int dev, size_t bytes, void* p, bool pinned) {
+    if (!p) return;
+    ResPool& r = respool();
+    {
+        std::lock_guard<std::mutex> lk(r.mu);
+        size_t& tot = pinned ? r.pin_total : r.dev_total;
+        if (tot + bytes <= (pinned ? kPoolPin : kPoolDev)) {
+            (pinned ? r.pin : r.dev).push_back({dev, bytes, p});
+            tot += bytes;
+            return;
+        }
+    }
+    if (pinned) (void)hipHostFree(p);
+    else (void)hipFree(p);
+}
+int pool_stream(Shard& s) {
+    ResPool& r = respool();
+    {
+        std::lock_guard<std::mutex> lk(r.mu);
+        for (size_t i = r.str.size(); i-- > 0;)
+            if (r.str[i].dev == s.dev) {
+                s.stream = r.str[i].st; s.ev0 = r.str[i].e0; s.ev1 = r.str[i].e1; s.last_ev = r.str[i].el;
+                r.str.erase(r.str.begin() + i);
+                return 0;
+            }
+    }
+    HIPCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreate(&s.ev0));
+    HIPCHK(hipEventCreate(&s.ev1));
+    HIPCHK(hipEventCreateWithFlags(&s.last_ev, hipEventDisableTiming));
+    return 0;
+}
+void pool_stream_release(Shard& s) {
+    if (!s.stream) return;
+    ResPool& r = respool();
+    {
+        std::lock_guard<std::mutex> lk(r.mu);
+        if (r.str.size() < kPoolStreams && s.ev0 && s.ev1 && s.last_ev) {
+            r.str.push_back({s.dev, s.stream, s.ev0, s.ev1, s.last_ev});
+            return;
+        }
+    }
+    if (s.ev0) (void)hipEventDestroy(s.ev0);
+    if (s.ev1) (void)hipEventDestroy(s.ev1);
+    if (s.last_ev) (void)hipEventDestroy(s.last_ev);
+    (void)hipStreamDestroy(s.stream);
+}
+
 int upload_plan(const Plan& pl, Shard& s) {
     std::vector<const std::vector<int>*> parts = {
         &pl.pad_var, &pl.acsc_ptr, &pl.acsc_row, &pl.acsc_v, &pl.acsr_ptr, &pl.acsr_col, &pl.acsr_v,
@@ -135,7 +223,8 @@ int upload_plan(const Plan& pl, Shard& s) {
         flat.insert(flat.end(), v->begin(), v->end());
         flat.push_back(0);  // never allocate zero-length parts
     }
-    HIPCHK(hipMalloc(&s.dplan, flat.size() * sizeof(int)));
+    s.dplan_bytes = flat.size() * sizeof(int);
+    HIPCHK(pool_malloc(s.dev, s.dplan_bytes, (void**)&s.dplan, false));
     HIPCHK(hipMemcpy(s.dplan, flat.data(), flat.size() * sizeof(int), hipMemcpyHostToDevice));
     const int** dst[] = {&s.kp.pad_var, &s.kp.acsc_ptr, &s.kp.acsc_row, &s.kp.acsc_v, &s.kp.acsr_ptr,
                          &s.kp.acsr_col, &s.kp.acsr_v, &s.kp.psym_ptr, &s.kp.psym_col, &s.kp.psym_v,
@@ -175,15 +264,13 @@ size_t workspace_bytes(const Plan& pl, long B, bool with_io) {
 int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
     const Plan& pl = h->plan;
     HIPCHK(hipSetDevice(s.dev));
-    HIPCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-    HIPCHK(hipEventCreate(&s.ev0));
-    HIPCHK(hipEventCreate(&s.ev1));
-    HIPCHK(hipEventCreateWithFlags(&s.last_ev, hipEventDisableTiming));
+    if (int e = pool_stream(s)) return e;
     if (int e = upload_plan(pl, s)) return e;
     const long B = s.B, n = pl.n, m = pl.m, np = pl.npad, nb = pl.nb;
     const long SS = (long)kS * kS;
     size_t total = workspace_bytes(pl, B, with_io);
-    hipError_t e = hipMalloc(&s.dws, total);
+    hipError_t e = pool_malloc(s.dev, total, &s.dws, false);
+    if (e == hipSuccess) s.dws_bytes = total;
     if (e != hipSuccess)
         return fail(MPCQP_ENOMEM, "hipMalloc(%zu bytes) failed: %s", total, hipGetErrorString(e));
     HIPCHK(hipMemset(s.dws, 0, total));
@@ -345,6 +432,57 @@ std::string choose_plan(int32_t n, int32_t m, const int32_t* Pp, const int32_t* 
     return err;
 }
 
+// Plans by sparsity pattern: the Control/MPC scripts set up a fresh osqp object, with the same
+// pattern, every control step (mpc_kinematics.py:194-198), and planning is most of a small
+// setup's host time (~0.8 ms at N = 20).  A few recent plans are kept; a hit compares the whole
+// pattern, the polish flag and the plan-choice overrides, so it returns exactly the plan
+// choose_plan would build.
+struct PlanKey {
+    int32_t n = 0, m = 0;
+    bool polish = false;
+    std::string env;
+    std::vector<int32_t> pat;
+    bool operator==(const PlanKey& o) const {
+        return n == o.n && m == o.m && polish == o.polish && env == o.env && pat == o.pat;
+    }
+};
+std::mutex g_plan_mu;
+std::vector<std::pair<PlanKey, Plan>> g_plans;  // most recently used last
+constexpr size_t kPlanCache = 8;
+
+std::string cached_plan(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
+                        const int32_t* Ai, const mpcqp_settings& st, Plan& pl) {
+    if (n <= 0 || m < 0 || Pp[n] < 0 || Ap[n] < 0) return choose_plan(n, m, Pp, Pi, Ap, Ai, st, pl);
+    PlanKey k;
+    k.n = n;
+    k.m = m;
+    k.polish = st.polish != 0;
+    const char* ev = getenv("MPCQP_ELIM");
+    const char* vv = getenv("MPCQP_VARIANT");
+    k.env = std::string(ev ? ev : "") + "|" + (vv ? vv : "");
+    k.pat.reserve(2 * ((size_t)n + 1) + (size_t)Pp[n] + (size_t)Ap[n]);
+    k.pat.insert(k.pat.end(), Pp, Pp + n + 1);
+    k.pat.insert(k.pat.end(), Pi, Pi + Pp[n]);
+    k.pat.insert(k.pat.end(), Ap, Ap + n + 1);
+    k.pat.insert(k.pat.end(), Ai, Ai + Ap[n]);
+    {
+        std::lock_guard<std::mutex> lk(g_plan_mu);
+        for (size_t i = g_plans.size(); i-- > 0;)
+            if (g_plans[i].first == k) {
+                pl = g_plans[i].second;
+                std::rotate(g_plans.begin() + i, g_plans.begin() + i + 1, g_plans.end());
+                return std::string();
+            }
+    }
+    std::string err = choose_plan(n, m, Pp, Pi, Ap, Ai, st, pl);
+    if (err.empty()) {
+        std::lock_guard<std::mutex> lk(g_plan_mu);
+        g_plans.emplace_back(std::move(k), pl);
+        if (g_plans.size() > kPlanCache) g_plans.erase(g_plans.begin());
+    }
+    return err;
+}
+
 int validate_settings(const mpcqp_settings& s) {
     if (!(s.rho > 0) || !(s.sigma > 0) || s.max_iter <= 0 || s.eps_abs < 0 || s.eps_rel < 0 ||
         (s.eps_abs == 0 && s.eps_rel == 0) || !(s.eps_prim_inf > 0) || !(s.eps_dual_inf > 0) ||
@@ -366,7 +504,7 @@ int make_handle(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi, cons
     if (settings) h->set = *settings;
     else mpcqp_default_settings(&h->set);
     if (int e = validate_settings(h->set)) return e;
-    std::string err = choose_plan(n, m, Pp, Pi, Ap, Ai, h->set, h->plan);
+    std::string err = cached_plan(n, m, Pp, Pi, Ap, Ai, h->set, h->plan);
     if (!err.empty()) {
         bool unsup = err.rfind("unsupported", 0) == 0;
         return fail(unsup ? MPCQP_EUNSUPPORTED : MPCQP_EINVAL, "%s", err.c_str());
@@ -502,14 +640,13 @@ int check_convex(mpcqp_handle* h) {
 void free_shard(Shard& s) {
     (void)hipSetDevice(s.dev);
     if (s.stream) (void)hipStreamSynchronize(s.stream);
-    if (s.dws) (void)hipFree(s.dws);
-    if (s.dplan) (void)hipFree(s.dplan);
-    if (s.hstage) (void)hipHostFree(s.hstage);
-    if (s.hin) (void)hipHostFree(s.hin);
-    if (s.ev0) (void)hipEventDestroy(s.ev0);
-    if (s.ev1) (void)hipEventDestroy(s.ev1);
-    if (s.last_ev) (void)hipEventDestroy(s.last_ev);
-    if (s.stream) (void)hipStreamDestroy(s.stream);
+    if (s.last_st && s.last_st != s.stream && s.last_ev)
+        (void)hipEventSynchronize(s.last_ev);  // a caller stream's last call
+    pool_free(s.dev, s.dws_bytes, s.dws, false);
+    pool_free(s.dev, s.dplan_bytes, s.dplan, false);
+    pool_free(s.dev, s.hstage_bytes, s.hstage, true);
+    pool_free(s.dev, s.hin_bytes, s.hin, true);
+    pool_stream_release(s);
     s = Shard{};
 }
 
@@ -519,7 +656,8 @@ void free_shard(Shard& s) {
 // Everything a solve carries from call to call moves over unchanged: the scaled data and
 // the scaling, the iterates x, z, y, each instance's rho and row classes, its last status,
 // info and certificates, the setup inputs; the per-column arrays (q, D, x: padded order)
-// are permuted from the old padded index to the new one.  The factor is formed at the start
+// are permuted from the old padded index to the new one, and the scaled A values from the
+// old plan's padded-CSC order to the new one's.  The factor is formed at the start
 // of every solve, so nothing of it is kept.  The dispatch order restarts in identity order.
 int replan_plain(mpcqp_handle* h) {
     if (int e = sync_all(h)) return e;
@@ -551,7 +689,7 @@ int replan_plain(mpcqp_handle* h) {
             return 0;
         };
         const size_t D8 = sizeof(double), I4 = sizeof(int);
-        if ((rc = cp(b.Px, a.Px, D8 * B * old.nnzP)) || (rc = cp(b.Ax, a.Ax, D8 * B * old.nnzA)) ||
+        if ((rc = cp(b.Px, a.Px, D8 * B * old.nnzP)) ||
             (rc = cp(b.l, a.l, D8 * B * m)) || (rc = cp(b.u, a.u, D8 * B * m)) || (rc = cp(b.E, a.E, D8 * B * m)) ||
             (rc = cp(b.z, a.z, D8 * B * m)) || (rc = cp(b.y, a.y, D8 * B * m)) || (rc = cp(b.scal, a.scal, D8 * B * 4)) ||
             (rc = cp(b.dyc, a.dyc, D8 * B * m)) || (rc = cp(b.dxc, a.dxc, D8 * B * n)) ||
@@ -581,6 +719,20 @@ int replan_plain(mpcqp_handle* h) {
                 for (long j = 0; j < n; ++j) hn[i * npn + h->plan.var_pad[j]] = ho[i * npo + old.var_pad[j]];
             if (hipMemcpy(cols_new[t], hn.data(), D8 * B * npn, hipMemcpyHostToDevice) != hipSuccess)
                 rc = fail(MPCQP_EDEVICE, "re-plan: copy-in failed");
+        }
+        // the scaled A values: the padded-CSC order of each plan (k.Ax[e] = Ax[acsc_v[e]],
+        // kernels.hip::k_setup), user value v at csc_pos[v]
+        if (!rc && old.nnzA > 0) {
+            const long nz = old.nnzA;
+            std::vector<double> ao((size_t)B * nz), an((size_t)B * nz);
+            if (hipMemcpy(ao.data(), a.Ax, D8 * B * nz, hipMemcpyDeviceToHost) != hipSuccess) {
+                rc = fail(MPCQP_EDEVICE, "re-plan: copy-out failed");
+            } else {
+                for (long i = 0; i < B; ++i)
+                    for (long v = 0; v < nz; ++v) an[i * nz + h->plan.csc_pos[v]] = ao[i * nz + old.csc_pos[v]];
+                if (hipMemcpy(b.Ax, an.data(), D8 * B * nz, hipMemcpyHostToDevice) != hipSuccess)
+                    rc = fail(MPCQP_EDEVICE, "re-plan: copy-in failed");
+            }
         }
         if (rc) break;
         (void)hipSetDevice(ns.dev);
@@ -691,7 +843,10 @@ int mpcqp_update_batch(mpcqp_handle* h, const double* q, const double* l, const 
         if (int e = stream_enter(s, s.stream)) return e;
         const long Bs = s.B;
         if (in_bytes(Bs) <= kStageMax) {
-            if (!s.hin) HIPCHK(hipHostMalloc((void**)&s.hin, in_bytes(Bs), hipHostMallocDefault));
+            if (!s.hin) {
+                HIPCHK(pool_malloc(s.dev, in_bytes(Bs), (void**)&s.hin, true));
+                s.hin_bytes = in_bytes(Bs);
+            }
             double *hq = (double*)s.hin, *hl = hq + Bs * n, *hu = hl + Bs * m;
             int* herr = (int*)(hu + Bs * m);
             if (q) {
@@ -891,7 +1046,10 @@ int mpcqp_solve_batch(mpcqp_handle* h, double* x, double* y, int32_t* status, in
         HIPCHK(hipSetDevice(s.dev));
         const size_t sb = stage_bytes(h, s.B);
         if (sb <= kStageMax) {
-            if (!s.hstage) HIPCHK(hipHostMalloc((void**)&s.hstage, sb, hipHostMallocDefault));
+            if (!s.hstage) {
+                HIPCHK(pool_malloc(s.dev, sb, (void**)&s.hstage, true));
+                s.hstage_bytes = sb;
+            }
             const Stage g = stage_of(h, s);
             const long Bs = s.B;
             auto cp = [&](void* dst, const void* src, size_t bytes) -> int {

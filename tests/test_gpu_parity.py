@@ -1008,9 +1008,33 @@ def test_nonconvex_eliminated_slack_raises_like_osqp():
         h.setup(P, b["q"], b["A"], b["l"], b["u"], Px=Px, Ax=b["Ax"], **s)
     h.setup(P, b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
     assert h.plan_info()["n_eliminated"] > 0
-    assert (h.solve().status_val == 1).all()
     with pytest.raises(ValueError, match="instance 5"):
         h.update(Px=Px)
+    # After a solve the KKT matrix is refactored with the rho vector the solve adapted to
+    # (orc_update_P_A, OSQP 0.6 osqp_update_P_A): instance 5's rho grew (200 iterations,
+    # one rho update), so sigma + rho a^2 now outweighs a weight of -10 and OSQP accepts the
+    # update -- and so must the device; a weight of -1000 is refused by both.
+    for w, refused in ((-10.0, False), (-1000.0, True)):
+        Px[5, pos] = w
+        Pk.data = Px[5].copy()
+        Ak = b["A"].copy()
+        Ak.data = b["Ax"][5].copy()
+        Pg = P.copy()
+        Pg.data = b["Px"][5].copy()
+        o = pyoracle.OSQP()
+        o.setup(Pg, b["q"][5], Ak, b["l"][5], b["u"][5], **s)
+        o.solve()
+        h = OSQPBatch()
+        h.setup(P, b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
+        assert (h.solve().status_val == 1).all()
+        if refused:
+            with pytest.raises(ValueError):
+                o.update(Px=Pk.data)
+            with pytest.raises(ValueError, match="instance 5"):
+                h.update(Px=Px)
+        else:
+            o.update(Px=Pk.data)
+            h.update(Px=Px)
 
 
 @pytest.mark.parametrize("cfg,B", [(2, 64), (3, 48), (5, 12)])
