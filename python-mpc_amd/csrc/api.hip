@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -29,6 +31,29 @@ using namespace mpcqp;
 namespace {
 
 thread_local std::string g_err;
+
+// MPCQP_SETUP_TRACE=1 (diagnostic): the host-side stages of a setup call, in microseconds
+// since the previous mark, on stderr
+struct SetupTrace {
+    bool on = false;
+    std::chrono::steady_clock::time_point t;
+    SetupTrace() {
+        const char* e = getenv("MPCQP_SETUP_TRACE");
+        on = e && e[0] == '1';
+        t = std::chrono::steady_clock::now();
+    }
+    void mark(const char* what) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "mpcqp setup: %-22s %8.1f us\n", what,
+                std::chrono::duration<double, std::micro>(now - t).count());
+        t = now;
+    }
+};
+SetupTrace& strace() {
+    static thread_local SetupTrace tr;
+    return tr;
+}
 
 int fail(int code, const char* fmt, ...) {
     char buf[512];
@@ -82,6 +107,7 @@ struct Shard {
     char* hstage = nullptr;
     char* hin = nullptr;  // ... and of update()'s q, l, u and the error flags it reads back
     size_t dws_bytes = 0, dplan_bytes = 0, hstage_bytes = 0, hin_bytes = 0;  // (resource pool keys)
+    unsigned long long dplan_tag = 0;  // Plan::uid of the device plan copy
     KParams kp{};
 };
 
@@ -133,7 +159,7 @@ void shape_params(const Plan& pl, KParams& k) {
 // 64 MiB pinned, 8 streams; past that, resources are released as before.  The pool is never
 // torn down (process exit reclaims it; no HIP call runs from a static destructor).
 struct ResPool {
-    struct Blk { int dev; size_t bytes; void* p; };
+    struct Blk { int dev; size_t bytes; void* p; unsigned long long tag; };
     struct Str { int dev; hipStream_t st; hipEvent_t e0, e1, el; };
     std::mutex mu;
     std::vector<Blk> dev, pin;
@@ -147,29 +173,40 @@ ResPool& respool() {
 constexpr size_t kPoolDev = 256u << 20, kPoolPin = 64u << 20;
 constexpr size_t kPoolStreams = 8;
 
-hipError_t pool_malloc(int dev, size_t bytes, void** out, bool pinned) {
+// tag: what a block holds (a device plan's Plan::uid; 0 nothing reusable).  A block with the
+// asked-for tag is preferred, and *hit says whether it was found (its contents are then the
+// same as the caller would write).
+hipError_t pool_malloc(int dev, size_t bytes, void** out, bool pinned, unsigned long long tag = 0,
+                       bool* hit = nullptr) {
     ResPool& r = respool();
+    if (hit) *hit = false;
     {
         std::lock_guard<std::mutex> lk(r.mu);
         auto& v = pinned ? r.pin : r.dev;
+        size_t pick = v.size();
         for (size_t i = v.size(); i-- > 0;)
             if (v[i].dev == dev && v[i].bytes == bytes) {
-                *out = v[i].p;
-                (pinned ? r.pin_total : r.dev_total) -= bytes;
-                v.erase(v.begin() + i);
-                return hipSuccess;
+                if (tag && v[i].tag == tag) { pick = i; break; }
+                if (pick == v.size()) pick = i;
             }
+        if (pick < v.size()) {
+            *out = v[pick].p;
+            if (hit) *hit = tag && v[pick].tag == tag;
+            (pinned ? r.pin_total : r.dev_total) -= bytes;
+            v.erase(v.begin() + pick);
+            return hipSuccess;
+        }
     }
     return pinned ? hipHostMalloc(out, bytes, hipHostMallocDefault) : hipMalloc(out, bytes);
 }
-void pool_free(int dev, size_t bytes, void* p, bool pinned) {
+void pool_free(int dev, size_t bytes, void* p, bool pinned, unsigned long long tag = 0) {
     if (!p) return;
     ResPool& r = respool();
     {
         std::lock_guard<std::mutex> lk(r.mu);
         size_t& tot = pinned ? r.pin_total : r.dev_total;
         if (tot + bytes <= (pinned ? kPoolPin : kPoolDev)) {
-            (pinned ? r.pin : r.dev).push_back({dev, bytes, p});
+            (pinned ? r.pin : r.dev).push_back({dev, bytes, p, tag});
             tot += bytes;
             return;
         }
@@ -224,8 +261,10 @@ int upload_plan(const Plan& pl, Shard& s) {
         flat.push_back(0);  // never allocate zero-length parts
     }
     s.dplan_bytes = flat.size() * sizeof(int);
-    HIPCHK(pool_malloc(s.dev, s.dplan_bytes, (void**)&s.dplan, false));
-    HIPCHK(hipMemcpy(s.dplan, flat.data(), flat.size() * sizeof(int), hipMemcpyHostToDevice));
+    s.dplan_tag = pl.uid;
+    bool have = false;  // a pooled copy of this very plan (a fresh handle of the same pattern)
+    HIPCHK(pool_malloc(s.dev, s.dplan_bytes, (void**)&s.dplan, false, pl.uid, &have));
+    if (!have) HIPCHK(hipMemcpy(s.dplan, flat.data(), flat.size() * sizeof(int), hipMemcpyHostToDevice));
     const int** dst[] = {&s.kp.pad_var, &s.kp.acsc_ptr, &s.kp.acsc_row, &s.kp.acsc_v, &s.kp.acsr_ptr,
                          &s.kp.acsr_col, &s.kp.acsr_v, &s.kp.psym_ptr, &s.kp.psym_col, &s.kp.psym_v,
                          &s.kp.p_r, &s.kp.p_c, &s.kp.a_r, &s.kp.a_c, &s.kp.asm_blk_ptr, &s.kp.asm_tgt,
@@ -265,7 +304,9 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
     const Plan& pl = h->plan;
     HIPCHK(hipSetDevice(s.dev));
     if (int e = pool_stream(s)) return e;
+    strace().mark("stream");
     if (int e = upload_plan(pl, s)) return e;
+    strace().mark("plan upload");
     const long B = s.B, n = pl.n, m = pl.m, np = pl.npad, nb = pl.nb;
     const long SS = (long)kS * kS;
     size_t total = workspace_bytes(pl, B, with_io);
@@ -273,7 +314,9 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
     if (e == hipSuccess) s.dws_bytes = total;
     if (e != hipSuccess)
         return fail(MPCQP_ENOMEM, "hipMalloc(%zu bytes) failed: %s", total, hipGetErrorString(e));
-    HIPCHK(hipMemset(s.dws, 0, total));
+    strace().mark("workspace alloc");
+    HIPCHK(hipMemsetAsync(s.dws, 0, total, s.stream));
+    strace().mark("workspace memset");
     char* base = (char*)s.dws;
     size_t off = 0;
     KParams& k = s.kp;
@@ -305,10 +348,9 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
     k.err = (int*)(base + carve<int>(off, B));
     {  // dispatch order (kernels.hip::k_order), identity until the first solve
         int* ord = (int*)(base + carve<int>(off, B));
-        std::vector<int> id(B);
-        for (long i = 0; i < B; ++i) id[i] = (int)i;
-        HIPCHK(hipMemcpy(ord, id.data(), sizeof(int) * B, hipMemcpyHostToDevice));
+        HIPCHK(launch_iota(ord, B, s.stream));
         k.order = ord;
+        strace().mark("order upload");
         if (const char* ev = getenv("MPCQP_DISPATCH"); ev && !strcmp(ev, "identity")) k.order = nullptr;  // A/B
     }
     int* const done = (int*)(base + carve<int>(off, 1));  // zero from the memset above
@@ -355,8 +397,13 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
         if (occ < 0) return fail(MPCQP_EDEVICE, "occupancy query for solve variant %d failed", k.variant);
         k.slots = (long)ncu * occ;
     }
+    strace().mark("variant + occupancy");
     k.self = (const KParams*)(base + carve<KParams>(off, 1));
-    HIPCHK(hipMemcpy((void*)k.self, &k, sizeof(KParams), hipMemcpyHostToDevice));
+    // the zeroing, the identity order and the parameter block in stream order, one wait for
+    // all three (callers then use the workspace from any stream or from the host)
+    HIPCHK(hipMemcpyAsync((void*)k.self, &k, sizeof(KParams), hipMemcpyHostToDevice, s.stream));
+    HIPCHK(hipStreamSynchronize(s.stream));
+    strace().mark("params upload");
     if (size_t lds = lds_kernel_bytes(k); lds > 160 * 1024)
         return fail(MPCQP_EUNSUPPORTED, "problem needs %zu bytes of LDS per instance (> 160 KiB)", lds);
     return 0;
@@ -400,6 +447,11 @@ std::string w4_misfit(const KParams& k) {
     return r.empty() ? "does not fit variant 17" : r;
 }
 
+unsigned long long next_plan_uid() {
+    static std::atomic<unsigned long long> c{0};
+    return ++c;
+}
+
 std::string choose_plan(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
                         const int32_t* Ai, const mpcqp_settings& st, Plan& pl) {
     const char* ev = getenv("MPCQP_ELIM");
@@ -414,6 +466,7 @@ std::string choose_plan(int32_t n, int32_t m, const int32_t* Pp, const int32_t* 
             k.mode = 2;
             if (variant_fits(k, 17)) {
                 pl.choice = 1;
+                pl.uid = next_plan_uid();
                 return err;
             }
             choice = 2;
@@ -425,6 +478,7 @@ std::string choose_plan(int32_t n, int32_t m, const int32_t* Pp, const int32_t* 
         }
     }
     std::string err = build_plan(n, m, Pp, Pi, Ap, Ai, pl, false);
+    pl.uid = next_plan_uid();
     pl.choice = choice;
     pl.choice_note = note;
     if (const char* lg = getenv("MPCQP_PLAN_LOG"); lg && lg[0] == '1' && !note.empty())
@@ -504,7 +558,9 @@ int make_handle(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi, cons
     if (settings) h->set = *settings;
     else mpcqp_default_settings(&h->set);
     if (int e = validate_settings(h->set)) return e;
+    strace().mark("(enter)");
     std::string err = cached_plan(n, m, Pp, Pi, Ap, Ai, h->set, h->plan);
+    strace().mark("plan");
     if (!err.empty()) {
         bool unsup = err.rfind("unsupported", 0) == 0;
         return fail(unsup ? MPCQP_EUNSUPPORTED : MPCQP_EINVAL, "%s", err.c_str());
@@ -617,6 +673,55 @@ Stage stage_of(const mpcqp_handle* h, const Shard& s) {
 // definite -- the reduced matrix the solve kernels factor): one factor-only launch of the
 // solve kernel per shard, which stops after the first factorisation and marks an instance
 // whose factorisation fails as non-convex.  The first such instance is reported.
+// The setup's invalid-data flags (check_err_flags) and osqp_setup's convexity test
+// (check_convex) behind the setup kernel with one synchronisation: the factor-only launch is
+// enqueued right after it, and both the flags and the statuses come back through the shard's
+// pinned staging (update()'s, allocated here) in stream order.  Invalid data is reported
+// first, as the two checks in turn would.
+int check_setup(mpcqp_handle* h) {
+    const long n = h->n, m = h->m;
+    std::vector<int*> got(h->shards.size(), nullptr);
+    std::vector<std::vector<int>> host(h->shards.size());
+    for (size_t si = 0; si < h->shards.size(); ++si) {
+        Shard& s = h->shards[si];
+        HIPCHK(hipSetDevice(s.dev));
+        if (int e = stream_enter(s, s.stream)) return e;
+        HIPCHK(launch_solve(s.kp, s.B, s.out_x, s.out_y, 1, s.stream));
+        const size_t ib = sizeof(double) * (size_t)s.B * (n + 2 * m) + sizeof(int) * (size_t)s.B;
+        if (ib <= kStageMax) {
+            if (!s.hin) {
+                HIPCHK(pool_malloc(s.dev, ib, (void**)&s.hin, true));
+                s.hin_bytes = ib;
+            }
+            got[si] = (int*)s.hin;  // err (B), then status (B)
+            HIPCHK(hipMemcpyAsync(got[si], s.kp.err, sizeof(int) * s.B, hipMemcpyDeviceToHost, s.stream));
+            HIPCHK(hipMemcpyAsync(got[si] + s.B, s.kp.status, sizeof(int) * s.B, hipMemcpyDeviceToHost, s.stream));
+        }
+        if (int e = stream_leave(s, s.stream)) return e;
+    }
+    if (int e = sync_all(h)) return e;
+    for (size_t si = 0; si < h->shards.size(); ++si) {
+        Shard& s = h->shards[si];
+        if (!got[si]) {
+            host[si].resize(2 * s.B);
+            HIPCHK(hipSetDevice(s.dev));
+            HIPCHK(hipMemcpy(host[si].data(), s.kp.err, sizeof(int) * s.B, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(host[si].data() + s.B, s.kp.status, sizeof(int) * s.B, hipMemcpyDeviceToHost));
+            got[si] = host[si].data();
+        }
+    }
+    for (size_t si = 0; si < h->shards.size(); ++si)
+        for (long i = 0; i < h->shards[si].B; ++i)
+            if (got[si][i])
+                return fail(MPCQP_EINVAL, "instance %ld: invalid data (l > u or NaN bounds)", h->shards[si].b0 + i);
+    for (size_t si = 0; si < h->shards.size(); ++si)
+        for (long i = 0; i < h->shards[si].B; ++i)
+            if (got[si][h->shards[si].B + i] == MPCQP_NON_CVX_)
+                return fail(MPCQP_ENONCVX, "instance %ld: P is not convex (the KKT matrix is not quasi-definite)",
+                            h->shards[si].b0 + i);
+    return 0;
+}
+
 int check_convex(mpcqp_handle* h) {
     for (auto& s : h->shards) {
         HIPCHK(hipSetDevice(s.dev));
@@ -643,7 +748,7 @@ void free_shard(Shard& s) {
     if (s.last_st && s.last_st != s.stream && s.last_ev)
         (void)hipEventSynchronize(s.last_ev);  // a caller stream's last call
     pool_free(s.dev, s.dws_bytes, s.dws, false);
-    pool_free(s.dev, s.dplan_bytes, s.dplan, false);
+    pool_free(s.dev, s.dplan_bytes, s.dplan, false, s.dplan_tag);
     pool_free(s.dev, s.hstage_bytes, s.hstage, true);
     pool_free(s.dev, s.hin_bytes, s.hin, true);
     pool_stream_release(s);
@@ -820,11 +925,12 @@ int mpcqp_setup_batch(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi
         HIPCHK(launch_setup(s.kp, Bs, s.in_Px, s.in_Ax, s.in_q, s.in_l, s.in_u, s.stream));
         return stream_leave(s, s.stream);
     };
+    strace().mark("handle");
     for (auto& s : h->shards)
         if (int e = upload(s)) { mpcqp_free(h); return e; }
-    if (int e = sync_all(h)) { mpcqp_free(h); return e; }
-    if (int e = check_err_flags(h)) { mpcqp_free(h); return e; }
-    if (int e = check_convex(h)) { mpcqp_free(h); return e; }
+    strace().mark("inputs + setup launch");
+    if (int e = check_setup(h)) { mpcqp_free(h); return e; }
+    strace().mark("setup + convexity wait");
     *out = h;
     return 0;
 }

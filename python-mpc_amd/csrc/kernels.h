@@ -94,6 +94,8 @@ hipError_t launch_warm(const KParams& p, long B, const double* x, const double* 
 // longest-processing-time dispatch: sort the instances by the iteration count of the
 // solve just run (descending) into p.order, for the next solve on this workspace
 hipError_t launch_order(const KParams& p, long B, hipStream_t st);
+// order[i] = i (the identity dispatch order of a fresh workspace), enqueued on st
+hipError_t launch_iota(int* order, long B, hipStream_t st);
 int solve_variant(const KParams& p);  // -1: no instantiation fits the plan
 int solve_mode(int variant);
 int solve_threads(int variant);  // workgroup size of the variant's kernel

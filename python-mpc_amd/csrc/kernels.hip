@@ -392,6 +392,15 @@ hipError_t launch_warm(const KParams& p, long B, const double* x, const double* 
     return hipGetLastError();
 }
 
+__global__ void k_iota(int* __restrict__ order, long B) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < B) order[i] = (int)i;
+}
+hipError_t launch_iota(int* order, long B, hipStream_t st) {
+    hipLaunchKernelGGL(k_iota, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, order, B);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ order --
 // Dispatch order for the next solve on this workspace: longest previous solve first.
 // A batch larger than the resident slots (cfg 2: 1024 instances, 512 two-wave

@@ -88,6 +88,9 @@ struct Plan {
     // says which precondition failed), 3 nothing to eliminate
     int choice = 0;
     std::string choice_note;
+    // identity of the plan's contents (api.hip: a fresh value per build, kept by the plan cache's
+    // copies), so that a pooled device copy of the same plan is reused without an upload
+    unsigned long long uid = 0;
 };
 
 // Returns "" on success, otherwise an error message.  eliminate: take degree <= 1
