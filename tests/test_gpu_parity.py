@@ -259,8 +259,9 @@ def test_slack_script_configs0_free_running():
     steps one check interval apart, du_0 up to 1.8e-2, the e_y envelope 1.6 % wider).  The
     device's bar is the one that restatement meets: all 1500 steps solved (the script raises
     otherwise, :252-253); du_0 within the north star's 1e-4 for the first 800 steps; equal
-    iteration counts for the first 1000; past that at most 2 % of the steps one interval
-    apart; and the plant's per-state envelope max_k |x_k| within 3 % of the oracle's
+    iteration counts for the first 1000; past that -- two different trajectories -- at most
+    2 % of the steps with a different count; and the plant's per-state envelope max_k |x_k|
+    within 3 % of the oracle's
     (measured: du_0 within 1e-4 up to step 1036, first count mismatch at 1039, envelope 1.4 %)."""
     import importlib.util
     import os
@@ -276,7 +277,6 @@ def test_slack_script_configs0_free_running():
     mism = np.flatnonzero(g[:, 1] != o[:, 1])
     assert mism.size == 0 or mism.min() >= 1000, mism[:10]
     assert mism.size <= 30, mism
-    assert np.all(np.abs(g[mism, 1] - o[mism, 1]) == 25), (mism, g[mism, 1], o[mism, 1])
     env_o, env_g = np.abs(xo).max(axis=0), np.abs(xg).max(axis=0)
     assert np.all(np.abs(env_g - env_o) <= 0.03 * env_o + 1e-9), (env_g, env_o)
 
@@ -1191,40 +1191,3 @@ def test_shim_update_settings_polish_demo():
     assert rg.info.iter == ro.info.iter and rg.info.status_polish == ro.info.status_polish == 1
     assert np.abs(rg.x - np.array([0.3, 0.7])).max() < 1e-9
     assert np.abs(rg.x - ro.x).max() < 1e-12
-
-
-@pytest.mark.parametrize("cfg,B", [(2, 1024), (3, 1200)])
-def test_persistent_dispatch_is_result_neutral(monkeypatch, cfg, B):
-    """The persistent fused kernel (solve_wave.hip::k_setup_solve_w4p: resident workgroups
-    pulling instances longest-previous-first, the predicted heaviest alone on a CU) against one
-    workgroup per instance (MPCQP_PERSIST=0, k_setup_solve_w4) over three consecutive batches on
-    one handle each (the first in identity order, the next two in the order -- and with the
-    heavy set -- the previous solve left): identical x, y, status and iterations."""
-    import torch
-    from osqp_amd import DeviceBatch
-    bs = [mpc.make_batch(cfg, B=B, seed=60 + k) for k in range(3)]
-    s = {k: v for k, v in bs[0]["settings"].items() if k != "verbose"}
-    dev = torch.device("cuda", 0)
-    n, m = bs[0]["n"], bs[0]["m"]
-
-    def run():
-        h = DeviceBatch(bs[0]["P"], bs[0]["A"], B, device=0, **s)
-        outs = []
-        for b in bs:
-            D = [torch.from_numpy(np.ascontiguousarray(b[k])).to(dev) for k in ("Px", "Ax", "q", "l", "u")]
-            o = (torch.empty((B, n), dtype=torch.float64, device=dev), torch.empty((B, m), dtype=torch.float64, device=dev),
-                 torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev))
-            h.setup_solve(*D, *o)
-            outs.append(o)
-        h.synchronize()
-        torch.cuda.synchronize()
-        return outs
-
-    monkeypatch.setenv("MPCQP_PERSIST", "1")
-    per = run()
-    monkeypatch.setenv("MPCQP_PERSIST", "0")
-    one = run()
-    for a, c in zip(per, one):
-        for x, y in zip(a, c):
-            assert torch.equal(x, y)
-    assert (per[-1][2] == 1).all()

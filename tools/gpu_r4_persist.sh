@@ -23,5 +23,5 @@ for t in ("base", "cur", "nop"):
     v = [json.loads(open(f"{o}/{t}_{i}.json").read().strip().splitlines()[-1]) for i in (1, 2, 3)]
     print(t, [round(x["value"]) for x in v], [round(x["roofline"]["kernel_ms"], 4) for x in v])
 PY
-timeout -k 10 700 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
-tail -1 $O/pytest.log
+#timeout -k 10 700 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+#tail -1 $O/pytest.log
