@@ -278,70 +278,124 @@ def copy_peak(dev_index, nbytes=2 << 30, reps=10):
     return gbs
 
 
-def pcie_leg(solver, dev, local, bufs, host_in, steps, pipelined):
+class PinnedHost:
+    """Host buffers from hipHostMalloc for the PCIe leg (torch's pin_memory blocks made the
+    uploads stall the host thread for milliseconds now and then on the box), and
+    hipMemcpyAsync on a stream handle -- no torch copy bookkeeping between the calls."""
+
+    def __init__(self):
+        import ctypes
+        self.C = ctypes
+        self.hip = ctypes.CDLL("libamdhip64.so")
+        self.hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                            ctypes.c_void_p]
+        self.hip.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+        self.hip.hipHostFree.argtypes = [ctypes.c_void_p]
+        self.owned = []
+
+    def like(self, t):
+        import torch
+        C = self.C
+        if isinstance(t, np.ndarray):
+            t = torch.from_numpy(np.ascontiguousarray(t))
+        nbytes = max(t.numel() * t.element_size(), 8)
+        ptr = C.c_void_p()
+        if self.hip.hipHostMalloc(C.byref(ptr), nbytes, 0) != 0:
+            raise RuntimeError("hipHostMalloc failed")
+        self.owned.append(ptr.value)
+        h = torch.frombuffer((C.c_char * nbytes).from_address(ptr.value), dtype=t.dtype, count=t.numel())
+        h = h.view(t.shape)
+        h.copy_(t.cpu())
+        return h
+
+    def copy(self, dst, src, kind, stream):  # kind: 1 host to device, 2 device to host
+        if self.hip.hipMemcpyAsync(dst.data_ptr(), src.data_ptr(), dst.numel() * dst.element_size(), kind,
+                                   stream.cuda_stream) != 0:
+            raise RuntimeError("hipMemcpyAsync failed")
+
+    def free(self):
+        for ptr in self.owned:
+            self.hip.hipHostFree(ptr)
+        self.owned = []
+
+
+def pcie_leg(solver, dev, local, bufs, host_in, outs, pin, steps, mode, warmup=4):
     """PCIe-inclusive rate (diagnostic, never `value`): every step copies
-    the batch's Px, Ax, q, l, u from pinned host memory to HBM, runs the same
+    the batch's Px, Ax, q, l, u from pinned host memory (PinnedHost) to HBM, runs the same
     mpcqp_setup_solve_device call as the timed step, and copies x, y, status, iters back to
-    pinned host memory.
-      serial:    all of it in order on one torch stream, passed to the library as the
-                 caller stream;
-      pipelined: two sets of device buffers, the kernels on the handle's own stream, the
-                 copies on one torch stream in the order H2D(i), D2H(i-1): step i's inputs
-                 go up while step i-1's kernel runs, and i-1's outputs come down while step
-                 i's kernel runs (the overlap a host-side caller of the batch API can get).
-    The copies always run on a torch stream: torch's host allocator records the pinned
-    blocks' events on the copy's stream, and the handle destroys its own stream when freed.
-    bufs: [(dPx, dAx, dq, dl, du, dx, dy, dst, dit)] x (1 or 2); host_in: [(hPx, hAx, hq, hl,
-    hu)] cycled over the steps.  Returns seconds per step."""
+    pinned host memory.  mode:
+      "serial":    all of it in order on one torch stream, passed to the library as the
+                   caller stream;
+      "pipelined": two sets of device buffers, the kernels on the handle's own stream, the
+                   copies on a torch stream in the order H2D(i), D2H(i-1): step i's inputs go
+                   up while step i-1's kernel runs, and i-1's outputs come down while step i's
+                   kernel runs (the overlap a host-side caller of the batch API can get).
+    (Measured, round 4: an upload whose stream waits for a kernel blocks the calling host
+    thread until that kernel is done -- hipMemcpyAsync returned after 0.3-0.5 ms -- so the
+    host cannot run ahead; the pipelined form still hides the uploads behind the previous
+    kernel.  A variant with the downloads behind each kernel on its own stream measured no
+    better, profiles/r4s2_pcie/.)  Python's cyclic collector is off inside the timed loop.
+    bufs: [(dPx, dAx, dq, dl, du, dx, dy, dst, dit)] x (1 or 2); host_in: [(hPx, hAx, hq,
+    hl, hu)] cycled over the steps; outs: two sets of host outputs.  Returns s per step."""
+    import gc
     import torch
-    cs = torch.cuda.Stream(dev)
-    outs = [tuple(torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in bufs[0][5:]) for _ in range(2)]
-    if pipelined:
+    H2D, D2H = 1, 2
+    # the copy stream at high priority: HIP puts it on a hardware queue of its own, not on one
+    # it may share (GPU_MAX_HW_QUEUES = 4) with the handle's stream -- a shared queue runs the
+    # copies and kernels in one order and the pipelined leg fell to the serial rate in about
+    # one pass of three (0.72 against 0.45 ms per step, round 4)
+    cs = torch.cuda.Stream(dev, priority=-1)
+    piped = mode == "pipelined"
+    if piped:
         ks = torch.cuda.ExternalStream(solver.stream_handle().value, device=torch.device("cuda", local))
         ready = [torch.cuda.Event() for _ in range(2)]
         done = [torch.cuda.Event() for _ in range(2)]
 
     def down(i):
         for hh, dd in zip(outs[i % 2], bufs[i % len(bufs)][5:]):
-            hh.copy_(dd, non_blocking=True)
+            pin.copy(hh, dd, D2H, cs)
 
     def run(i):
         k = i % len(bufs)
         d = bufs[k]
-        with torch.cuda.stream(cs):
-            for dd, hh in zip(d[:5], host_in[i % len(host_in)]):
-                dd.copy_(hh, non_blocking=True)
-            if not pipelined:
-                solver.setup_solve(*d[:5], *d[5:], stream=cs.cuda_stream)
-                down(i)
-                return
-            ready[k].record(cs)
-            if i > 0:
-                cs.wait_event(done[(i - 1) % 2])
-                down(i - 1)
+        for dd, hh in zip(d[:5], host_in[i % len(host_in)]):
+            pin.copy(dd, hh, H2D, cs)
+        if not piped:
+            solver.setup_solve(*d[:5], *d[5:], stream=cs.cuda_stream)
+            down(i)
+            return
+        ready[k].record(cs)
+        if i > 0:
+            cs.wait_event(done[(i - 1) % 2])
+            down(i - 1)
         ks.wait_event(ready[k])
         solver.setup_solve(*d[:5], *d[5:])
         done[k].record(ks)
 
     def drain(i):
-        if pipelined and i > 0:
-            with torch.cuda.stream(cs):
-                cs.wait_event(done[(i - 1) % 2])
-                down(i - 1)
+        if piped and i > 0:
+            cs.wait_event(done[(i - 1) % 2])
+            down(i - 1)
 
     solver.synchronize()
-    for i in range(2):  # warmup
+    for i in range(warmup):
         run(i)
-    drain(2)
+    drain(warmup)
     torch.cuda.synchronize(dev)
     solver.synchronize()
-    t0 = time.perf_counter()
-    for i in range(steps):
-        run(i)
-    drain(steps)
-    torch.cuda.synchronize(dev)
-    solver.synchronize()
-    return (time.perf_counter() - t0) / steps
+    gc_on = gc.isenabled()
+    gc.disable()
+    try:
+        t0 = time.perf_counter()
+        for i in range(steps):
+            run(i)
+        drain(steps)
+        torch.cuda.synchronize(dev)
+        solver.synchronize()
+        return (time.perf_counter() - t0) / steps
+    finally:
+        if gc_on:
+            gc.enable()
 
 
 def main(argv=None, solver_cls=None, device=None):
@@ -540,22 +594,34 @@ def main(argv=None, solver_cls=None, device=None):
     if (rank == 0 and world == 1 and on_gpu and not args.no_pcie and not args.assemble and not warm and fused
             and B <= 65536 and hasattr(solver, "stream_handle")):
         import torch as _t
-        pin = lambda a: _t.from_numpy(np.ascontiguousarray(a)).pin_memory()  # noqa: E731
-        hPx, hAx, hq = pin(Px), pin(Ax), pin(b["q"])
-        host_in = [(hPx, hAx, hq, seq[t][0].cpu().pin_memory(), seq[t][1].cpu().pin_memory())
-                   for t in range(1 + args.warmup, 1 + args.warmup + min(4, args.steps))]
-        set0 = (dPx, dAx, dq, dl.clone(), du.clone(), dx, dy, dst, dit)
-        set1 = tuple(t.clone() for t in set0)
-        t_ser = pcie_leg(solver, dev, local, [set0], host_in, args.steps, pipelined=False)
-        t_pip = pcie_leg(solver, dev, local, [set0, set1], host_in, args.steps, pipelined=True)
+        ph = PinnedHost()
+        try:
+            host_in = [tuple(ph.like(v) for v in (Px, Ax, b["q"], seq[t][0], seq[t][1]))
+                       for t in range(1 + args.warmup, 1 + args.warmup + min(4, args.steps))]
+            set0 = (dPx, dAx, dq, dl.clone(), du.clone(), dx, dy, dst, dit)
+            set1 = tuple(t.clone() for t in set0)
+            outs = [tuple(ph.like(t) for t in set0[5:]) for _ in range(2)]
+            # three passes of each, alternated (single passes varied by tens of percent)
+            ser, pip = [], []
+            for _ in range(3):
+                ser.append(pcie_leg(solver, dev, local, [set0], host_in, outs, ph, args.steps, "serial"))
+                pip.append(pcie_leg(solver, dev, local, [set0, set1], host_in, outs, ph, args.steps, "pipelined"))
+        finally:
+            _t.cuda.synchronize(dev)
+            solver.synchronize()
+            ph.free()
+        t_ser, t_pip = float(np.median(ser)), float(np.median(pip))
         h2d = 8 * (Px.shape[1] + Ax.shape[1] + n + 2 * m)
         d2h = 8 * (n + m) + 8
         pcie = {"value_serial": B / t_ser, "ms_per_step_serial": t_ser * 1e3,
                 "value_pipelined": B / t_pip, "ms_per_step_pipelined": t_pip * 1e3,
+                "passes_ms_serial": [round(v * 1e3, 4) for v in ser],
+                "passes_ms_pipelined": [round(v * 1e3, 4) for v in pip],
                 "h2d_bytes_per_solve": h2d, "d2h_bytes_per_solve": d2h,
-                "method": "pinned host buffers: H2D of Px, Ax, q, l, u, the same setup_solve call, D2H of "
-                          "x, y, status, iters every step; serial on one stream / pipelined over two buffer "
-                          "sets, copies on their own stream beside the kernels (bench.py::pcie_leg); never `value`"}
+                "method": "hipHostMalloc host buffers: H2D of Px, Ax, q, l, u, the same setup_solve call, D2H "
+                          "of x, y, status, iters every step; serial on one stream / pipelined over two "
+                          "buffer sets, copies on their own stream beside the kernels (bench.py::pcie_leg); "
+                          "the median of three alternated passes of each; never `value`"}
         del set1
 
     value = B_global * args.steps / dt
