@@ -596,7 +596,8 @@ def main(argv=None, solver_cls=None, device=None):
         import torch as _t
         ph = PinnedHost()
         try:
-            host_in = [tuple(ph.like(v) for v in (Px, Ax, b["q"], seq[t][0], seq[t][1]))
+            hPx, hAx, hq = ph.like(Px), ph.like(Ax), ph.like(b["q"])
+            host_in = [(hPx, hAx, hq, ph.like(seq[t][0]), ph.like(seq[t][1]))
                        for t in range(1 + args.warmup, 1 + args.warmup + min(4, args.steps))]
             set0 = (dPx, dAx, dq, dl.clone(), du.clone(), dx, dy, dst, dit)
             set1 = tuple(t.clone() for t in set0)
