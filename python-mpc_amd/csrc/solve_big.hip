@@ -234,10 +234,247 @@ __device__ __forceinline__ bool factorize2(const KP& p, SLds& L, double* __restr
     return ok;
 }
 
+// Gauss-Jordan of the rows in `piv` (bit r: row r; increasing order) of the tile T (row
+// stride S; LDS or the workspace) by one wave, in place: gj_seg's rolled step with any row
+// set.  Rows in `done` were pivoted before (the sign rule M_ij = -M_ji tells pivoted rows
+// apart).  Before the first pivot, corrections are added to the unpivoted corners:
+// dl[a * 16 + c] to T[o1 + a][o1 + c] (a, c < n1) and dl2 likewise at o2 / n2 (n = 0: none).
+// Rows of T are loaded into registers once and stored back once.  False on a non-positive
+// pivot.  buf: 2 S doubles of LDS.
+__device__ __forceinline__ bool gj_rows(double* __restrict__ T, double* __restrict__ buf, const unsigned piv,
+                                        const unsigned done, const double* __restrict__ dl, const int o1, const int n1,
+                                        const double* __restrict__ dl2, const int o2, const int n2) {
+    const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
+    double v[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; jj += 2) {
+        const double2 t2 = *(const double2*)(T + i * S + 16 * h + jj);
+        v[jj] = t2.x;
+        v[jj + 1] = t2.y;
+    }
+    if (n1 > 0 && i >= o1 && i < o1 + n1) {
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            const int c = 16 * h + jj - o1;
+            if (c >= 0 && c < n1) v[jj] += dl[(i - o1) * 16 + c];
+        }
+    }
+    if (n2 > 0 && i >= o2 && i < o2 + n2) {
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            const int c = 16 * h + jj - o2;
+            if (c >= 0 && c < n2) v[jj] += dl2[(i - o2) * 16 + c];
+        }
+    }
+    double minpiv = 1.0, sc = 1.0, iv = 1.0;
+    bool pivd = ((done >> i) & 1u) != 0;  // row i already pivoted
+    int slot = 0;  // the publish buffer alternates between the pivots taken
+#pragma unroll 1
+    for (int p = 0; p < S; ++p) {
+        if (!((piv >> p) & 1u)) continue;  // (uniform)
+        const int pj = __builtin_amdgcn_readfirstlane(p & 15), ph = p >> 4;
+        double* rb = buf + slot * S;
+        slot ^= 1;
+        if (h == ph) {
+            const double vp = sc * pick16(v, pj);
+            rb[i] = pivd ? -vp : vp;  // row p = +-column p
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const double pv = rb[p];
+        const double mi = rb[i];
+        double rowv[16];
+#pragma unroll
+        for (int jj = 0; jj < 16; jj += 2) {
+            const double2 r2 = *(const double2*)(rb + 16 * h + jj);
+            rowv[jj] = r2.x;
+            rowv[jj + 1] = r2.y;
+        }
+        const double colv = pivd ? -mi : mi;
+        minpiv = pv > 0.0 ? minpiv : -1.0;
+        double d = __builtin_amdgcn_rcp(pv);
+        d = __builtin_fma(d, __builtin_fma(-pv, d, 1.0), d);
+        d = __builtin_fma(d, __builtin_fma(-pv, d, 1.0), d);
+        const bool self = i == p;
+        const double cd = self ? 0.0 : (colv * d) * iv;
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) v[jj] = __builtin_fma(-cd, rowv[jj], v[jj]);
+        sc = self ? d : sc;
+        iv = self ? pv : iv;
+        if (h == ph) put16(v, pj, self ? 1.0 : -cd);
+        pivd = pivd || self;
+    }
+#pragma unroll
+    for (int jj = 0; jj < 16; jj += 2) *(double2*)(T + i * S + 16 * h + jj) = make_double2(sc * v[jj], sc * v[jj + 1]);
+    return minpiv > 0.0;
+}
+
+// The two-sided factorisation split like factorize_g (round 4): the Gauss-Jordan pivots that
+// do not wait for a neighbouring block come off the chain.  S_k (top), T_k (bottom) and M
+// (middle) differ from the assembled D_k only on the coupling corners -- rows [0, amax) for a
+// top block's link to block k-1, rows [toff_k, toff_k + bmax) for a bottom block's link to
+// block k+1, both for the middle -- so:
+//   stage 1, the eight waves over the blocks (wave w: k = w, w + 8, ...): fill D_k (zeros,
+//     the diagonal) in the workspace tile Sg[k] and E_k (rows < amax) in Fg[k], write every
+//     assembly target once, and pivot every row of D_k outside its corners (blocks 0 and
+//     nb-1 whole);
+//   the chain, both ends in lock-step: top k = 1 .. p-1: F_k = E_k S_{k-1}^{-1} over E_k's
+//     nonzero columns (LDS, then Fg[k]), the corner -F_k E_k', wave 0 pivots rows [0, amax);
+//     bottom k = nb-2 .. p+1: G_k = E_{k+1}[:, toff_k + .]' T_{k+1}^{-1}[0, amax) (LDS, then
+//     Hg[k]), the corner -G_k E_{k+1}, wave 4 pivots the tail rows;
+//   the middle: both products and corners, wave 0 pivots both row sets.
+// The chain's Gauss-Jordan is amax (bmax) pivots a step instead of 32, and stage 1 runs on
+// eight waves at once.  Same outputs as factorize2 (Sg: S_k^{-1} / M^{-1} / T_k^{-1}; Fg rows
+// < amax: F_k, k = 1..p; Hg rows < bmax: G_k, k = p..nb-2); the inverses agree at rounding
+// level (the pivot order differs).  Scratch: the LDS tiles of SLds (SP, DK, EK).
+template <int TT, class KP>
+__device__ __forceinline__ bool factorize2s(const KP& p, SLds& L, double rho, double* __restrict__ Fg,
+                                            double* __restrict__ Hg, double* __restrict__ Sg) {
+    constexpr int NW = TT / 64, HT = TT / 2;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, half = tid / HT, u = tid % HT;
+    const int nb = p.nb, amax = p.amax, bmax = p.bmax, pm = p.pmeet;
+    double* const Fl = L.SP;                   // F_k of the top step, amax x 32
+    double* const Gl = L.SP + 16 * S;          // G_k of the bottom step, bmax x 32
+    double* const dlt = L.SP + 32 * S;         // top corner correction, row stride 16
+    double* const dlb = dlt + 256;             // bottom corner correction
+    double* const bufw = dlb + 256 + w * 2 * S;
+    double* const okf = bufw + (NW - w) * 2 * S;  // NW flags after the buffers
+    auto gsync = []() __attribute__((always_inline)) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    };
+    auto rows = [&](int a, int n) -> unsigned { return n <= 0 ? 0u : (((n >= 32 ? ~0u : ((1u << n) - 1u))) << a); };
+#ifdef MPCQP_PHASE_PROF
+    long long tf = clock64();
+#define FPH(k) if (tid == 0) { const long long t_ = clock64(); L.pacc[k] += t_ - tf; tf = t_; }
+#else
+#define FPH(k)
+#endif
+    bool okw = true;
+    // stage 1
+#pragma unroll 1
+    for (int k = w; k < nb; k += NW) {
+        double* D = Sg + (long)k * SS;
+        double* E = Fg + (long)k * SS;
+        for (int e = 2 * lane; e < SS; e += 128) {
+            const int r = e >> 5, c = e & (S - 1);  // c even: the diagonal is (r, r)
+            const double dg = p.pad_var[k * S + r] >= 0 ? p.sigma : 1.0;
+            *(double2*)(D + e) = make_double2(c == r ? dg : 0.0, c + 1 == r ? dg : 0.0);
+        }
+        if (k > 0)
+            for (int e = 2 * lane; e < amax * S; e += 128) *(double2*)(E + e) = make_double2(0.0, 0.0);
+        gsync();
+        assemble_targets<false, false, true>(p, L, rho, k, D, E, lane, 64);
+        gsync();
+        unsigned cut = 0;
+        if (k > 0 && k <= pm) cut |= rows(0, amax);              // the link to block k-1
+        if (k < nb - 1 && k >= pm) cut |= rows(p.toff[k], bmax);  // the link to block k+1
+        const unsigned all = rows(0, p.bsize[k]);
+        okw = gj_rows(D, bufw, all & ~cut, 0u, nullptr, 0, 0, nullptr, 0, 0) && okw;
+    }
+    __syncthreads();
+    FPH(10)
+    const int ntop = pm - 1 > 0 ? pm - 1 : 0, nbot = nb - 2 - pm > 0 ? nb - 2 - pm : 0;
+    const int nst = ntop > nbot ? ntop : nbot;
+    // step s: top block kt = s (s <= ntop), bottom block kb = nb - 1 - s (s <= nbot); s = nst + 1:
+    // the middle block (both links)
+#pragma unroll 1
+    for (int s = 1; s <= nst + 1; ++s) {
+        const bool mid = s == nst + 1;
+        const int kt = mid ? pm : s, kb = mid ? pm : nb - 1 - s;
+        const bool top = mid ? pm > 0 : s <= ntop;
+        const bool bot = mid ? pm < nb - 1 : s <= nbot;
+        // products: F_kt (top half's threads), G_kb (bottom half's)
+        if (half == 0 && top) {
+            const double* Sp = Sg + (long)(kt - 1) * SS;
+            const double* E = Fg + (long)kt * SS;
+            const int l0 = p.toff[kt - 1];
+            for (int o = u; o < amax * S; o += HT) {
+                const int r = o >> 5, j = o & (S - 1);
+                double sacc = 0.0;
+                for (int l = l0; l < l0 + bmax; ++l) sacc += E[r * S + l] * Sp[l * S + j];
+                Fl[o] = sacc;
+            }
+        }
+        if (half == 1 && bot) {
+            const double* Tn = Sg + (long)(kb + 1) * SS;
+            const double* E = Fg + (long)(kb + 1) * SS;
+            const int to = p.toff[kb];
+            for (int o = u; o < bmax * S; o += HT) {
+                const int a = o >> 5, j = o & (S - 1);
+                double sacc = 0.0;
+                for (int r = 0; r < amax; ++r) sacc += E[r * S + to + a] * Tn[r * S + j];
+                Gl[o] = sacc;
+            }
+        }
+        __syncthreads();
+        // corners: -F E' (amax x amax), -G E_{kb+1} (bmax x bmax); F -> Fg[kt], G -> Hg[kb]
+        if (half == 0 && top) {
+            const double* E = Fg + (long)kt * SS;
+            const int l0 = p.toff[kt - 1];
+            if (u < amax * amax) {
+                const int r = u / amax, c = u - r * amax;
+                double sacc = 0.0;
+                for (int l = l0; l < l0 + bmax; ++l) sacc += Fl[r * S + l] * E[c * S + l];
+                dlt[r * 16 + c] = -sacc;
+            }
+        }
+        if (half == 1 && bot) {
+            const double* E = Fg + (long)(kb + 1) * SS;
+            const int to = p.toff[kb];
+            if (u < bmax * bmax) {
+                const int a = u / bmax, c = u - a * bmax;
+                double sacc = 0.0;
+                for (int r = 0; r < amax; ++r) sacc += Gl[a * S + r] * E[r * S + to + c];
+                dlb[a * 16 + c] = -sacc;
+            }
+            for (int o = u; o < bmax * S; o += HT) Hg[(long)kb * SS + o] = Gl[o];
+        }
+        __syncthreads();  // (E_kt's reads are done: F_kt may overwrite it in Fg[kt])
+        if (half == 0 && top)
+            for (int o = u; o < amax * S; o += HT) Fg[(long)kt * SS + o] = Fl[o];
+        FPH(9)
+        // corner pivots: wave 0 the top (or middle) block, wave NW/2 the bottom one
+        if (mid) {
+            if (w == 0) {
+                const unsigned ct = top ? rows(0, amax) : 0u;
+                const unsigned cb = bot ? rows(p.toff[pm], bmax) : 0u;
+                const unsigned all = rows(0, p.bsize[pm]);
+                okw = gj_rows(Sg + (long)pm * SS, bufw, (ct | cb) & all, all & ~(ct | cb), dlt, 0, top ? amax : 0,
+                              dlb, bot ? p.toff[pm] : 0, bot ? bmax : 0) && okw;
+            }
+        } else {
+            if (w == 0 && top) {
+                const unsigned c = rows(0, amax), all = rows(0, p.bsize[kt]);
+                okw = gj_rows(Sg + (long)kt * SS, bufw, c & all, all & ~c, dlt, 0, amax, nullptr, 0, 0) && okw;
+            }
+            if (w == NW / 2 && bot) {
+                const unsigned c = rows(p.toff[kb], bmax), all = rows(0, p.bsize[kb]);
+                okw = gj_rows(Sg + (long)kb * SS, bufw, c & all, all & ~c, nullptr, 0, 0, dlb, p.toff[kb], bmax) && okw;
+            }
+        }
+        __syncthreads();
+        FPH(11)
+    }
+#undef FPH
+    if (lane == 0) okf[w] = okw ? 1.0 : 0.0;
+    __syncthreads();
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) ok = ok && okf[k] > 0.5;
+    __syncthreads();  // (the flags are read before any later reuse of the scratch)
+    return ok;
+}
+
 template <int TT, class KP>
 __device__ __noinline__ bool factorize2_nl(const KP* gp, long b, double rho, double* X2) {
     const KPc& p = kconst(gp);
     SL2 C = carve(p);
+    if constexpr (TT == 512)  // (the two-wave variant 14 keeps the unsplit form)
+        return factorize2s<TT>(p, C.L, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
+                               p.Si + b * (long)p.nb * SS);
     return factorize2<TT>(p, C.L, X2, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
                           p.Si + b * (long)p.nb * SS);
 }
