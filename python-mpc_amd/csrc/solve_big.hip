@@ -526,9 +526,31 @@ __device__ __forceinline__ double dot4c(const double (&a)[4], const double (&v)[
 // dot products side by side.  Both halves run the same instruction stream with per-half
 // operands.  2 max(p, nb-1-p) + 1 barriers.  Same sums as the earlier read-only form
 // (w - corT - corB), which subtracted exact zeros for the other chain.
+// The LDS offsets of each step (twisted_solve), formed once per run instead of per step:
+// bits 0-15 the forward step's destination row offset kd S (+ toff_kd on the bottom chain),
+// bits 16-31 the backward step's x_{k+-1} offset.  Formed per step they were a dependent LDS
+// read (toff) in front of the step's own reads.
+template <int SL>
+__device__ __forceinline__ void step_offsets(const KParams& p, const int* toffL, int (&so)[SL]) {
+    const int half = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8));
+    const int nb = p.nb, pm = p.pmeet, nmine = half ? nb - 1 - pm : pm;
+#pragma unroll
+    for (int s = 0; s < SL; ++s) {
+        int f = 0, bk = 0;
+        if (s >= 1 && s <= nmine) {
+            const int kd = half ? nb - 1 - s : s;
+            f = kd * S + (half ? toffL[kd] : 0);
+            const int k = half ? pm + s : pm - s;
+            bk = half ? (k - 1) * S + toffL[k - 1] : (k + 1) * S;
+        }
+        so[s] = f | (bk << 16);
+        asm volatile("" : "+v"(so[s]));  // (in a VGPR: the kernel's scalar registers are spoken for)
+    }
+}
+
 template <int SL>
 __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KParams& p, const double* Fc,
-                                              const double* Gc, const int* toffL, double* rb, double* xt,
+                                              const double* Gc, const int (&so)[SL], double* rb, double* xt,
                                               double* corB, long long* pacc) {
 #ifdef MPCQP_PHASE_PROF
     long long t0s = clock64();
@@ -552,7 +574,7 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
         if (s <= nst) {
             if (s <= nmine) {
                 const int ks = half ? nb - s : s - 1, kd = half ? nb - 1 - s : s;
-                const int woff = kd * S + (half ? toffL[kd] : 0);
+                const int woff = so[s] & 0xFFFF;
                 const bool mid = half && kd == pm;
                 double* dst = (mid ? corB : rb) + woff + i;
                 const double old = (writer && lowrank && !mid) ? *dst : 0.0;
@@ -595,7 +617,7 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
         if (s <= nst) {
             if (s <= nmine) {
                 const int k = half ? pm + s : pm - s;
-                const double* x1 = xt + (half ? (k - 1) * S + toffL[k - 1] : (k + 1) * S);
+                const double* x1 = xt + (so[s] >> 16);
                 // H_k[i][r] = F_{k+1}[r][i] (top), G_{k-1}[r][i] (bottom); rows >= lim read as 0
                 const double* h = (half ? Gc + (k - 1 - pm) * bmax * FGS : Fc + k * amax * FGS) + i;
                 const double tk = xt[k * S + i];
@@ -881,6 +903,8 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
         // ---- run state (re-derived at every run start; nothing but scalars lives across calls) ----
         std::conditional_t<TTK == 512, TwoSided<NS + 1>, TwoSidedW<NS>> RF;
         RF.load(nb, p.pmeet, amax, p.bmax, Fg, Hg, Sg, Fc, Gc);
+        int so[NS + 1];  // (TTK == 512: twisted_solve's step offsets)
+        if constexpr (TTK == 512) step_offsets<NS + 1>(p, toffL, so);
         int cvar[CS];
         Gather<K> cg[CS];
 #pragma unroll
@@ -927,7 +951,7 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
 #else
             long long* pacc = nullptr;
 #endif
-            if constexpr (TTK == 512) twisted_solve<NS + 1>(RF, p, Fc, Gc, toffL, L.rb, L.xt, L.tv, pacc);
+            if constexpr (TTK == 512) twisted_solve<NS + 1>(RF, p, Fc, Gc, so, L.rb, L.xt, L.tv, pacc);
             else wave_twisted_solve<NS>(RF, p, Fc, Gc, toffL, L.rb, L.xt, L.cor, pacc);
             PH(2)
             // z~ = A x~ ; relaxed + projected z ; y ; next w.   x update; deltas for the checks.

@@ -10,7 +10,7 @@ timeout -k 10 700 python3 -u -m pytest tests -m gpu -x -q --timeout 200 --timeou
 tail -1 $O/pytest.log
 for i in 1 2; do
   for t in base cur; do
-    if [ $t = base ]; then pkg=$PWD/ab/base; else pkg=$PWD/python-mpc_amd; fi
+    if [ $t = base ]; then pkg=$PWD/ab/${AB_BASE:-base}; else pkg=$PWD/python-mpc_amd; fi
     MPCQP_PKG=$pkg timeout -k 10 300 python3 bench.py --no-cpu --no-dispatch-ab --config 5 --steps 5 --warmup 1 > $O/${t}_$i.json 2> $O/${t}_$i.err || { echo "$t failed"; tail -5 $O/${t}_$i.err; exit 1; }
     python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);print(sys.argv[2], round(d['value']), round(d['roofline']['kernel_ms'],3), d['config']['iters_mean'])" $O/${t}_$i.json $t
   done
