@@ -532,21 +532,29 @@ __device__ __forceinline__ double dot4c(const double (&a)[4], const double (&v)[
 // read (toff) in front of the step's own reads.
 // fo: the F / G row block of each step, in rows of the F / G region (FGS doubles): bits 0-15
 // the forward step's F_s (top) / G_kd (bottom), bits 16-31 the backward step's H_k.
+// All four are double offsets from the dynamic LDS base (sm), so a step forms its addresses
+// from registers alone (no reload of a spilled base pointer in front of its reads):
+//   so: bits 0-15 the forward step's destination row (rb or corB, + kd S + toff), bits 16-31
+//       the backward step's x_{k+-1} (xt + ...);  fo: the F / G rows of the forward step,
+//       bits 16-31 the backward step's H rows.
 template <int SL>
-__device__ __forceinline__ void step_offsets(const KParams& p, const int* toffL, int (&so)[SL], int (&fo)[SL]) {
+__device__ __forceinline__ void step_offsets(const KParams& p, const int* toffL, const double* rb, const double* xt,
+                                             const double* corB, const double* Fc, int (&so)[SL], int (&fo)[SL]) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
     const int half = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8));
     const int nb = p.nb, pm = p.pmeet, nmine = half ? nb - 1 - pm : pm;
     const int amax = p.amax, bmax = p.bmax, g0 = pm * amax;  // (Gc = Fc + g0 FGS)
+    const int orb = (int)(rb - sm), oxt = (int)(xt - sm), ocb = (int)(corB - sm), ofc = (int)(Fc - sm);
 #pragma unroll
     for (int s = 0; s < SL; ++s) {
         int f = 0, bk = 0, ff = 0, fb = 0;
         if (s >= 1 && s <= nmine) {
             const int kd = half ? nb - 1 - s : s;
-            f = kd * S + (half ? toffL[kd] : 0);
+            f = (half && kd == pm ? ocb : orb) + kd * S + (half ? toffL[kd] : 0);
             const int k = half ? pm + s : pm - s;
-            bk = half ? (k - 1) * S + toffL[k - 1] : (k + 1) * S;
-            ff = half ? g0 + (kd - pm) * bmax : (s - 1) * amax;
-            fb = half ? g0 + (k - 1 - pm) * bmax : k * amax;
+            bk = oxt + (half ? (k - 1) * S + toffL[k - 1] : (k + 1) * S);
+            ff = ofc + (half ? g0 + (kd - pm) * bmax : (s - 1) * amax) * FGS;
+            fb = ofc + (half ? g0 + (k - 1 - pm) * bmax : k * amax) * FGS;
         }
         so[s] = f | (bk << 16);
         fo[s] = ff | (fb << 16);
@@ -562,6 +570,7 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
     // PRE: the step offsets were formed at the run start (step_offsets); the long instantiation
     // (nb <= 24) has no registers for them and forms them per step
     constexpr bool PRE = SL <= 10;
+    extern __shared__ __attribute__((aligned(16))) double sm[];
 #ifdef MPCQP_PHASE_PROF
     long long t0s = clock64();
 #define SPH(k) if (pacc && threadIdx.x == 0) { const long long t_ = clock64(); pacc[k] += t_ - t0s; t0s = t_; }
@@ -584,13 +593,13 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
         if (s <= nst) {
             if (s <= nmine) {
                 const int ks = half ? nb - s : s - 1, kd = half ? nb - 1 - s : s;
-                const int woff = PRE ? so[s] & 0xFFFF : kd * S + (half ? toffL[kd] : 0);
+                const int woff = PRE ? 0 : kd * S + (half ? toffL[kd] : 0);
                 const bool mid = half && kd == pm;
-                double* dst = (mid ? corB : rb) + woff + i;
+                double* dst = PRE ? sm + (so[s] & 0xFFFF) + i : (mid ? corB : rb) + woff + i;
                 const double old = (writer && lowrank && !mid) ? *dst : 0.0;
                 const double* w = rb + ks * S;
                 const double v4[4] = {w[jg], w[jg + 8], w[jg + 16], w[jg + 24]};
-                const double* f = PRE ? Fc + ((fo[s] & 0xFFFF) + ir) * FGS
+                const double* f = PRE ? sm + (fo[s] & 0xFFFF) + ir * FGS
                                            : (half ? Gc + (kd - pm) * bmax * FGS : Fc + (s - 1) * amax * FGS) + ir * FGS;
                 const double f4[4] = {f[jg], f[jg + 8], f[jg + 16], f[jg + 24]};
                 const double t = reduce8(dot4c(R.Inv[s - 1], v4));
@@ -628,9 +637,9 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
         if (s <= nst) {
             if (s <= nmine) {
                 const int k = half ? pm + s : pm - s;
-                const double* x1 = xt + (PRE ? so[s] >> 16 : (half ? (k - 1) * S + toffL[k - 1] : (k + 1) * S));
+                const double* x1 = PRE ? sm + (so[s] >> 16) : xt + (half ? (k - 1) * S + toffL[k - 1] : (k + 1) * S);
                 // H_k[i][r] = F_{k+1}[r][i] (top), G_{k-1}[r][i] (bottom); rows >= lim read as 0
-                const double* h = PRE ? Fc + (fo[s] >> 16) * FGS + i
+                const double* h = PRE ? sm + (fo[s] >> 16) + i
                                            : (half ? Gc + (k - 1 - pm) * bmax * FGS : Fc + k * amax * FGS) + i;
                 const double tk = xt[k * S + i];
                 const int r0 = j0 < lim ? j0 : 0, r1 = j0 + 8 < lim ? j0 + 8 : 0;
@@ -916,7 +925,7 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
         std::conditional_t<TTK == 512, TwoSided<NS + 1>, TwoSidedW<NS>> RF;
         RF.load(nb, p.pmeet, amax, p.bmax, Fg, Hg, Sg, Fc, Gc);
         int so[NS + 1], fo[NS + 1];  // (TTK == 512, NS < 10: twisted_solve's step offsets)
-        if constexpr (TTK == 512 && NS < 10) step_offsets<NS + 1>(p, toffL, so, fo);
+        if constexpr (TTK == 512 && NS < 10) step_offsets<NS + 1>(p, toffL, L.rb, L.xt, L.tv, Fc, so, fo);
         int cvar[CS];
         Gather<K> cg[CS];
 #pragma unroll
