@@ -927,23 +927,26 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
         int so[NS + 1], fo[NS + 1];  // (TTK == 512, NS < 10: twisted_solve's step offsets)
         if constexpr (TTK == 512 && NS < 10) step_offsets<NS + 1>(p, toffL, L.rb, L.xt, L.tv, Fc, so, fo);
         int cvar[CS];
-        Gather<K> cg[CS];
+        // gather lists as LDS-base offsets (GatherR): A' w for the rhs, A x~ for the rows
+        extern __shared__ __attribute__((aligned(16))) double smb[];
+        const unsigned oA = (unsigned)(L.Acsc - smb), oW = (unsigned)(L.w - smb), oXt = (unsigned)(L.xt - smb);
+        GatherR<K> cg[CS];
 #pragma unroll
         for (int s = 0; s < CS; ++s) {
             const int pc = tid + s * TTK;
             cvar[s] = pc < npad ? p.pad_var[pc] : -1;
-            if (pc < npad) cg[s].load(p.gcol + pc, &p.self->npad);
-            else cg[s].clear(nnzA);
+            if (pc < npad) cg[s].load(p.gcol + pc, &p.self->npad, oA, oW);
+            else cg[s].clear(nnzA, oA, oW);
         }
-        Gather<K> rg[RS];
+        GatherR<K> rg[RS];
 #pragma unroll
         for (int s = 0; s < RS; ++s) {
             const int i = tid + s * TTK;
             if (i < m) {
-                rg[s].load(p.grow + i, &p.self->m);
+                rg[s].load(p.grow + i, &p.self->m, oA, oXt);
                 L.w[i] = rho_of(L.ct[i], rho) * Z[i] - y[s];  // w = rho z_prev - y (rho may be new)
             } else {
-                rg[s].clear(nnzA);
+                rg[s].clear(nnzA, oA, oXt);
             }
         }
         int stop_at = p.max_iter;
@@ -963,7 +966,7 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
             for (int s = 0; s < CS; ++s) {
                 const int pc = tido + s * TTK;
                 if (pc < npad)
-                    L.rb[pc] = cvar[s] >= 0 ? (sigma * X[pc] - L.qv[pc]) + cg[s].dot(L.Acsc, L.w) : 0.0;
+                    L.rb[pc] = cvar[s] >= 0 ? (sigma * X[pc] - L.qv[pc]) + cg[s].dot() : 0.0;
             }
             __syncthreads();
             PH(1)
@@ -980,7 +983,7 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
             for (int s = 0; s < RS; ++s) {
                 const int i = tido + s * TTK;
                 if (i < m) {
-                    const double zt = rg[s].dot(L.Acsc, L.xt);
+                    const double zt = rg[s].dot();
                     const signed char cl = L.ct[i];
                     const double rv = cl < 0 ? RHO_MIN : (cl > 0 ? r_hi : rho);
                     const double rvi = cl < 0 ? ri_lo : (cl > 0 ? ri_hi : ri_mid);

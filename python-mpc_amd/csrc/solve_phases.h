@@ -1061,6 +1061,42 @@ struct Gather {
     }
 };
 
+// Gather with both halves of an entry as double offsets from the dynamic LDS base (the
+// A value's and the vector element's), so a dot product forms its addresses from the entry
+// alone -- no base pointer (kept in a spilled SGPR by the long-horizon kernel) reloaded in
+// front of its reads.  oA / oV: the A values' and the vector's offsets from the base
+// (< 65536 doubles: LDS holds at most 20 K).
+template <int K>
+struct GatherR {
+    unsigned e[K];
+    __device__ __forceinline__ void load(const int* list, const volatile int* stride, unsigned oA, unsigned oV) {
+        const int st = *stride;
+        const unsigned o = oA + (oV << 16);
+#pragma unroll
+        for (int k = 0; k < K; ++k) e[k] = (unsigned)list[k * st] + o;
+    }
+    __device__ __forceinline__ void clear(int zero_pos, unsigned oA, unsigned oV) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) e[k] = (unsigned)zero_pos + oA + (oV << 16);
+    }
+    __device__ __forceinline__ double dot() const {
+        extern __shared__ __attribute__((aligned(16))) double sm[];
+        int opq = 0;
+        asm volatile("" : "+s"(opq));  // (Gather::dot: the unpacked addresses are not hoisted out of the loop)
+        double t[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const unsigned ek = e[k] + (unsigned)opq;
+            t[k] = sm[ek & 0xFFFFu] * sm[ek >> 16];
+        }
+#pragma unroll
+        for (int w = 1; w < K; w *= 2)
+#pragma unroll
+            for (int k = 0; k + w < K; k += 2 * w) t[k] += t[k + w];
+        return t[0];
+    }
+};
+
 struct Res {  // update_info results
     double pri, dua, nz, nax, nq, naty, npx;    // termination (unscaled)
     double rpri, rdua, rz, rax, rq, raty, rpx;  // rho estimate (scaled space)
