@@ -143,6 +143,11 @@ size_t carve(size_t& off, size_t count) {
 void shape_params(const Plan& pl, KParams& k) {
     k.n = pl.n; k.m = pl.m; k.nb = pl.nb; k.npad = pl.npad; k.nnzP = pl.nnzP; k.nnzA = pl.nnzA; k.amax = pl.amax;
     k.bmax = pl.bmax; k.pmeet = (pl.nb - 1) / 2;
+    k.bsz02 = k.bsz13 = 1 << 20;
+    if (pl.nb == 4) {
+        k.bsz02 = std::max(pl.bsize[0], pl.bsize[2]);
+        k.bsz13 = std::max(pl.bsize[1], pl.bsize[3]);
+    }
     k.gk = pl.gather_k; k.pk = pl.p_k; k.ntgt = pl.ntgt; k.term_max = pl.term_max;
     k.gk1 = 0;
     for (int i = 128; i < pl.m; ++i) k.gk1 = std::max(k.gk1, pl.acsr_ptr[i + 1] - pl.acsr_ptr[i]);
@@ -285,6 +290,7 @@ size_t workspace_bytes(const Plan& pl, long B, bool with_io) {
     carve<double>(off, B * np); carve<double>(off, B * m); carve<double>(off, B * m); // x z y
     carve<double>(off, B * 4);
     carve<double>(off, B * nb * SS); carve<double>(off, B * nb * SS); carve<double>(off, B * nb * SS);
+    carve<double>(off, B * dense_rows_doubles(pl.nb, pl.ne));       // Kd
     carve<double>(off, B * m); carve<double>(off, B * n);              // certificates
     for (int i = 0; i < 4; ++i) carve<double>(off, B);
     carve<signed char>(off, B * m);
@@ -334,6 +340,8 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
     k.F = (double*)(base + carve<double>(off, B * nb * SS));
     k.H = (double*)(base + carve<double>(off, B * nb * SS));
     k.Si = (double*)(base + carve<double>(off, B * nb * SS));
+    k.Kd = dense_rows_doubles(pl.nb, pl.ne) ? (double*)(base + carve<double>(off, B * dense_rows_doubles(pl.nb, pl.ne)))
+                                            : nullptr;
     k.dyc = (double*)(base + carve<double>(off, B * m));
     k.dxc = (double*)(base + carve<double>(off, B * n));
     k.obj = (double*)(base + carve<double>(off, B));

@@ -33,6 +33,7 @@ struct KParams {
     int gk1;          // most nonzeros in a row >= 128 (the two-wave kernel's second row slot)
     int gkr, gkc;     // most nonzeros in a row / a column of A (gk = the larger)
     int bmax, pmeet;  // two-sided factorisation (solve_big.hip): tail width, meeting block
+    int bsz02, bsz13; // largest of blocks 0 and 2 / 1 and 3 (real columns; nb = 4 plans)
     int variant;  // solve-kernel instantiation (solve.hip: launch_solve)
     int mode;     // factor storage of that variant (solve.hip: factorize)
     // plan
@@ -47,6 +48,7 @@ struct KParams {
     const int *eown, *etterm;
     // workspace
     double *Px, *Ax, *q, *D, *l, *u, *E, *x, *z, *y, *scal, *F, *H, *Si, *dyc, *dxc;
+    double* Kd;  // dense-inverse rows of the four-wave kernel's DK form (dense_rows_doubles per instance), or null
     double *obj, *pri, *dua, *rho_est;
     signed char* ct;
     int *status, *iter, *rho_upd, *err;
@@ -96,6 +98,10 @@ hipError_t launch_warm(const KParams& p, long B, const double* x, const double* 
 hipError_t launch_order(const KParams& p, long B, hipStream_t st);
 // order[i] = i (the identity dispatch order of a fresh workspace), enqueued on st
 hipError_t launch_iota(int* order, long B, hipStream_t st);
+// doubles per instance of the four-wave kernel's dense-inverse rows (KParams::Kd): 256 lanes x
+// (NB0 + NB1 = 54) for plans of four blocks without eliminated columns (solve_wave.hip, DK)
+constexpr long kDenseRowDoubles = 256L * 54;
+inline long dense_rows_doubles(int nb, int ne) { return nb == 4 && ne == 0 ? kDenseRowDoubles : 0; }
 int solve_variant(const KParams& p);  // -1: no instantiation fits the plan
 int solve_mode(int variant);
 int solve_threads(int variant);  // workgroup size of the variant's kernel

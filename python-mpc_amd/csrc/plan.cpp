@@ -37,6 +37,18 @@ std::vector<std::vector<int>> bfs_levels(const Graph& g, int s, std::vector<int>
     return levels;
 }
 
+// balanced four-block merge (build_plan), with the four-wave kernel's dense-inverse form;
+// MPCQP_DENSE_W4=1 turns both on (solve_wave.hip::dense_w4)
+bool balance_blocks() {
+    static const bool on = [] {
+        const char* b = getenv("MPCQP_BALANCE");  // (diagnostic override)
+        if (b) return b[0] != '0';
+        const char* e = getenv("MPCQP_DENSE_W4");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 }  // namespace
 
 std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
@@ -150,6 +162,25 @@ std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const
             blocks.back().insert(blocks.back().end(), L.begin(), L.end());
         else
             blocks.push_back(L);
+    }
+    if (!eliminate && blocks.size() == 4 && balance_blocks()) {
+        // balanced merge for the four-wave kernel's dense-inverse form (solve_wave.hip, DK):
+        // the smallest block capacity that still merges the levels into four blocks, so that
+        // no block has more real columns than the kernel's static per-block count (cfg 2:
+        // 31 / 30 / 30 / 13 -> 27 / 26 / 26 / 25).  Levels stay whole: the blocks stay
+        // block-tridiagonal with the same coupling rows at each block's top.
+        size_t tot = 0;
+        for (auto& L : all_levels) tot += L.size();
+        for (size_t cap = (tot + 3) / 4; cap < (size_t)kS; ++cap) {
+            std::vector<std::vector<int>> b2;
+            for (auto& L : all_levels) {
+                if (!b2.empty() && b2.back().size() + L.size() <= cap) b2.back().insert(b2.back().end(), L.begin(), L.end());
+                else b2.push_back(L);
+            }
+            bool fit = b2.size() == 4;
+            for (auto& B : b2) fit = fit && B.size() <= cap;
+            if (fit) { blocks.swap(b2); break; }
+        }
     }
     if (eliminate) {
         // greedy packing: consecutive runs of kS variables of the level order, a level split

@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "setup_r.h"
@@ -1036,12 +1037,90 @@ constexpr int T4 = 256;
 // factorize_w4) -- the elementwise back-substitution of the scalar Schur complement --
 // which the rows phase reads from xt like any other column.  Its termination-check column
 // is pe (the lower half keeps the block column).
+// DK (dense inverse, no eliminated columns): the three-phase solve x~ = L' D L b (L = I + the
+// G blocks below the diagonal, D = diag(S_k^{-1}); phases A, B, C above) replaced by one
+// product with M^{-1} = L' D L formed explicitly after each factorisation.  Lane (h, r) of
+// wave a keeps row a S + r of M^{-1} over the real columns of blocks 2 h and 2 h + 1 (the
+// first NBC of each: plan.cpp's balanced merge keeps every block at <= NBC real columns):
+//   rhs   -> barrier ->   x~ = M^{-1} b: 2 NBC FMAs per lane, one permlane32   -> barrier -> rows
+// Three barriers a step instead of four, and no phase whose length depends on the block
+// (the three-phase form's wave 3 runs three phase-A pairs, wave 0 two phase-C slots).
+// Block (a, b) of L' D L is  sum over k >= max(a, b) of  L_ka' S_k^{-1} L_kb  (L_kk = I, L_kj
+// = G_kj for j < k, nonzero rows < QR):
+//   [a = b] S_a^{-1}[i][c]
+//   + sum_q S_a^{-1}[i][q] G_ab[q][c]                       (a > b)
+//   + sum_q G_ba[q][i] S_b^{-1}[q][c]                       (b > a)
+//   + sum_{k > a, k > b} sum_q V_ka[i][q] G_kb[q][c],  V_ka[i][q] = sum_p G_ka[p][i] S_k^{-1}[p][q]
+// Each term is a sum of rank-one row updates: a lane coefficient times a row read from LDS
+// by broadcast (one row per half-wave).  G blocks come from the LDS copy gl (pair (k, j) at
+// k (k - 1) / 2 + j, pair NP the zero block: a lane whose b does not satisfy the term's
+// condition reads zeros), S_k^{-1} from the LDS tiles Sg.
+template <int O, int NBC>
+__device__ __forceinline__ void axpy_row(double* Kr, const double coef, const double* row) {
+#pragma unroll
+    for (int c = 0; c < NBC; c += 2) {
+        double v0, v1;
+        ld2(row + c, v0, v1);
+        Kr[O + c] += coef * v0;
+        Kr[O + c + 1] += coef * v1;
+    }
+}
+// columns [0, NBC) of block b = 2 h + BB (its real columns: plan.cpp's balanced merge keeps
+// them within NBC) of the lane's row r of block a, into Kr[O, O + NBC)
+template <int QR, int BB, int NBC, int O>
+__device__ __forceinline__ void dense_inverse_block(double* Kr, const double* Sg, const double* gl, int a, int h,
+                                                    int r) {
+    constexpr int NP = 6;
+    const int b = 2 * h + BB;  // the half's column block
+    auto pidx = [](int x, int y) { return y < x ? x * (x - 1) / 2 + y : NP; };
+    {   // [a = b] the lane's row of S_a^{-1}
+        const double* src = Sg + b * SS + r * S;
+        const bool diag = b == a;
+#pragma unroll
+        for (int c = 0; c < NBC; c += 2) {
+            double v0, v1;
+            ld2(src + c, v0, v1);
+            Kr[O + c] = diag ? v0 : 0.0;
+            Kr[O + c + 1] = diag ? v1 : 0.0;
+        }
+    }
+    const double* const Ta = Sg + a * SS;
+    if (a > BB) {  // (a > b) for some half (the lower half's b = BB is the smaller)
+        const double* g = gl + pidx(a, b) * 8 * S;
+#pragma unroll
+        for (int q = 0; q < QR; ++q) axpy_row<O, NBC>(Kr, Ta[r * S + q], g + q * S);
+    }
+    if (a < 2 + BB) {  // (b > a) for some half (the upper half's b = 2 + BB is the larger)
+        const double* g = gl + pidx(b, a) * 8 * S;
+        const double* Tb = Sg + b * SS;
+#pragma unroll
+        for (int q = 0; q < QR; ++q) axpy_row<O, NBC>(Kr, g[q * S + r], Tb + q * S);
+    }
+#pragma unroll 1
+    for (int k = max(a, BB) + 1; k < 4; ++k) {  // k > a, k > b for some half
+        const double* gka = gl + pidx(k, a) * 8 * S;
+        const double* gkb = gl + pidx(k, b) * 8 * S;
+        const double* Tk = Sg + k * SS;
+        double g[QR];
+#pragma unroll
+        for (int p = 0; p < QR; ++p) g[p] = gka[p * S + r];
+#pragma unroll
+        for (int q = 0; q < QR; ++q) {
+            double v = 0.0;
+#pragma unroll
+            for (int p = 0; p < QR; ++p) v += g[p] * Tk[p * S + q];
+            axpy_row<O, NBC>(Kr, v, gkb + q * S);
+        }
+    }
+}
+
 // K: row-list length, KC: column-list length (even: the rhs splits it over the half-waves).
 // factor_only: return after the first factorisation (the setup-time convexity check of
 // api.hip::check_convex); the fused setup + solve kernel passes 0
-template <int K, int KPK, int QR, bool EL = false, int KC = K>
+template <int K, int KPK, int QR, bool EL = false, int KC = K, bool DK = false>
 __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restrict__ xo, double* __restrict__ yo,
                                               int factor_only = 0) {
+    static_assert(!(DK && EL), "the dense inverse covers plans without eliminated columns");
     const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int h = lane >> 5, r = lane & 31;  // (rr, ch: per pass, below)
     constexpr int NB = 4, NP = NB * (NB - 1) / 2;  // exactly four blocks (solve.hip::variant_fits)
@@ -1114,6 +1193,14 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
     GatherW<KH> chs;  // the half's share of the block column's list (the rhs sums)
     GatherW<LE> el;   // EL: the eliminated column's list (zero entries for the other lanes)
     const bool rows_wave = w * 64 < mp;  // wave-uniform
+    // DK: the lane's half of row pc of M^{-1}: columns [0, NB0) of block 2 h and [0, NB1) of block
+    // 2 h + 1 (their real columns), formed after each factorisation.  NB0 = 26, NB1 = 28
+    // (dense_w4: bsize[0], bsize[2] <= 26 and bsize[1], bsize[3] <= 28; cfg 2's balanced
+    // blocks are 26 / 25 / 25 / 28)
+    constexpr int NB0 = 26, NB1 = 28;
+    static_assert(!DK || (NB0 + NB1) * T4 == kDenseRowDoubles, "KParams::Kd rows");
+    double Kr[DK ? NB0 + NB1 : 1];
+    constexpr int DKW = 8;  // DK: b values read per batch of the product (even)
     PH(5)
     for (;;) {
         // The lane's identity through an empty asm at each pass (opaque_v): the addresses and
@@ -1176,11 +1263,36 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
             }
             if (ri < m) rg.load(p.grow + ri, m, abase, xbase);  // by ri: duplicate lanes repeat its row
             else rg.clear(abase + 8u * nnzA, xbase);
+            if constexpr (DK) {
+                // M^{-1}'s rows formed once per factorisation and kept in the instance's Kd rows
+                // (lane-contiguous pairs): each run start reloads them, so that nothing lives in
+                // registers across the termination check -- the check's registers and the
+                // 108 of the rows do not fit together (spilled, and wrong in the divergent
+                // check: DESIGN.md §5)
+                __syncthreads();  // the G copy is complete
+                double Kf[NB0 + NB1];
+                dense_inverse_block<QR, 0, NB0, 0>(Kf, Sg, L.gl, w, h, r);
+                dense_inverse_block<QR, 1, NB1, NB0>(Kf, Sg, L.gl, w, h, r);
+                // (each pair's address: a wave-uniform base through an empty asm + the lane's
+                // index, formed at the store -- hoisted, the 27 64-bit addresses were spilled
+                // across the factorisation call)
+#pragma unroll
+                for (int j = 0; j < NB0 + NB1; j += 2)
+                    ((double2*)opaque_ptr(p.Kd + b * kDenseRowDoubles + (long)j * T4))[tid] = make_double2(Kf[j], Kf[j + 1]);
+            }
             PH(0)
         }
         // ---- run state ----
+        if constexpr (DK) {
+#pragma unroll
+            for (int j = 0; j < NB0 + NB1; j += 2) {
+                const double2 v = ((const double2*)opaque_ptr(p.Kd + b * kDenseRowDoubles + (long)j * T4))[tid];
+                Kr[j] = v.x;
+                Kr[j + 1] = v.y;
+            }
+        }
         double SB[16];
-        {
+        if constexpr (!DK) {
             const double* src = Sg + (long)w * SS + r * S + 16 * h;
 #pragma unroll
             for (int c = 0; c < 16; c += 2) ld2(src + c, SB[c], SB[c + 1]);
@@ -1222,7 +1334,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
         // iteration)
         double av[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) av[k] = lds_at(rg.e[k] & 0xFFFFu);
+        for (int k = 0; k < K; ++k) av[k] = DK ? 0.0 : lds_at(rg.e[k] & 0xFFFFu);
         const double rlo = L.lo[ri], rup = L.up[ri];
         const signed char cl = L.ct[ri];
         const double rv = cl < 0 ? RHO_MIN : (cl > 0 ? r_hi : rho);
@@ -1230,7 +1342,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
         __syncthreads();  // (the G copy of a refactorisation is complete)
         // phase A's G values (rows rr < 8 of G_wj, columns [4 ch, 4 ch + 4), j < w) in registers for the run
         double ga[NB - 1][4];
-        {
+        if constexpr (!DK) {
             const double* gq = L.gl + (w * (w - 1) / 2) * 8 * S + rr * S + 4 * ch;
 #pragma unroll
             for (int j = 0; j < NB - 1; ++j) {
@@ -1244,10 +1356,12 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
         }
         // phase C's G values (column r of the slots' pairs, rows < QR) in registers for the run
         double gc[2][QR];
+        if constexpr (!DK) {
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
+            for (int s = 0; s < 2; ++s)
 #pragma unroll
-            for (int q = 0; q < QR; ++q) gc[s][q] = s < nsw ? lds_at(gslot[s] + q * S * 8) : 0.0;
+                for (int q = 0; q < QR; ++q) gc[s][q] = s < nsw ? lds_at(gslot[s] + q * S * 8) : 0.0;
+        }
         if (rows_wave) L.w[ri] = rv * Z - y;  // (lanes past the padded rows may hold a stale y)
         int stop_at = p.max_iter;
         if (p.check_term) stop_at = min(stop_at, (iter / p.check_term + 1) * p.check_term);
@@ -1290,6 +1404,42 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
             }
             __syncthreads();
             PH(1)
+            if constexpr (DK) {
+                // x~[pc] = M^{-1}[pc] b: the half's NB0 + NB1 columns (broadcast reads, one address
+                // per half-wave), four FMA chains, one permlane32 swap
+                const double* const rbh = L.rb + 64 * h;
+                double a[4] = {0.0, 0.0, 0.0, 0.0};
+                // software-pipelined in windows of DKW values: window k + 1's reads are issued
+                // before window k's FMAs (two windows in flight; all 27 reads at once spill)
+                constexpr int NE = NB0 + NB1, NWIN = (NE + DKW - 1) / DKW;
+                double v[2][DKW];
+                auto issue = [&](int k, double (&dst)[DKW]) __attribute__((always_inline)) {
+#pragma unroll
+                    for (int c = 0; c < DKW; c += 2) {
+                        const int e = k * DKW + c;  // block 2 h column e, or block 2 h + 1 column e - NB0
+                        if (e < NE) ld2(rbh + (e < NB0 ? e : 32 + e - NB0), dst[c], dst[c + 1]);
+                    }
+                };
+                issue(0, v[0]);
+#pragma unroll
+                for (int k = 0; k < NWIN; ++k) {
+                    if (k + 1 < NWIN) issue(k + 1, v[(k + 1) & 1]);
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int c = 0; c < DKW; ++c)
+                        if (k * DKW + c < NE) a[c & 3] += Kr[k * DKW + c] * v[k & 1][c];
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                const double th = (a[0] + a[1]) + (a[2] + a[3]);
+                const unsigned lo = (unsigned)__double2loint(th), hi = (unsigned)__double2hiint(th);
+                const auto l2 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+                const auto h2 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+                const double xn = __hiloint2double((int)h2[0], (int)l2[0]) + __hiloint2double((int)h2[1], (int)l2[1]);
+                if (low) L.xt[pc] = xn;
+                const double xnew = alpha * xn + (1.0 - alpha) * X;
+                DX = xnew - X;
+                X = xnew;
+            } else {
             // A: c_w = sum_{j<w} G_wj b_j (rows < 8), wave w only
             if (w > 0) {
                 // one accumulator per pair (wave 3: three 4-deep FMA chains instead of one 12-deep)
@@ -1382,18 +1532,23 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 DX = xnew - X;
                 X = xnew;
             }
+            }  // !DK
             __syncthreads();
             PH(14)
             // rows: z~ = A x~ ; relaxed + projected z ; y ; next w (waves wholly past the
             // padded rows skip it: their lanes would only repeat the inert last row)
             if (rows_wave) {
-                double xv[K];
+                double xv[K], ar[K];
 #pragma unroll
                 for (int k = 0; k < K; ++k) xv[k] = lds_at(rg.e[k] >> 16);
-                const double lo = rlo, up = rup;
-                double zt = av[0] * xv[0];
+                // DK: the row's A values read with x~ (the dense rows leave no registers to
+                // keep them across the run)
 #pragma unroll
-                for (int k = 1; k < K; ++k) zt += av[k] * xv[k];
+                for (int k = 0; k < K; ++k) ar[k] = DK ? lds_at(rg.e[k] & 0xFFFFu) : av[k];
+                const double lo = rlo, up = rup;
+                double zt = ar[0] * xv[0];
+#pragma unroll
+                for (int k = 1; k < K; ++k) zt += ar[k] * xv[k];
                 const double zr = alpha * zt + (1.0 - alpha) * Z;
                 const double zn = __builtin_fmin(__builtin_fmax(zr + rvi * y, lo), up);
                 const double dd = rv * (zr - zn);
@@ -1624,16 +1779,16 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
 
 // FO: the factor-only instantiation (api.hip::check_convex), so that the solve's own code
 // carries no factor_only test
-template <int K, int KPK, int QR, bool EL = false, int KC = K, bool FO = false>
+template <int K, int KPK, int QR, bool EL = false, int KC = K, bool FO = false, bool DK = false>
 __global__ __launch_bounds__(T4, 2) void k_solve_w4(KParams p, double* __restrict__ xo, double* __restrict__ yo,
                                                     int /*factor_only: FO*/) {
-    solve_w4_body<K, KPK, QR, EL, KC>(p, xo, yo, FO ? 1 : 0);
+    solve_w4_body<K, KPK, QR, EL, KC, DK>(p, xo, yo, FO ? 1 : 0);
     extern __shared__ __attribute__((aligned(16))) double sm[];
     order_epilogue<T4>(p, (int*)sm);
 }
 
 // setup (setup_r.h with 256 threads: one column and one row per thread) + solve
-template <int K, int KPK, int QR, int SK, int SAS, bool EL = false, int KC = K>
+template <int K, int KPK, int QR, int SK, int SAS, bool EL = false, int KC = K, bool DK = false>
 __global__ __launch_bounds__(T4, 2) void k_setup_solve_w4(KParams p, const double* __restrict__ Px_in,
                                                           const double* __restrict__ Ax_in,
                                                           const double* __restrict__ q_in,
@@ -1643,7 +1798,7 @@ __global__ __launch_bounds__(T4, 2) void k_setup_solve_w4(KParams p, const doubl
     extern __shared__ __attribute__((aligned(16))) double sm[];
     setup_r_body<T4, SK, 4, 1, SAS, 1>(p, instance_of(p), Px_in, Ax_in, q_in, l_in, u_in, sm);
     __syncthreads();
-    solve_w4_body<K, KPK, QR, EL, KC>(p, xo, yo);
+    solve_w4_body<K, KPK, QR, EL, KC, DK>(p, xo, yo);
     order_epilogue<T4>(p, (int*)sm);
 }
 
@@ -2157,6 +2312,19 @@ static hipError_t lists_fit(const KParams& p, int K, int KC, int KPK, int QR, in
     return ok ? hipSuccess : hipErrorInvalidValue;
 }
 
+// the four-wave kernel's dense-inverse form (DK) for plans without eliminated columns whose
+// blocks have at most NB0 = 26 (blocks 0, 2) / NB1 = 28 (blocks 1, 3) real columns
+// (plan.cpp balances the four blocks for it):
+// opt-in (MPCQP_DENSE_W4=1, which also turns on the planner's balanced merge) until it beats the
+// three-phase form on the bench
+static bool dense_w4(const KParams& p) {
+    static const bool on = [] {
+        const char* e = getenv("MPCQP_DENSE_W4");
+        return e && e[0] == '1';
+    }();
+    return on && p.ne == 0 && p.Kd && p.bsz02 <= 26 && p.bsz13 <= 28;
+}
+
 // the fused kernel's instantiation for the plan, or 0: variant 10 and the 128-thread
 // register-list setup shape (one padded column per thread, two rows, four A values)
 static int setup_solve_fits(const KParams& p) {
@@ -2176,7 +2344,9 @@ hipError_t launch_setup_solve(const KParams& p, long B, const double* Px, const 
         // QR: rows of the G blocks phase C sums (the nonzero ones: amax)
         // EL (eliminated columns, the slack layouts): three A values per setup thread
         auto k4 = p.ne ? k_setup_solve_w4<6, 4, 8, 8, 3, true, 8>
-                       : (p.amax <= 5 ? k_setup_solve_w4<6, 4, 5, 6, 2> : k_setup_solve_w4<6, 4, 8, 6, 2>);
+                       : (p.amax <= 5 ? (dense_w4(p) ? k_setup_solve_w4<6, 4, 5, 6, 2, false, 6, true>
+                                                     : k_setup_solve_w4<6, 4, 5, 6, 2>)
+                                      : k_setup_solve_w4<6, 4, 8, 6, 2>);
         hipError_t e = lists_fit(p, 6, p.ne ? 8 : 6, 4, p.ne || p.amax > 5 ? 8 : 5);
         if (e != hipSuccess) return e;
         e = hipFuncSetAttribute((const void*)k4, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -2242,7 +2412,9 @@ hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, i
                          ? (p.ne ? k_solve_w4<6, 4, 8, true, 8, true>
                                  : (p.amax <= 5 ? k_solve_w4<6, 4, 5, false, 6, true> : k_solve_w4<6, 4, 8, false, 6, true>))
                          : (p.ne ? k_solve_w4<6, 4, 8, true, 8>
-                                 : (p.amax <= 5 ? k_solve_w4<6, 4, 5> : k_solve_w4<6, 4, 8>));
+                                 : (p.amax <= 5 ? (dense_w4(p) ? k_solve_w4<6, 4, 5, false, 6, false, true>
+                                                               : k_solve_w4<6, 4, 5>)
+                                                : k_solve_w4<6, 4, 8>));
             const size_t lds = lds_w2_bytes(p);
             hipError_t e = lists_fit(p, 6, p.ne ? 8 : 6, 4, p.ne || p.amax > 5 ? 8 : 5);
             if (e != hipSuccess) return e;
