@@ -143,10 +143,10 @@ size_t carve(size_t& off, size_t count) {
 void shape_params(const Plan& pl, KParams& k) {
     k.n = pl.n; k.m = pl.m; k.nb = pl.nb; k.npad = pl.npad; k.nnzP = pl.nnzP; k.nnzA = pl.nnzA; k.amax = pl.amax;
     k.bmax = pl.bmax; k.pmeet = (pl.nb - 1) / 2;
-    k.bsz02 = k.bsz13 = 1 << 20;
+    k.bsz01 = k.bsz23 = 1 << 20;
     if (pl.nb == 4) {
-        k.bsz02 = std::max(pl.bsize[0], pl.bsize[2]);
-        k.bsz13 = std::max(pl.bsize[1], pl.bsize[3]);
+        k.bsz01 = std::max(pl.bsize[0], pl.bsize[1]);
+        k.bsz23 = std::max(pl.bsize[2], pl.bsize[3]);
     }
     k.gk = pl.gather_k; k.pk = pl.p_k; k.ntgt = pl.ntgt; k.term_max = pl.term_max;
     k.gk1 = 0;

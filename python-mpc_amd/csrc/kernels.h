@@ -33,7 +33,7 @@ struct KParams {
     int gk1;          // most nonzeros in a row >= 128 (the two-wave kernel's second row slot)
     int gkr, gkc;     // most nonzeros in a row / a column of A (gk = the larger)
     int bmax, pmeet;  // two-sided factorisation (solve_big.hip): tail width, meeting block
-    int bsz02, bsz13; // largest of blocks 0 and 2 / 1 and 3 (real columns; nb = 4 plans)
+    int bsz01, bsz23; // largest of blocks 0 and 1 / 2 and 3 (real columns; nb = 4 plans)
     int variant;  // solve-kernel instantiation (solve.hip: launch_solve)
     int mode;     // factor storage of that variant (solve.hip: factorize)
     // plan

@@ -1065,13 +1065,16 @@ __device__ __forceinline__ void axpy_row(double* Kr, const double coef, const do
         Kr[O + c + 1] += coef * v1;
     }
 }
-// columns [0, NBC) of block b = 2 h + BB (its real columns: plan.cpp's balanced merge keeps
-// them within NBC) of the lane's row r of block a, into Kr[O, O + NBC)
+// columns [0, NBC) of block b = 2 BB + h (its real columns: plan.cpp's balanced merge keeps
+// them within NBC) of the lane's row r of block a, into Kr[O, O + NBC).  Slot BB pairs blocks
+// 2 BB (lower half) and 2 BB + 1 (upper half): the terms a half needs bound the steps both
+// halves run, and with adjacent blocks in a slot the most-loaded wave runs 30 row updates
+// (blocks 0 / 2 and 1 / 3 paired: 35)
 template <int QR, int BB, int NBC, int O>
 __device__ __forceinline__ void dense_inverse_block(double* Kr, const double* Sg, const double* gl, int a, int h,
                                                     int r) {
     constexpr int NP = 6;
-    const int b = 2 * h + BB;  // the half's column block
+    const int b = 2 * BB + h;  // the half's column block
     auto pidx = [](int x, int y) { return y < x ? x * (x - 1) / 2 + y : NP; };
     {   // [a = b] the lane's row of S_a^{-1}
         const double* src = Sg + b * SS + r * S;
@@ -1085,19 +1088,19 @@ __device__ __forceinline__ void dense_inverse_block(double* Kr, const double* Sg
         }
     }
     const double* const Ta = Sg + a * SS;
-    if (a > BB) {  // (a > b) for some half (the lower half's b = BB is the smaller)
+    if (a > 2 * BB) {  // (a > b) for some half (the lower half's b = 2 BB is the smaller)
         const double* g = gl + pidx(a, b) * 8 * S;
 #pragma unroll
         for (int q = 0; q < QR; ++q) axpy_row<O, NBC>(Kr, Ta[r * S + q], g + q * S);
     }
-    if (a < 2 + BB) {  // (b > a) for some half (the upper half's b = 2 + BB is the larger)
+    if (a < 2 * BB + 1) {  // (b > a) for some half (the upper half's b = 2 BB + 1 is the larger)
         const double* g = gl + pidx(b, a) * 8 * S;
         const double* Tb = Sg + b * SS;
 #pragma unroll
         for (int q = 0; q < QR; ++q) axpy_row<O, NBC>(Kr, g[q * S + r], Tb + q * S);
     }
 #pragma unroll 1
-    for (int k = max(a, BB) + 1; k < 4; ++k) {  // k > a, k > b for some half
+    for (int k = max(a, 2 * BB) + 1; k < 4; ++k) {  // k > a, k > b for some half
         const double* gka = gl + pidx(k, a) * 8 * S;
         const double* gkb = gl + pidx(k, b) * 8 * S;
         const double* Tk = Sg + k * SS;
@@ -1193,9 +1196,9 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
     GatherW<KH> chs;  // the half's share of the block column's list (the rhs sums)
     GatherW<LE> el;   // EL: the eliminated column's list (zero entries for the other lanes)
     const bool rows_wave = w * 64 < mp;  // wave-uniform
-    // DK: the lane's half of row pc of M^{-1}: columns [0, NB0) of block 2 h and [0, NB1) of block
-    // 2 h + 1 (their real columns), formed after each factorisation.  NB0 = 26, NB1 = 28
-    // (dense_w4: bsize[0], bsize[2] <= 26 and bsize[1], bsize[3] <= 28; cfg 2's balanced
+    // DK: the lane's half of row pc of M^{-1}: columns [0, NB0) of block h and [0, NB1) of block
+    // 2 + h (their real columns), formed after each factorisation.  NB0 = 26, NB1 = 28
+    // (dense_w4: bsize[0], bsize[1] <= 26 and bsize[2], bsize[3] <= 28; cfg 2's balanced
     // blocks are 26 / 25 / 25 / 28)
     constexpr int NB0 = 26, NB1 = 28;
     static_assert(!DK || (NB0 + NB1) * T4 == kDenseRowDoubles, "KParams::Kd rows");
@@ -1407,7 +1410,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
             if constexpr (DK) {
                 // x~[pc] = M^{-1}[pc] b: the half's NB0 + NB1 columns (broadcast reads, one address
                 // per half-wave), four FMA chains, one permlane32 swap
-                const double* const rbh = L.rb + 64 * h;
+                const double* const rbh = L.rb + S * h;
                 double a[4] = {0.0, 0.0, 0.0, 0.0};
                 // software-pipelined in windows of DKW values: window k + 1's reads are issued
                 // before window k's FMAs (two windows in flight; all 27 reads at once spill)
@@ -1416,8 +1419,8 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 auto issue = [&](int k, double (&dst)[DKW]) __attribute__((always_inline)) {
 #pragma unroll
                     for (int c = 0; c < DKW; c += 2) {
-                        const int e = k * DKW + c;  // block 2 h column e, or block 2 h + 1 column e - NB0
-                        if (e < NE) ld2(rbh + (e < NB0 ? e : 32 + e - NB0), dst[c], dst[c + 1]);
+                        const int e = k * DKW + c;  // block h column e, or block 2 + h column e - NB0
+                        if (e < NE) ld2(rbh + (e < NB0 ? e : 2 * S + e - NB0), dst[c], dst[c + 1]);
                     }
                 };
                 issue(0, v[0]);
@@ -2313,7 +2316,7 @@ static hipError_t lists_fit(const KParams& p, int K, int KC, int KPK, int QR, in
 }
 
 // the four-wave kernel's dense-inverse form (DK) for plans without eliminated columns whose
-// blocks have at most NB0 = 26 (blocks 0, 2) / NB1 = 28 (blocks 1, 3) real columns
+// blocks have at most NB0 = 26 (blocks 0, 1) / NB1 = 28 (blocks 2, 3) real columns
 // (plan.cpp balances the four blocks for it):
 // opt-in (MPCQP_DENSE_W4=1, which also turns on the planner's balanced merge) until it beats the
 // three-phase form on the bench
@@ -2322,7 +2325,7 @@ static bool dense_w4(const KParams& p) {
         const char* e = getenv("MPCQP_DENSE_W4");
         return e && e[0] == '1';
     }();
-    return on && p.ne == 0 && p.Kd && p.bsz02 <= 26 && p.bsz13 <= 28;
+    return on && p.ne == 0 && p.Kd && p.bsz01 <= 26 && p.bsz23 <= 28;
 }
 
 // the fused kernel's instantiation for the plan, or 0: variant 10 and the 128-thread

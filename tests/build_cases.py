@@ -74,12 +74,14 @@ def run_batch(name, cfg, B, variant, settings):
             f"{name}_variant": np.int32(info["variant"])}
 
 
-def in_build(build, specs, out, timeout=240):
+def in_build(build, specs, out, timeout=240, extra_env=None):
     """Run specs -- ("case", *CASES entry) or ("batch", name, cfg, B, variant, settings) --
-    in a child process under MPCQP_BUILD=build; returns the saved arrays."""
+    in a child process under MPCQP_BUILD=build (plus extra_env: switches the library reads
+    once per process, such as MPCQP_DENSE_W4); returns the saved arrays."""
     env = dict(os.environ, MPCQP_BUILD=build)
-    for k in ("MPCQP_VARIANT", "MPCQP_ELIM", "MPCQP_PHASE_PROF"):
+    for k in ("MPCQP_VARIANT", "MPCQP_ELIM", "MPCQP_PHASE_PROF", "MPCQP_DENSE_W4"):
         env.pop(k, None)
+    env.update(extra_env or {})
     if build == "prof":
         env["MPCQP_PHASE_PROF"] = "1"
     subprocess.run([sys.executable, os.path.join(HERE, "build_cases.py"), str(out), json.dumps(specs)], env=env,

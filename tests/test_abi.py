@@ -9,8 +9,11 @@
   run (no CPU fallback).
 """
 import ctypes as C
+import json
 import os
 import re
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -165,6 +168,35 @@ def test_plan_preview_pins_each_workloads_kernel(cfg, nb, amax_max, variant, cho
     # polish factors the full system: the plain plan, elimination not tried
     pol = osqp_amd.plan_preview(P, A, **dict(b["settings"], polish=True))
     assert pol["plan_choice"] == 0 and pol["n_eliminated"] == 0
+
+
+def test_balanced_four_block_merge_for_the_dense_form():
+    """With the four-wave kernel's dense-inverse form on (MPCQP_DENSE_W4=1, read once per
+    process: a child), the planner merges cfg 2's BFS levels into four balanced blocks
+    (26 / 25 / 25 / 28 instead of 31 / 30 / 30 / 13: every block within the form's static
+    26 / 28 columns per half) that stay block-tridiagonal with the same coupling rows."""
+    code = r"""
+import json, sys
+import numpy as np
+import osqp_amd
+from osqp_amd import mpc
+b = mpc.make_batch(2, B=2, seed=3)
+P, _ = osqp_amd._drop_common_zeros(b["P"], b["Px"])
+A, _ = osqp_amd._drop_common_zeros(b["A"], b["Ax"])
+nb, blk, var_pad, bsize = osqp_amd.analyze(P, A)
+info = osqp_amd.plan_preview(P, A, **b["settings"])
+K = (abs(P) + abs(P).T + abs(A).T @ abs(A)).tocoo()
+blk_of = np.asarray(var_pad) // blk
+span = int(np.abs(blk_of[K.row] - blk_of[K.col]).max())
+print(json.dumps(dict(nb=int(nb), bsize=[int(v) for v in bsize], span=span, amax=info["amax"],
+                      variant=info["variant"])))
+"""
+    env = dict(os.environ, MPCQP_DENSE_W4="1", PYTHONPATH=os.path.join(ROOT, "python-mpc_amd"))
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
+    got = json.loads(out.stdout.strip().splitlines()[-1])
+    assert got["nb"] == 4 and got["bsize"] == [26, 25, 25, 28], got
+    assert max(got["bsize"][0], got["bsize"][1]) <= 26 and max(got["bsize"][2], got["bsize"][3]) <= 28
+    assert got["span"] <= 1 and got["amax"] == 5 and got["variant"] == 17, got
 
 
 def test_plan_preview_reports_a_rejected_elimination():

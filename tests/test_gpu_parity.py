@@ -387,6 +387,23 @@ def test_experimental_kernel_variants(tmp_path):
         _batch_parity(mpc.make_batch(cfg, B=B), sets[cfg], rg=rg)
 
 
+def test_dense_inverse_form(tmp_path):
+    """The four-wave kernel's dense-inverse form (MPCQP_DENSE_W4=1: M^-1 = L' D L formed after
+    each factorisation, solve_wave.hip DK, on the planner's balanced blocks) against the
+    oracle, in a child process (the switch is read once per process): cfg 2 with the
+    workload's settings, and with a termination check after every iteration -- the rows of
+    M^-1 must survive every run boundary (a form that kept them in registers across the
+    check went wrong from the fifth check on)."""
+    import build_cases
+    sets = {"dflt": dict(polish=False, warm_start=False),
+            "ck1": dict(polish=False, warm_start=False, check_termination=1, max_iter=60)}
+    specs = [("batch", k, 2, 1024, None, s) for k, s in sets.items()]
+    got = build_cases.in_build("", specs, tmp_path / "dk.npz", extra_env={"MPCQP_DENSE_W4": "1"})
+    for k, s in sets.items():
+        rg = SimpleNamespace(x=got[f"{k}_x"], iter=got[f"{k}_iter"], status_val=got[f"{k}_status_val"])
+        _batch_parity(mpc.make_batch(2, B=1024), s, rg=rg)
+
+
 @pytest.mark.parametrize("variant", [v for v, _, _ in EXPERIMENTAL])
 def test_production_library_refuses_experimental_variants(monkeypatch, variant):
     cfg = next(c for v, c, _ in EXPERIMENTAL if v == variant)
