@@ -1157,7 +1157,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
     constexpr bool OPQ = EL || QR > 5;
     // c and 1 / c of the cost scaling, from the instance's scal slots where used
     auto cscal = [&](int k) __attribute__((always_inline)) {
-        return OPQ ? opaque_ptr(p.scal + b * 4)[k] : p.scal[b * 4 + k];
+        return OPQ ? opaque_gptr(p.scal + b * 4)[k] : p.scal[b * 4 + k];
     };
     double rho = p.scal[b * 4 + 2];
     const double sigma = p.sigma, alpha = p.alpha;
@@ -1223,7 +1223,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
         if (need_factor) {
             need_factor = false;
             if (iter > 0) {
-                double* const yp = opaque_ptr(p.y + b * m);
+                const auto yp = opaque_gptr(p.y + b * m);
                 for (int i = tid; i < m; i += T4) yp[i] = L.ys[i];
                 __syncthreads();  // every ys read is done before factorize_w4's E tiles overwrite it
             }
@@ -1246,7 +1246,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
             __syncthreads();
             const bool have_y = iter > 0 || warm;
             {
-                const double* const yp = opaque_ptr(p.y + b * m);
+                const auto yp = opaque_gptr(p.y + b * m);
                 for (int i = tid; i < mp; i += T4) L.ys[i] = (have_y && i < m) ? yp[i] : 0.0;
             }
             for (int o = tid; o < (NP + 1) * 8 * S; o += T4) {
@@ -1276,22 +1276,25 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 double Kf[NB0 + NB1];
                 dense_inverse_block<QR, 0, NB0, 0>(Kf, Sg, L.gl, w, h, r);
                 dense_inverse_block<QR, 1, NB1, NB0>(Kf, Sg, L.gl, w, h, r);
-                // (each pair's address: a wave-uniform base through an empty asm + the lane's
-                // index, formed at the store -- hoisted, the 27 64-bit addresses were spilled
-                // across the factorisation call)
+                // (the instance's base through an empty asm + the lane's 32-bit index, formed at
+                // the store -- hoisted, the 27 64-bit addresses were spilled across the
+                // factorisation call)
+                const auto kd = (__attribute__((address_space(1))) dpair*)opaque_gptr(p.Kd + b * kDenseRowDoubles);
 #pragma unroll
-                for (int j = 0; j < NB0 + NB1; j += 2)
-                    ((double2*)opaque_ptr(p.Kd + b * kDenseRowDoubles + (long)j * T4))[tid] = make_double2(Kf[j], Kf[j + 1]);
+                for (int j = 0; j < NB0 + NB1; j += 2) {
+                    kd[(unsigned)((j / 2) * T4 + tid)].x = Kf[j];
+                    kd[(unsigned)((j / 2) * T4 + tid)].y = Kf[j + 1];
+                }
             }
             PH(0)
         }
         // ---- run state ----
         if constexpr (DK) {
+            const auto kd = (const __attribute__((address_space(1))) dpair*)opaque_gptr(p.Kd + b * kDenseRowDoubles);
 #pragma unroll
             for (int j = 0; j < NB0 + NB1; j += 2) {
-                const double2 v = ((const double2*)opaque_ptr(p.Kd + b * kDenseRowDoubles + (long)j * T4))[tid];
-                Kr[j] = v.x;
-                Kr[j + 1] = v.y;
+                Kr[j] = kd[(unsigned)((j / 2) * T4 + tid)].x;
+                Kr[j + 1] = kd[(unsigned)((j / 2) * T4 + tid)].y;
             }
         }
         double SB[16];
@@ -1580,7 +1583,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
             // column (EL: the upper half checks its eliminated column pe) with its A and P lists
             // and D, the row's E
             const int col = EL ? (low ? pc : pe) : pc;
-            const bool cv = col >= 0 && (EL || low) && opaque_ptr(p.pad_var)[col] >= 0;
+            const bool cv = col >= 0 && (EL || low) && opaque_gptr(p.pad_var)[col] >= 0;
             GatherW<KC> cg;
             GatherW<KPK> pg;
             if (col >= 0) {
@@ -1591,8 +1594,8 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 pg.clear(lds_addr(L.Pv) + 8u * nnzP, Xbase);
             }
             const int oz = opaque_zero();
-            const double Dv = col >= 0 ? opaque_ptr(p.D + b * npad)[col] : 1.0;
-            const double Ev = ri < m ? opaque_ptr(p.E + b * m)[ri] : 1.0;
+            const double Dv = col >= 0 ? opaque_gptr(p.D + b * npad)[col] : 1.0;
+            const double Ev = ri < m ? opaque_gptr(p.E + b * m)[ri] : 1.0;
             // inline update_info + check_termination (as solve_w2_body's), one row per thread
             const bool unscale = p.scaling && !p.scaled_term;
             const unsigned ysbase = lds_addr(L.ys), dYbase = lds_addr(C.dY), dxbase = lds_addr(L.dx);
@@ -1655,7 +1658,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                     mx[16] = fabs(unscale ? pdx * di : pdx);
                 }
             }
-            if (tid < npad && opaque_ptr(p.pad_var)[tid] >= 0) sm[1] = L.qv[tid + oz] * L.dx[tid + oz];
+            if (tid < npad && opaque_gptr(p.pad_var)[tid] >= 0) sm[1] = L.qv[tid + oz] * L.dx[tid + oz];
             block_max_sum_tr<T4, 17, 2>(mx, sm, L.red);
             Res R;
             if (unscale) {

@@ -62,6 +62,14 @@ __device__ __forceinline__ T* opaque_ptr(T* p) {
     asm volatile("" : "+s"(p));
     return p;
 }
+// The same, keeping the global address space: through the asm a plain pointer becomes a
+// generic one, and a flat access counts on the LDS counter as well -- the next LDS wait then
+// waits for the global access too (the termination check's D / E / pad_var loads did)
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* opaque_gptr(T* p) {
+    asm volatile("" : "+s"(p));
+    return (__attribute__((address_space(1))) T*)p;
+}
 // A per-lane int through an empty asm (see opaque_zero).
 __device__ __forceinline__ int opaque_v(int x) {
     asm volatile("" : "+v"(x));
