@@ -1055,64 +1055,110 @@ constexpr int T4 = 256;
 // by broadcast (one row per half-wave).  G blocks come from the LDS copy gl (pair (k, j) at
 // k (k - 1) / 2 + j, pair NP the zero block: a lane whose b does not satisfy the term's
 // condition reads zeros), S_k^{-1} from the LDS tiles Sg.
-template <int O, int NBC>
-__device__ __forceinline__ void axpy_row(double* Kr, const double coef, const double* row) {
-#pragma unroll
-    for (int c = 0; c < NBC; c += 2) {
-        double v0, v1;
-        ld2(row + c, v0, v1);
-        Kr[O + c] += coef * v0;
-        Kr[O + c + 1] += coef * v1;
-    }
-}
-// columns [0, NBC) of block b = 2 BB + h (its real columns: plan.cpp's balanced merge keeps
-// them within NBC) of the lane's row r of block a, into Kr[O, O + NBC).  Slot BB pairs blocks
-// 2 BB (lower half) and 2 BB + 1 (upper half): the terms a half needs bound the steps both
-// halves run, and with adjacent blocks in a slot the most-loaded wave runs 30 row updates
-// (blocks 0 / 2 and 1 / 3 paired: 35)
-template <int QR, int BB, int NBC, int O>
-__device__ __forceinline__ void dense_inverse_block(double* Kr, const double* Sg, const double* gl, int a, int h,
-                                                    int r) {
-    constexpr int NP = 6;
-    const int b = 2 * BB + h;  // the half's column block
+// M^{-1} = L' D L into the instance's Kd rows, in 4 x 8 tiles: wave a forms block row a,
+// lanes [16 b, 16 b + 16) block (a, b), lane l16 = lane & 15 the rows 4 (l16 >> 1) .. + 3 and
+// columns 16 (l16 & 1) .. + 15 in two passes of 8 -- an outer-product update per term step
+// (4 coefficients, 8 row values, 32 FMAs) instead of a 28-wide row per lane (28 values for 28
+// FMAs): 3/8 of the LDS reads per FMA, the wave's steps 5 [a > 0] + 5 [a < 3] + 5 (3 - a) (pair NP, the
+// zero block, for the blocks a term does not apply to).  Element (i, c) of block (a, b) goes
+// to the dense-row slot of its lane (a, b & 1, i): pair j / 2 of the lane's row, j = c (b < 2)
+// or NB0 + c (b >= 2), c below NB0 / NB1 only.  Stored through global memory, read back by
+// other lanes after the next workgroup barrier.
+template <int QR, int NB0, int NB1>
+__device__ __forceinline__ void form_dense_rows(__attribute__((address_space(1))) dpair* kd, const double* Sg,
+                                                const double* gl, int a, int lane) {
+    constexpr int NP = 6, T4_ = 256, TC = 8;  // TC: tile columns per pass (two passes of the lane's 16)
     auto pidx = [](int x, int y) { return y < x ? x * (x - 1) / 2 + y : NP; };
-    {   // [a = b] the lane's row of S_a^{-1}
-        const double* src = Sg + b * SS + r * S;
-        const bool diag = b == a;
-#pragma unroll
-        for (int c = 0; c < NBC; c += 2) {
-            double v0, v1;
-            ld2(src + c, v0, v1);
-            Kr[O + c] = diag ? v0 : 0.0;
-            Kr[O + c + 1] = diag ? v1 : 0.0;
-        }
-    }
+    const int bq = lane >> 4, l16 = lane & 15, i0 = 4 * (l16 >> 1);
     const double* const Ta = Sg + a * SS;
-    if (a > 2 * BB) {  // (a > b) for some half (the lower half's b = 2 BB is the smaller)
-        const double* g = gl + pidx(a, b) * 8 * S;
-#pragma unroll
-        for (int q = 0; q < QR; ++q) axpy_row<O, NBC>(Kr, Ta[r * S + q], g + q * S);
-    }
-    if (a < 2 * BB + 1) {  // (b > a) for some half (the upper half's b = 2 BB + 1 is the larger)
-        const double* g = gl + pidx(b, a) * 8 * S;
-        const double* Tb = Sg + b * SS;
-#pragma unroll
-        for (int q = 0; q < QR; ++q) axpy_row<O, NBC>(Kr, g[q * S + r], Tb + q * S);
-    }
+    const int nbs = (bq >> 1) ? NB1 : NB0, jb = (bq >> 1) ? NB0 : 0;
+    const unsigned t0 = (unsigned)(a * 64 + (bq & 1) * 32 + i0);
 #pragma unroll 1
-    for (int k = max(a, 2 * BB) + 1; k < 4; ++k) {  // k > a, k > b for some half
-        const double* gka = gl + pidx(k, a) * 8 * S;
-        const double* gkb = gl + pidx(k, b) * 8 * S;
-        const double* Tk = Sg + k * SS;
-        double g[QR];
+    for (int pass = 0; pass < 2; ++pass) {
+        const int c0 = 16 * (l16 & 1) + TC * pass;
+        double acc[4][TC];
+        {   // [a = b] the tile of S_a^{-1}
+            const double* src = Sg + bq * SS + i0 * S + c0;
+            const bool diag = bq == a;
 #pragma unroll
-        for (int p = 0; p < QR; ++p) g[p] = gka[p * S + r];
+            for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int q = 0; q < QR; ++q) {
-            double v = 0.0;
+                for (int c = 0; c < TC; c += 2) {
+                    double v0, v1;
+                    ld2(src + i * S + c, v0, v1);
+                    acc[i][c] = diag ? v0 : 0.0;
+                    acc[i][c + 1] = diag ? v1 : 0.0;
+                }
+        }
+        auto step = [&](const double (&cf)[4], const double* row) __attribute__((always_inline)) {
+            double rv[TC];
 #pragma unroll
-            for (int p = 0; p < QR; ++p) v += g[p] * Tk[p * S + q];
-            axpy_row<O, NBC>(Kr, v, gkb + q * S);
+            for (int c = 0; c < TC; c += 2) ld2(row + c, rv[c], rv[c + 1]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int c = 0; c < TC; ++c) acc[i][c] += cf[i] * rv[c];
+        };
+        if (a > 0) {  // (a > b): S_a^{-1}[i][q] G_ab[q][c]
+            const double* g = gl + pidx(a, bq) * 8 * S + c0;
+#pragma unroll
+            for (int q = 0; q < QR; ++q) {
+                double cf[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) cf[i] = Ta[(i0 + i) * S + q];
+                step(cf, g + q * S);
+            }
+        }
+        if (a < 3) {  // (b > a): G_ba[q][i] S_b^{-1}[q][c]
+            const double* g = gl + pidx(bq, a) * 8 * S + i0;
+            const double* Tb = Sg + bq * SS + c0;
+#pragma unroll
+            for (int q = 0; q < QR; ++q) {
+                double cf[4];
+                ld2(g + q * S, cf[0], cf[1]);
+                ld2(g + q * S + 2, cf[2], cf[3]);
+                step(cf, Tb + q * S);
+            }
+        }
+#pragma unroll 1
+        for (int k = a + 1; k < 4; ++k) {  // (k > a, k > b): V_ka[i][q] G_kb[q][c]
+            const double* gka = gl + pidx(k, a) * 8 * S + i0;
+            const double* gkb = gl + pidx(k, bq) * 8 * S + c0;
+            const double* Tk = Sg + k * SS;
+            double V[4][QR];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int q = 0; q < QR; ++q) V[i][q] = 0.0;
+#pragma unroll
+            for (int pp = 0; pp < QR; ++pp) {
+                double g[4];
+                ld2(gka + pp * S, g[0], g[1]);
+                ld2(gka + pp * S + 2, g[2], g[3]);
+#pragma unroll
+                for (int q = 0; q < QR; ++q) {
+                    const double t = Tk[pp * S + q];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) V[i][q] += g[i] * t;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < QR; ++q) {
+                const double cf[4] = {V[0][q], V[1][q], V[2][q], V[3][q]};
+                step(cf, gkb + q * S);
+            }
+        }
+        // element (i0 + i, c0 + c) -> lane a 64 + (bq & 1) 32 + i0 + i, pair (jb + c0 + c) / 2
+#pragma unroll
+        for (int c = 0; c < TC; c += 2) {
+            if (c0 + c < nbs) {
+                const unsigned jp = (unsigned)((jb + c0 + c) >> 1);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    kd[jp * T4_ + t0 + i].x = acc[i][c];
+                    kd[jp * T4_ + t0 + i].y = acc[i][c + 1];
+                }
+            }
         }
     }
 }
@@ -1273,18 +1319,12 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 // 108 of the rows do not fit together (spilled, and wrong in the divergent
                 // check: DESIGN.md §5)
                 __syncthreads();  // the G copy is complete
-                double Kf[NB0 + NB1];
-                dense_inverse_block<QR, 0, NB0, 0>(Kf, Sg, L.gl, w, h, r);
-                dense_inverse_block<QR, 1, NB1, NB0>(Kf, Sg, L.gl, w, h, r);
-                // (the instance's base through an empty asm + the lane's 32-bit index, formed at
-                // the store -- hoisted, the 27 64-bit addresses were spilled across the
-                // factorisation call)
-                const auto kd = (__attribute__((address_space(1))) dpair*)opaque_gptr(p.Kd + b * kDenseRowDoubles);
-#pragma unroll
-                for (int j = 0; j < NB0 + NB1; j += 2) {
-                    kd[(unsigned)((j / 2) * T4 + tid)].x = Kf[j];
-                    kd[(unsigned)((j / 2) * T4 + tid)].y = Kf[j + 1];
-                }
+                // (the instance's base through an empty asm, the lanes' 32-bit indices formed at
+                // the stores; the run start's reads follow a workgroup barrier)
+                form_dense_rows<QR, NB0, NB1>((__attribute__((address_space(1))) dpair*)opaque_gptr(
+                                                  p.Kd + b * kDenseRowDoubles),
+                                              Sg, L.gl, w, lane);
+                __syncthreads();  // every tile stored before any lane reads its rows (run start)
             }
             PH(0)
         }
