@@ -258,21 +258,25 @@ def pmc_traffic(workload, batch, kernel):
 
 
 def copy_peak(dev_index, nbytes=2 << 30, reps=10):
-    """Achievable HBM bandwidth of a device-to-device copy (torch's copy kernel): a 2 GiB
-    buffer copied `reps` times, (read + write) bytes / time, GB/s.  Outside the timed region."""
+    """Achievable HBM bandwidth of a device-to-device copy: libmpcqp's streaming copy kernel
+    (mpcqp_debug_copy: 16-byte non-temporal loads and stores, four per lane in flight, the
+    MI355X guide's float4-copy form, which measures ~6.3 TB/s) over a 2 GiB buffer `reps`
+    times, (read + write) bytes / time, GB/s.  Outside the timed region."""
+    import ctypes as C
     import torch
+    import osqp_amd
     dev = torch.device("cuda", dev_index)
     src = torch.empty(nbytes // 8, dtype=torch.float64, device=dev).fill_(1.0)
     dst = torch.empty_like(src)
-    dst.copy_(src)
     torch.cuda.synchronize(dev)
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record()
-    for _ in range(reps):
-        dst.copy_(src)
-    b.record()
-    torch.cuda.synchronize(dev)
-    gbs = 2 * nbytes * reps / (a.elapsed_time(b) * 1e-3) / 1e9
+    ms = C.c_double()
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    rc = osqp_amd.lib().mpcqp_debug_copy(src.data_ptr(), dst.data_ptr(), src.numel(), reps, stream, C.byref(ms))
+    if rc != 0:
+        raise RuntimeError(osqp_amd.lib().mpcqp_last_error().decode())
+    if not torch.equal(dst[:: 1 << 20], src[:: 1 << 20]):
+        raise RuntimeError("copy_peak: the copy kernel's output differs from its input")
+    gbs = 2 * nbytes / (ms.value * 1e-3) / 1e9
     del src, dst
     torch.cuda.empty_cache()
     return gbs

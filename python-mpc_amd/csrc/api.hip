@@ -202,6 +202,27 @@ hipError_t pool_malloc(int dev, size_t bytes, void** out, bool pinned, unsigned 
             return hipSuccess;
         }
     }
+    hipError_t e = pinned ? hipHostMalloc(out, bytes, hipHostMallocDefault) : hipMalloc(out, bytes);
+    if (e == hipSuccess) return e;
+    // out of memory: give the pooled blocks of this kind back (a caller that freed a handle to
+    // make room must not fail where hipFree would have returned the memory) and try once more
+    (void)hipGetLastError();
+    std::vector<ResPool::Blk> rel;
+    {
+        std::lock_guard<std::mutex> lk(r.mu);
+        auto& v = pinned ? r.pin : r.dev;
+        for (size_t i = v.size(); i-- > 0;)
+            if (pinned || v[i].dev == dev) {
+                rel.push_back(v[i]);
+                (pinned ? r.pin_total : r.dev_total) -= v[i].bytes;
+                v.erase(v.begin() + i);
+            }
+    }
+    if (rel.empty()) return e;
+    for (auto& b : rel) {
+        if (pinned) (void)hipHostFree(b.p);
+        else (void)hipFree(b.p);
+    }
     return pinned ? hipHostMalloc(out, bytes, hipHostMallocDefault) : hipMalloc(out, bytes);
 }
 void pool_free(int dev, size_t bytes, void* p, bool pinned, unsigned long long tag = 0) {
@@ -485,7 +506,7 @@ std::string choose_plan(int32_t n, int32_t m, const int32_t* Pp, const int32_t* 
             if (!err.empty()) note = "eliminated plan failed: " + err;
         }
     }
-    std::string err = build_plan(n, m, Pp, Pi, Ap, Ai, pl, false);
+    std::string err = build_plan(n, m, Pp, Pi, Ap, Ai, pl, false, dense_w4_on());
     pl.uid = next_plan_uid();
     pl.choice = choice;
     pl.choice_note = note;
@@ -889,7 +910,7 @@ int mpcqp_analyze_ex(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi,
                      const int32_t* Ai, int32_t eliminate, int32_t* nb, int32_t* block, int32_t* var_pad,
                      int32_t* bsize, int32_t* n_eliminated) {
     Plan pl;
-    std::string err = build_plan(n, m, Pp, Pi, Ap, Ai, pl, eliminate != 0);
+    std::string err = build_plan(n, m, Pp, Pi, Ap, Ai, pl, eliminate != 0, !eliminate && dense_w4_on());
     if (n_eliminated) *n_eliminated = pl.ne;
     if (!err.empty()) return fail(err.rfind("unsupported", 0) == 0 ? MPCQP_EUNSUPPORTED : MPCQP_EINVAL, "%s", err.c_str());
     if (nb) *nb = pl.nb;
@@ -1487,6 +1508,11 @@ int mpcqp_plan_preview(int32_t n, int32_t m, const int32_t* Pp, const int32_t* P
     KParams k{};
     shape_params(pl, k);
     k.variant = solve_variant(k);
+    if (const char* ev = getenv("MPCQP_VARIANT"); ev && *ev) {  // the override alloc_shard applies
+        const int v = atoi(ev);
+        if (!variant_fits(k, v)) return fail(MPCQP_EUNSUPPORTED, "MPCQP_VARIANT=%d does not fit this plan", v);
+        k.variant = v;
+    }
     k.mode = k.variant >= 0 ? solve_mode(k.variant) : 0;
     *info = mpcqp_plan_info{};
     info->n = n; info->m = m; info->nb = pl.nb; info->block = kS; info->npad = pl.npad;
@@ -1524,6 +1550,26 @@ int mpcqp_debug_dispatch_order(mpcqp_handle* h, int32_t* out) {
         HIPCHK(hipMemcpy(o, s.kp.order, sizeof(int32_t) * s.B, hipMemcpyDeviceToHost));
         for (long i = 0; i < s.B; ++i) o[i] += (int32_t)s.b0;
     }
+    return 0;
+}
+
+int mpcqp_debug_copy(const double* src, double* dst, int64_t n, int32_t reps, void* stream, double* ms) {
+    if (!src || !dst || !ms || n <= 0 || n % 4096 || reps <= 0 || ((uintptr_t)src | (uintptr_t)dst) & 15)
+        return fail(MPCQP_EINVAL, "mpcqp_debug_copy: n > 0, n %% 4096 == 0, reps > 0, 16-byte aligned buffers");
+    hipStream_t st = (hipStream_t)stream;
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    HIPCHK(launch_copy16(src, dst, n, st));  // (warm-up)
+    HIPCHK(hipEventRecord(a, st));
+    for (int r = 0; r < reps; ++r) HIPCHK(launch_copy16(src, dst, n, st));
+    HIPCHK(hipEventRecord(b, st));
+    HIPCHK(hipEventSynchronize(b));
+    float t = 0.0f;
+    HIPCHK(hipEventElapsedTime(&t, a, b));
+    *ms = (double)t / reps;
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
     return 0;
 }
 

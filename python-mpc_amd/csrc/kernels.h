@@ -98,10 +98,16 @@ hipError_t launch_warm(const KParams& p, long B, const double* x, const double* 
 hipError_t launch_order(const KParams& p, long B, hipStream_t st);
 // order[i] = i (the identity dispatch order of a fresh workspace), enqueued on st
 hipError_t launch_iota(int* order, long B, hipStream_t st);
+// streaming device copy of n doubles (n % 4096 == 0), mpcqp_debug_copy
+hipError_t launch_copy16(const double* src, double* dst, long n, hipStream_t st);
 // doubles per instance of the four-wave kernel's dense-inverse rows (KParams::Kd): 256 lanes x
-// (NB0 + NB1 = 54) for plans of four blocks without eliminated columns (solve_wave.hip, DK)
+// (NB0 + NB1 = 54) for plans of four blocks without eliminated columns (solve_wave.hip, DK).
+// The DK form was measured and not taken: it is compiled into the experimental
+// builds only and runs there under MPCQP_DENSE_W4=1; dense_w4_on() is false in the production
+// library, so no workspace is carved for it there (cfg 2: 231 -> 121 kB per instance).
 constexpr long kDenseRowDoubles = 256L * 54;
-inline long dense_rows_doubles(int nb, int ne) { return nb == 4 && ne == 0 ? kDenseRowDoubles : 0; }
+bool dense_w4_on();  // solve_wave.hip: experimental build and MPCQP_DENSE_W4=1
+inline long dense_rows_doubles(int nb, int ne) { return nb == 4 && ne == 0 && dense_w4_on() ? kDenseRowDoubles : 0; }
 int solve_variant(const KParams& p);  // -1: no instantiation fits the plan
 int solve_mode(int variant);
 int solve_threads(int variant);  // workgroup size of the variant's kernel

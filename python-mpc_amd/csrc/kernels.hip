@@ -447,4 +447,25 @@ hipError_t launch_order(const KParams& p, long B, hipStream_t st) {
                        shift);
     return hipGetLastError();
 }
+// Streaming copy (mpcqp_debug_copy, bench.py's achievable-HBM reference): each lane moves four
+// 16-byte granules per pass, loads issued together ahead of the stores, non-temporal both
+// ways (no L2 / MALL pollution), grid-stride over n4 = n / 4096 passes of the whole grid.
+typedef double v2d __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(256) void k_copy16(const v2d* __restrict__ s, v2d* __restrict__ d, long n2) {
+    const long per = 4L * 256;  // granules per workgroup pass
+    for (long base = (long)blockIdx.x * per; base < n2; base += (long)gridDim.x * per) {
+        const long i = base + threadIdx.x;
+        v2d a[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a[k] = __builtin_nontemporal_load(s + i + k * 256);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(a[k], d + i + k * 256);
+    }
+}
+
+hipError_t launch_copy16(const double* src, double* dst, long n, hipStream_t st) {
+    hipLaunchKernelGGL(k_copy16, dim3(2048), dim3(256), 0, st, (const v2d*)src, (v2d*)dst, n / 2);
+    return hipGetLastError();
+}
+
 }  // namespace mpcqp

@@ -37,22 +37,20 @@ std::vector<std::vector<int>> bfs_levels(const Graph& g, int s, std::vector<int>
     return levels;
 }
 
-// balanced four-block merge (build_plan), with the four-wave kernel's dense-inverse form;
-// MPCQP_DENSE_W4=1 turns both on (solve_wave.hip::dense_w4)
-bool balance_blocks() {
-    static const bool on = [] {
+// balanced four-block merge (build_plan's balance4: the caller's choice -- the experimental
+// builds' dense-inverse form, solve_wave.hip::dense_w4_on); MPCQP_BALANCE overrides it
+bool balance_blocks(bool balance4) {
+    static const int ov = [] {
         const char* b = getenv("MPCQP_BALANCE");  // (diagnostic override)
-        if (b) return b[0] != '0';
-        const char* e = getenv("MPCQP_DENSE_W4");
-        return e && e[0] == '1';
+        return b ? (b[0] != '0' ? 1 : 0) : -1;
     }();
-    return on;
+    return ov < 0 ? balance4 : ov == 1;
 }
 
 }  // namespace
 
 std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
-                       const int32_t* Ai, Plan& pl, bool eliminate) {
+                       const int32_t* Ai, Plan& pl, bool eliminate, bool balance4) {
     char buf[256];
     if (n <= 0 || m < 0) return "invalid dimensions";
     if (Pp[0] != 0 || Ap[0] != 0) return "CSC column pointers must start at 0";
@@ -163,7 +161,7 @@ std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const
         else
             blocks.push_back(L);
     }
-    if (!eliminate && blocks.size() == 4 && balance_blocks()) {
+    if (!eliminate && blocks.size() == 4 && balance_blocks(balance4)) {
         // balanced merge for the four-wave kernel's dense-inverse form (solve_wave.hip, DK):
         // the smallest block capacity that still merges the levels into four blocks, so that
         // no block has more real columns than the kernel's static per-block count (cfg 2:
@@ -223,7 +221,7 @@ std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const
         size_t next = 0;
         for (int pc = 0; pc < pl.nbp && next < iso.size(); ++pc)
             if (owner_var[pc] < 0) owner_var[pc] = iso[next++];
-        if (next < iso.size()) return build_plan(n, m, Pp, Pi, Ap, Ai, pl, false);  // no free columns left
+        if (next < iso.size()) return build_plan(n, m, Pp, Pi, Ap, Ai, pl, false, balance4);  // no free columns left
         for (int pc = 0; pc < pl.nbp; ++pc)
             if (owner_var[pc] >= 0) {
                 pl.eown[pc] = pl.nbp + pl.ne;

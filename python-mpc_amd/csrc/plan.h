@@ -96,8 +96,10 @@ struct Plan {
 // Returns "" on success, otherwise an error message.  eliminate: take degree <= 1
 // vertices of K's graph out of the block system (see Plan::eown); the blocks are then
 // packed greedily (consecutive runs of S variables of the level order) when that gives
-// fewer blocks and stays block-tridiagonal.
+// fewer blocks and stays block-tridiagonal.  balance4: a plain plan of four blocks is merged
+// into four balanced ones (the experimental dense-inverse form, solve_wave.hip::dense_w4_on).
 std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi,
-                       const int32_t* Ap, const int32_t* Ai, Plan& out, bool eliminate = false);
+                       const int32_t* Ap, const int32_t* Ai, Plan& out, bool eliminate = false,
+                       bool balance4 = false);
 
 }  // namespace mpcqp

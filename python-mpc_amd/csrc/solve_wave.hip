@@ -2360,15 +2360,22 @@ static hipError_t lists_fit(const KParams& p, int K, int KC, int KPK, int QR, in
 
 // the four-wave kernel's dense-inverse form (DK) for plans without eliminated columns whose
 // blocks have at most NB0 = 26 (blocks 0, 1) / NB1 = 28 (blocks 2, 3) real columns
-// (plan.cpp balances the four blocks for it):
-// opt-in (MPCQP_DENSE_W4=1, which also turns on the planner's balanced merge) until it beats the
-// three-phase form on the bench
-static bool dense_w4(const KParams& p) {
+// (plan.cpp balances the four blocks for it): measured and not taken, so it is
+// compiled into the experimental builds only, where MPCQP_DENSE_W4=1 turns it on (and the
+// planner's balanced merge with it)
+bool dense_w4_on() {
+#ifdef MPCQP_EXPERIMENTAL
     static const bool on = [] {
         const char* e = getenv("MPCQP_DENSE_W4");
         return e && e[0] == '1';
     }();
-    return on && p.ne == 0 && p.Kd && p.bsz01 <= 26 && p.bsz23 <= 28;
+    return on;
+#else
+    return false;
+#endif
+}
+[[maybe_unused]] static bool dense_w4(const KParams& p) {
+    return dense_w4_on() && p.ne == 0 && p.Kd && p.bsz01 <= 26 && p.bsz23 <= 28;
 }
 
 // the fused kernel's instantiation for the plan, or 0: variant 10 and the 128-thread
@@ -2390,9 +2397,10 @@ hipError_t launch_setup_solve(const KParams& p, long B, const double* Px, const 
         // QR: rows of the G blocks phase C sums (the nonzero ones: amax)
         // EL (eliminated columns, the slack layouts): three A values per setup thread
         auto k4 = p.ne ? k_setup_solve_w4<6, 4, 8, 8, 3, true, 8>
-                       : (p.amax <= 5 ? (dense_w4(p) ? k_setup_solve_w4<6, 4, 5, 6, 2, false, 6, true>
-                                                     : k_setup_solve_w4<6, 4, 5, 6, 2>)
-                                      : k_setup_solve_w4<6, 4, 8, 6, 2>);
+                       : (p.amax <= 5 ? k_setup_solve_w4<6, 4, 5, 6, 2> : k_setup_solve_w4<6, 4, 8, 6, 2>);
+#ifdef MPCQP_EXPERIMENTAL
+        if (!p.ne && p.amax <= 5 && dense_w4(p)) k4 = k_setup_solve_w4<6, 4, 5, 6, 2, false, 6, true>;
+#endif
         hipError_t e = lists_fit(p, 6, p.ne ? 8 : 6, 4, p.ne || p.amax > 5 ? 8 : 5);
         if (e != hipSuccess) return e;
         e = hipFuncSetAttribute((const void*)k4, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -2458,9 +2466,10 @@ hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, i
                          ? (p.ne ? k_solve_w4<6, 4, 8, true, 8, true>
                                  : (p.amax <= 5 ? k_solve_w4<6, 4, 5, false, 6, true> : k_solve_w4<6, 4, 8, false, 6, true>))
                          : (p.ne ? k_solve_w4<6, 4, 8, true, 8>
-                                 : (p.amax <= 5 ? (dense_w4(p) ? k_solve_w4<6, 4, 5, false, 6, false, true>
-                                                               : k_solve_w4<6, 4, 5>)
-                                                : k_solve_w4<6, 4, 8>));
+                                 : (p.amax <= 5 ? k_solve_w4<6, 4, 5> : k_solve_w4<6, 4, 8>));
+#ifdef MPCQP_EXPERIMENTAL
+            if (!factor_only && !p.ne && p.amax <= 5 && dense_w4(p)) k = k_solve_w4<6, 4, 5, false, 6, false, true>;
+#endif
             const size_t lds = lds_w2_bytes(p);
             hipError_t e = lists_fit(p, 6, p.ne ? 8 : 6, 4, p.ne || p.amax > 5 ? 8 : 5);
             if (e != hipSuccess) return e;

@@ -146,6 +146,7 @@ def lib():
     L.mpcqp_timing_read.argtypes = [vp, dp, i32p, dp, i32p]
     L.mpcqp_debug_phase_times.argtypes = [vp, _P(C.c_int64)]
     L.mpcqp_debug_dispatch_order.argtypes = [vp, _P(C.c_int32)]
+    L.mpcqp_debug_copy.argtypes = [vp, vp, C.c_int64, C.c_int32, vp, dp]
     L.mpcqp_free.argtypes = [vp]
     L.mpcqp_free.restype = None
     L.mpcqp_analyze.argtypes = [C.c_int32, C.c_int32, i32p, i32p, i32p, i32p,

@@ -171,8 +171,8 @@ def test_plan_preview_pins_each_workloads_kernel(cfg, nb, amax_max, variant, cho
 
 
 def test_balanced_four_block_merge_for_the_dense_form():
-    """With the four-wave kernel's dense-inverse form on (MPCQP_DENSE_W4=1, read once per
-    process: a child), the planner merges cfg 2's BFS levels into four balanced blocks
+    """With the four-wave kernel's dense-inverse form on (MPCQP_DENSE_W4=1 in the experimental
+    build, read once per process: a child), the planner merges cfg 2's BFS levels into four balanced blocks
     (26 / 25 / 25 / 28 instead of 31 / 30 / 30 / 13: every block within the form's static
     26 / 28 columns per half) that stay block-tridiagonal with the same coupling rows."""
     code = r"""
@@ -191,12 +191,37 @@ span = int(np.abs(blk_of[K.row] - blk_of[K.col]).max())
 print(json.dumps(dict(nb=int(nb), bsize=[int(v) for v in bsize], span=span, amax=info["amax"],
                       variant=info["variant"])))
 """
-    env = dict(os.environ, MPCQP_DENSE_W4="1", PYTHONPATH=os.path.join(ROOT, "python-mpc_amd"))
+    env = dict(os.environ, MPCQP_DENSE_W4="1", MPCQP_BUILD="exp", PYTHONPATH=os.path.join(ROOT, "python-mpc_amd"))
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
     got = json.loads(out.stdout.strip().splitlines()[-1])
     assert got["nb"] == 4 and got["bsize"] == [26, 25, 25, 28], got
     assert max(got["bsize"][0], got["bsize"][1]) <= 26 and max(got["bsize"][2], got["bsize"][3]) <= 28
     assert got["span"] <= 1 and got["amax"] == 5 and got["variant"] == 17, got
+    # the production library has no dense-inverse form: the switch changes nothing there
+    env["MPCQP_BUILD"] = ""
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
+    prod = json.loads(out.stdout.strip().splitlines()[-1])
+    assert prod["bsize"] == [31, 30, 30, 13], prod
+
+
+def test_cfg2_workspace_carries_no_dense_inverse_rows():
+    """The production library carves no dense-inverse rows (KParams::Kd, 256 x 54 doubles per
+    instance) for cfg 2's four-block plan: that form is compiled into the experimental build
+    only.  Pinned: 120,760 bytes per instance (231,352 with the rows), with and
+    without MPCQP_DENSE_W4=1 (read once per process: children)."""
+    code = r"""
+import json
+import osqp_amd
+from osqp_amd import mpc
+b = mpc.make_batch(2, B=2, seed=3)
+P, _ = osqp_amd._drop_common_zeros(b["P"], b["Px"])
+A, _ = osqp_amd._drop_common_zeros(b["A"], b["Ax"])
+print(json.dumps(osqp_amd.plan_preview(P, A, **b["settings"])["bytes_per_instance"]))
+"""
+    for dk in ("0", "1"):
+        env = dict(os.environ, MPCQP_DENSE_W4=dk, MPCQP_BUILD="", PYTHONPATH=os.path.join(ROOT, "python-mpc_amd"))
+        out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
+        assert json.loads(out.stdout.strip().splitlines()[-1]) == 120760
 
 
 def test_plan_preview_reports_a_rejected_elimination():

@@ -388,9 +388,9 @@ def test_experimental_kernel_variants(tmp_path):
 
 
 def test_dense_inverse_form(tmp_path):
-    """The four-wave kernel's dense-inverse form (MPCQP_DENSE_W4=1: M^-1 = L' D L formed after
-    each factorisation, solve_wave.hip DK, on the planner's balanced blocks) against the
-    oracle, in a child process (the switch is read once per process): cfg 2 with the
+    """The four-wave kernel's dense-inverse form (MPCQP_DENSE_W4=1 in the experimental build:
+    M^-1 = L' D L formed after each factorisation, solve_wave.hip DK, on the planner's balanced
+    blocks) against the oracle, in a child process (the switch is read once per process): cfg 2 with the
     workload's settings, and with a termination check after every iteration -- the rows of
     M^-1 must survive every run boundary (a form that kept them in registers across the
     check went wrong from the fifth check on)."""
@@ -398,7 +398,7 @@ def test_dense_inverse_form(tmp_path):
     sets = {"dflt": dict(polish=False, warm_start=False),
             "ck1": dict(polish=False, warm_start=False, check_termination=1, max_iter=60)}
     specs = [("batch", k, 2, 1024, None, s) for k, s in sets.items()]
-    got = build_cases.in_build("", specs, tmp_path / "dk.npz", extra_env={"MPCQP_DENSE_W4": "1"})
+    got = build_cases.in_build("exp", specs, tmp_path / "dk.npz", extra_env={"MPCQP_DENSE_W4": "1"})
     for k, s in sets.items():
         rg = SimpleNamespace(x=got[f"{k}_x"], iter=got[f"{k}_iter"], status_val=got[f"{k}_status_val"])
         _batch_parity(mpc.make_batch(2, B=1024), s, rg=rg)
@@ -1189,6 +1189,38 @@ def test_update_settings_polish_on_eliminated_plan(golden):
     assert (rd.status_polish[same] == ps[same]).all()
     xo = np.stack([r.x for r in ros])
     assert np.abs(rd.x[same] - xo[same]).max() < 1e-6 * max(1.0, np.abs(xo).max())
+
+
+def test_replan_matches_a_handle_set_up_on_the_plain_plan(monkeypatch):
+    """Device against device: a cfg-3 handle set up on the eliminated plan, solved,
+    then re-planned by update_settings(polish=True) (api.hip::replan_plain) and warm-started,
+    against a handle set up on the plain plan directly (polish on) from the same (x, y).  With
+    adaptive rho off both carry rho = 0.1, the same scaling and z = Ax, so every per-column and
+    per-row array the re-plan permutes must land where the plain plan's setup puts it: the next
+    solve agrees on every instance -- status, iterations, polish decision -- and x, y to rounding."""
+    b = mpc.make_batch(3, B=96, seed=41)
+    s = dict(warm_start=True, adaptive_rho=False, max_iter=400)
+    a = OSQPBatch()
+    a.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
+    assert a.plan_info()["n_eliminated"] == 105
+    r0 = a.solve()
+    x0, y0 = r0.x.copy(), r0.y.copy()
+    a.update_settings(polish=True)
+    assert a.plan_info()["n_eliminated"] == 0 and a.plan_info()["plan_choice"] == 0
+    c = OSQPBatch()
+    c.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **dict(s, polish=True))
+    assert c.plan_info()["n_eliminated"] == 0 and c.plan_info()["plan_choice"] == 0
+    lb, ub = b["l"].copy(), b["u"].copy()
+    lb[:, :5] = ub[:, :5] = b["l"][:, :5] * 0.97
+    for h in (a, c):
+        h.warm_start(x=x0, y=y0)
+        h.update(l=lb, u=ub)
+    ra, rc = a.solve(), c.solve()
+    assert (ra.status_val == rc.status_val).all()
+    assert (ra.iter == rc.iter).all(), (ra.iter, rc.iter)
+    assert (ra.status_polish == rc.status_polish).all()
+    assert np.abs(ra.x - rc.x).max() <= 1e-12 * max(1.0, np.abs(rc.x).max())
+    assert np.abs(ra.y - rc.y).max() <= 1e-12 * max(1.0, np.abs(rc.y).max())
 
 
 def test_shim_update_settings_polish_demo():
