@@ -1554,20 +1554,25 @@ int mpcqp_debug_dispatch_order(mpcqp_handle* h, int32_t* out) {
 }
 
 int mpcqp_debug_copy(const double* src, double* dst, int64_t n, int32_t reps, void* stream, double* ms) {
-    if (!src || !dst || !ms || n <= 0 || n % 4096 || reps <= 0 || ((uintptr_t)src | (uintptr_t)dst) & 15)
-        return fail(MPCQP_EINVAL, "mpcqp_debug_copy: n > 0, n %% 4096 == 0, reps > 0, 16-byte aligned buffers");
+    if (!src || !dst || !ms || n <= 0 || n % 16384 || reps <= 0 || ((uintptr_t)src | (uintptr_t)dst) & 15)
+        return fail(MPCQP_EINVAL, "mpcqp_debug_copy: n > 0, n %% 16384 == 0, reps > 0, 16-byte aligned buffers");
     hipStream_t st = (hipStream_t)stream;
     hipEvent_t a, b;
     HIPCHK(hipEventCreate(&a));
     HIPCHK(hipEventCreate(&b));
-    HIPCHK(launch_copy16(src, dst, n, st));  // (warm-up)
-    HIPCHK(hipEventRecord(a, st));
-    for (int r = 0; r < reps; ++r) HIPCHK(launch_copy16(src, dst, n, st));
-    HIPCHK(hipEventRecord(b, st));
-    HIPCHK(hipEventSynchronize(b));
-    float t = 0.0f;
-    HIPCHK(hipEventElapsedTime(&t, a, b));
-    *ms = (double)t / reps;
+    double best = 0.0;
+    for (int form = 0; form < 3; ++form) {  // the fastest of the three forms
+        HIPCHK(launch_copy16(src, dst, n, st, form));  // (warm-up)
+        HIPCHK(hipEventRecord(a, st));
+        for (int r = 0; r < reps; ++r) HIPCHK(launch_copy16(src, dst, n, st, form));
+        HIPCHK(hipEventRecord(b, st));
+        HIPCHK(hipEventSynchronize(b));
+        float t = 0.0f;
+        HIPCHK(hipEventElapsedTime(&t, a, b));
+        const double per = (double)t / reps;
+        if (form == 0 || per < best) best = per;
+    }
+    *ms = best;
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
     return 0;

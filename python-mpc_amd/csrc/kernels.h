@@ -98,8 +98,9 @@ hipError_t launch_warm(const KParams& p, long B, const double* x, const double* 
 hipError_t launch_order(const KParams& p, long B, hipStream_t st);
 // order[i] = i (the identity dispatch order of a fresh workspace), enqueued on st
 hipError_t launch_iota(int* order, long B, hipStream_t st);
-// streaming device copy of n doubles (n % 4096 == 0), mpcqp_debug_copy
-hipError_t launch_copy16(const double* src, double* dst, long n, hipStream_t st);
+// streaming device copy of n doubles (n % 16384 == 0) in one of three forms (kernels.hip),
+// mpcqp_debug_copy
+hipError_t launch_copy16(const double* src, double* dst, long n, hipStream_t st, int form);
 // doubles per instance of the four-wave kernel's dense-inverse rows (KParams::Kd): 256 lanes x
 // (NB0 + NB1 = 54) for plans of four blocks without eliminated columns (solve_wave.hip, DK).
 // The DK form was measured and not taken: it is compiled into the experimental

@@ -447,24 +447,36 @@ hipError_t launch_order(const KParams& p, long B, hipStream_t st) {
                        shift);
     return hipGetLastError();
 }
-// Streaming copy (mpcqp_debug_copy, bench.py's achievable-HBM reference): each lane moves four
-// 16-byte granules per pass, loads issued together ahead of the stores, non-temporal both
-// ways (no L2 / MALL pollution), grid-stride over n4 = n / 4096 passes of the whole grid.
+// Streaming copy (mpcqp_debug_copy, bench.py's achievable-HBM reference): each lane moves G
+// 16-byte granules per pass, loads issued together ahead of the stores, grid-stride; NT:
+// non-temporal loads and stores (no L2 / MALL pollution) or the default policy.
 typedef double v2d __attribute__((ext_vector_type(2)));
+template <bool NT, int G>
 __global__ __launch_bounds__(256) void k_copy16(const v2d* __restrict__ s, v2d* __restrict__ d, long n2) {
-    const long per = 4L * 256;  // granules per workgroup pass
+    const long per = (long)G * 256;  // granules per workgroup pass
     for (long base = (long)blockIdx.x * per; base < n2; base += (long)gridDim.x * per) {
         const long i = base + threadIdx.x;
-        v2d a[4];
+        v2d a[G];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) a[k] = __builtin_nontemporal_load(s + i + k * 256);
+        for (int k = 0; k < G; ++k) a[k] = NT ? __builtin_nontemporal_load(s + i + k * 256) : s[i + k * 256];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(a[k], d + i + k * 256);
+        for (int k = 0; k < G; ++k) {
+            if (NT) __builtin_nontemporal_store(a[k], d + i + k * 256);
+            else d[i + k * 256] = a[k];
+        }
     }
 }
 
-hipError_t launch_copy16(const double* src, double* dst, long n, hipStream_t st) {
-    hipLaunchKernelGGL(k_copy16, dim3(2048), dim3(256), 0, st, (const v2d*)src, (v2d*)dst, n / 2);
+// form: 0 non-temporal, 4 granules per lane, 2048 workgroups; 1 default policy, 4 granules,
+// 2048; 2 default policy, 8 granules, 4096 (n % 8192 == 0)
+hipError_t launch_copy16(const double* src, double* dst, long n, hipStream_t st, int form) {
+    const v2d* s = (const v2d*)src;
+    v2d* d = (v2d*)dst;
+    switch (form) {
+        case 0: hipLaunchKernelGGL((k_copy16<true, 4>), dim3(2048), dim3(256), 0, st, s, d, n / 2); break;
+        case 1: hipLaunchKernelGGL((k_copy16<false, 4>), dim3(2048), dim3(256), 0, st, s, d, n / 2); break;
+        default: hipLaunchKernelGGL((k_copy16<false, 8>), dim3(4096), dim3(256), 0, st, s, d, n / 2); break;
+    }
     return hipGetLastError();
 }
 
