@@ -27,6 +27,7 @@
 // the CPU oracle.
 #include <hip/hip_runtime.h>
 
+#include <cstring>
 #include <type_traits>
 
 #include "solve_phases.h"
@@ -657,6 +658,252 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
 }
 
 // ---------------------------------------------------------------------------
+// The interface form of the two-sided solve (round 5; the default for k_solve_b<512>).
+// twisted_solve runs every forward and backward step of both chains on all 512 threads, one
+// workgroup barrier a step: 2 max(p, nb-1-p) + 1 barriers, ~820 cycles a forward step on cfg
+// 5 (profiles/r4s2_phase_cfg5.txt, s.A).  But a step only carries a few rows forward: F_s
+// (amax x 32) changes only rows [0, amax) of w_s (U_s, block s's first BFS level), and the
+// product F_s w_{s-1} reads w_{s-1}'s own updated rows U_{s-1} plus rows that no step changes
+// (b_{s-1} as the rhs left it).  So the sequential part is an amax-row recurrence:
+//     w_s[U] = b_s[U] - F_s[:, R] b_{s-1}[R] - F_s[:, U] w_{s-1}[U]        (top, s = 1..p)
+// (the bottom chain likewise on the window rows W_k = [toff_k, toff_k + bmax) with G_k), and
+// backward x_k[U] = t_k[U] - F_{k+1}[:, U]' x_{k+1}[U].  Each chain is run by ONE wave -- wave
+// 0 the top, wave 4 the bottom -- ordered by its own instruction stream (LDS fence + wave
+// barrier, no s_barrier), lane (r, q) = (lane / 4, lane % 4) taking row r and columns
+// [8 q, 8 q + 8) (a quad sum); everything that is not on the recurrence runs on all threads
+// between four workgroup barriers:
+//   F  the two forward chains (full-row products: the static columns' reads issue with the
+//      dynamic ones)                                                   -> barrier
+//   T  t_k = S_k^{-1} w_k for every block at once (M^{-1} (w_p - corB) for the middle), the
+//      factor's tiles in registers in the quad layout (TwoSidedQ)        -> barrier
+//   B  the two backward chains on the U / W rows                        -> barrier
+//   X  every other row: x_k = t_k - H_k x_{k+1}[U] (top), t_k - G_{k-1}' x_{k-1}[W] (bottom)
+//                                                                       -> barrier
+// Same factor (factorize2s), same LDS F / G rows, the same sums term for term up to their
+// association.
+template <int SL>
+struct TwoSidedQ {
+    static constexpr int NR = (SL + 1) / 2;  // rounds: two blocks per round and half
+    double Inv[NR][8];  // round r, this thread's block slot s = 2 r + sub: Inv_s[i][8 q + c]
+    __device__ __forceinline__ void load(int nb, int pm, int amax, int bmax, const double* __restrict__ Fg,
+                                         const double* __restrict__ Hg, const double* __restrict__ Sg,
+                                         double* __restrict__ Fc, double* __restrict__ Gc) {
+        const int tid = threadIdx.x, half = __builtin_amdgcn_readfirstlane(tid >> 8), u = tid & 255;
+        const int sub = u >> 7, i = (u & 127) >> 2, q = u & 3;
+        const int nbot = nb - 1 - pm;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const int s = 2 * r + sub;
+            const bool have = half == 0 ? s <= pm : s < nbot;
+            const int k = half == 0 ? s : nb - 1 - s;
+            const double* src = Sg + (long)(have ? k : 0) * SS + i * S + 8 * q;
+#pragma unroll
+            for (int c = 0; c < 8; c += 2) {
+                const double2 t2 = have ? *(const double2*)(src + c) : make_double2(0.0, 0.0);
+                Inv[r][c] = t2.x;
+                Inv[r][c + 1] = t2.y;
+            }
+        }
+        for (int o = tid; o < pm * amax * S; o += TB) {  // row q = k amax + r of F_{k+1}
+            const int qq = o >> 5, j = o & (S - 1), k = qq / amax, r = qq - k * amax;
+            Fc[qq * FGS + j] = Fg[(long)(k + 1) * SS + r * S + j];
+        }
+        for (int o = tid; o < nbot * bmax * S; o += TB) {
+            const int qq = o >> 5, j = o & (S - 1), k = qq / bmax, r = qq - k * bmax;
+            Gc[qq * FGS + j] = Hg[(long)(pm + k) * SS + r * S + j];
+        }
+    }
+};
+
+__device__ __forceinline__ double reduce4(double v) {  // sum over an aligned quad, result in all 4
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    return v;
+}
+
+__device__ __forceinline__ void chain_sync() {  // one wave's LDS stores before its later loads
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int SL>
+__device__ __forceinline__ void iface_solve(const TwoSidedQ<SL>& R, const KParams& p, const double* Fc,
+                                            const double* Gc, const int* toffL, double* rb, double* xt,
+                                            double* corB, long long* pacc) {
+#ifdef MPCQP_PHASE_PROF
+    long long t0s = clock64();
+#define SPH(k) if (pacc && threadIdx.x == 0) { const long long t_ = clock64(); pacc[k] += t_ - t0s; t0s = t_; }
+#else
+#define SPH(k)
+#endif
+    const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int nb = p.nb, pm = p.pmeet, amax = p.amax, bmax = p.bmax, nbot = nb - 1 - pm;
+    const int half = w >> 2;
+    const int r = lane >> 2, q = lane & 3;  // chain lanes: row r, columns [8 q, 8 q + 8)
+    // ---- F: the forward chains (wave 0 top, wave 4 bottom) ----
+    if (w == 0) {
+        const int ir = r < amax ? r : 0;
+        const bool wr = q == 0 && r < amax;
+#pragma unroll 1
+        for (int s = 1; s <= pm; ++s) {
+            const double* f = A16(Fc + ((s - 1) * amax + ir) * FGS + 8 * q);
+            const double* v = A16(rb + (s - 1) * S + 8 * q);
+            double* dst = rb + s * S + ir;
+            const double old = *dst;
+            double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+            for (int c = 0; c < 8; c += 2) {
+                const double2 f2 = *(const double2*)(f + c), v2 = *(const double2*)(v + c);
+                a0 = __builtin_fma(f2.x, v2.x, a0);
+                a1 = __builtin_fma(f2.y, v2.y, a1);
+            }
+            const double acc = reduce4(a0 + a1);
+            if (wr) *dst = old - acc;
+            chain_sync();
+        }
+    } else if (w == 4) {
+        const int ia = r < bmax ? r : 0;
+        const bool wr = q == 0 && r < bmax;
+#pragma unroll 1
+        for (int s = 1; s <= nbot; ++s) {
+            const int kd = nb - 1 - s;
+            const double* g = A16(Gc + ((kd - pm) * bmax + ia) * FGS + 8 * q);
+            const double* v = A16(rb + (kd + 1) * S + 8 * q);
+            const bool mid = kd == pm;
+            double* dst = (mid ? corB : rb) + kd * S + toffL[kd] + ia;
+            const double old = mid ? 0.0 : *dst;
+            double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+            for (int c = 0; c < 8; c += 2) {
+                const double2 g2 = *(const double2*)(g + c), v2 = *(const double2*)(v + c);
+                a0 = __builtin_fma(g2.x, v2.x, a0);
+                a1 = __builtin_fma(g2.y, v2.y, a1);
+            }
+            const double acc = reduce4(a0 + a1);
+            if (wr) *dst = mid ? acc : old - acc;
+            chain_sync();
+        }
+    }
+    __syncthreads();
+    SPH(12)
+    // ---- T: t_k = Inv_k w_k, every block of the half at once (quad layout) ----
+    {
+        const int u = tid & 255, sub = u >> 7, i = (u & 127) >> 2, qq = u & 3;
+#pragma unroll
+        for (int rr = 0; rr < TwoSidedQ<SL>::NR; ++rr) {
+            const int s = 2 * rr + sub;
+            const bool have = half == 0 ? s <= pm : s < nbot;
+            const int k = have ? (half == 0 ? s : nb - 1 - s) : 0;
+            const bool midb = half == 0 && s == pm;
+            const double* v = A16(rb + k * S + 8 * qq);
+            const double* cb = A16(corB + pm * S + 8 * qq);
+            double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+            for (int c = 0; c < 8; c += 2) {
+                double2 v2 = *(const double2*)(v + c);
+                if (midb) {
+                    const double2 c2 = *(const double2*)(cb + c);
+                    v2.x -= c2.x;
+                    v2.y -= c2.y;
+                }
+                a0 = __builtin_fma(R.Inv[rr][c], v2.x, a0);
+                a1 = __builtin_fma(R.Inv[rr][c + 1], v2.y, a1);
+            }
+            const double t = reduce4(a0 + a1);
+            if (have && qq == 0) xt[k * S + i] = t;
+        }
+    }
+    __syncthreads();
+    SPH(13)
+    // ---- B: the backward chains on the U (top) / W (bottom) rows ----
+    if (w == 0) {
+        const bool wr = q == 0 && r < amax;
+        const int ir = r < amax ? r : 0;
+#pragma unroll 1
+        for (int k = pm - 1; k >= 1; --k) {
+            // x_k[r] -= sum_{j < amax} F_{k+1}[j][r] x_{k+1}[j], lane q: j = 4 q + c
+            const double* f = Fc + (k * amax + 4 * q) * FGS + ir;
+            const double* xv = A16(xt + (k + 1) * S + 4 * q);
+            double* dst = xt + k * S + ir;
+            const double old = *dst;
+            double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+            for (int c = 0; c < 4; c += 2) {
+                const double2 x2 = *(const double2*)(xv + c);
+                const double f0 = 4 * q + c < amax ? f[c * FGS] : 0.0;
+                const double f1 = 4 * q + c + 1 < amax ? f[(c + 1) * FGS] : 0.0;
+                a0 = __builtin_fma(f0, x2.x, a0);
+                a1 = __builtin_fma(f1, x2.y, a1);
+            }
+            const double acc = reduce4(a0 + a1);
+            if (wr) *dst = old - acc;
+            chain_sync();
+        }
+    } else if (w == 4) {
+        const bool wr = q == 0 && r < bmax;
+        const int ia = r < bmax ? r : 0;
+#pragma unroll 1
+        for (int k = pm + 1; k <= nb - 2; ++k) {
+            // x_k[toff_k + a] -= sum_{a' < bmax} G_{k-1}[a'][toff_k + a] x_{k-1}[toff_{k-1} + a']
+            const int tk = toffL[k], tk1 = toffL[k - 1];
+            const double* g = Gc + ((k - 1 - pm) * bmax + 4 * q) * FGS + tk + ia;
+            const double* xv = xt + (k - 1) * S + tk1 + 4 * q;
+            double* dst = xt + k * S + tk + ia;
+            const double old = *dst;
+            double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+            for (int c = 0; c < 4; c += 2) {
+                const double g0 = 4 * q + c < bmax ? g[c * FGS] : 0.0;
+                const double g1 = 4 * q + c + 1 < bmax ? g[(c + 1) * FGS] : 0.0;
+                a0 = __builtin_fma(g0, xv[c], a0);
+                a1 = __builtin_fma(g1, xv[c + 1], a1);
+            }
+            const double acc = reduce4(a0 + a1);
+            if (wr) *dst = old - acc;
+            chain_sync();
+        }
+    }
+    __syncthreads();
+    // ---- X: every row the chains did not carry ----
+    {
+        const int u = tid & 255, sub = u >> 7, i = (u & 127) >> 2, qq = u & 3;
+        const int nmine = half ? nbot : pm;  // top: blocks 0 .. p-1; bottom: p+1 .. nb-1
+        const int lim = half ? bmax : amax;
+#pragma unroll 1
+        for (int s = sub; s < nmine; s += 2) {
+            const int k = half ? pm + 1 + s : s;
+            bool done;        // row i of block k was carried by the backward chain
+            const double* hv; // H_k[i][j] = F_{k+1}[j][i] (top) / G_{k-1}[j][i] (bottom), j = 4 qq + c
+            const double* xv; // x_{k+1}[j] (top) / x_{k-1}[toff_{k-1} + j] (bottom)
+            if (half == 0) {
+                done = k >= 1 && i < amax;
+                hv = Fc + (k * amax + 4 * qq) * FGS + i;
+                xv = xt + (k + 1) * S + 4 * qq;
+            } else {
+                const int tk = toffL[k];
+                done = k <= nb - 2 && i >= tk && i < tk + bmax;
+                hv = Gc + ((k - 1 - pm) * bmax + 4 * qq) * FGS + i;
+                xv = xt + (k - 1) * S + toffL[k - 1] + 4 * qq;
+            }
+            double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+            for (int c = 0; c < 4; c += 2) {
+                const double h0 = 4 * qq + c < lim ? hv[c * FGS] : 0.0;
+                const double h1 = 4 * qq + c + 1 < lim ? hv[(c + 1) * FGS] : 0.0;
+                a0 = __builtin_fma(h0, xv[c], a0);
+                a1 = __builtin_fma(h1, xv[c + 1], a1);
+            }
+            const double acc = reduce4(a0 + a1);
+            if (qq == 0 && !done) xt[k * S + i] -= acc;
+        }
+    }
+    __syncthreads();
+    SPH(14)
+#undef SPH
+}
+
+// ---------------------------------------------------------------------------
 // The two-wave variant (k_solve_b<128, ...>: nb <= 8, cfg 3/4's slack layout): one
 // wave per chain, so a sweep step is ordered by the wave's own instruction stream
 // (LDS fences + wave_barrier, no s_barrier) and the two chains run side by side;
@@ -834,7 +1081,7 @@ __device__ __forceinline__ double* big_fc(const SLds& L) {
 
 // TTK = 512: TwoSided / twisted_solve (nb up to 24); TTK = 128: TwoSidedW / wave_twisted_solve (nb <= 8).
 // NS: the most steps one chain takes, max(p, nb-1-p).
-template <int TTK, int NS, int K, int CS, int RS>
+template <int TTK, int NS, int K, int CS, int RS, bool IF = false>
 __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restrict__ xo, double* __restrict__ yo,
                                                    int factor_only) {
     const int tid = threadIdx.x;
@@ -922,10 +1169,10 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
             PH(0)
         }
         // ---- run state (re-derived at every run start; nothing but scalars lives across calls) ----
-        std::conditional_t<TTK == 512, TwoSided<NS + 1>, TwoSidedW<NS>> RF;
+        std::conditional_t<IF, TwoSidedQ<NS + 1>, std::conditional_t<TTK == 512, TwoSided<NS + 1>, TwoSidedW<NS>>> RF;
         RF.load(nb, p.pmeet, amax, p.bmax, Fg, Hg, Sg, Fc, Gc);
         int so[NS + 1], fo[NS + 1];  // (TTK == 512, NS < 10: twisted_solve's step offsets)
-        if constexpr (TTK == 512 && NS < 10) step_offsets<NS + 1>(p, toffL, L.rb, L.xt, L.tv, Fc, so, fo);
+        if constexpr (!IF && TTK == 512 && NS < 10) step_offsets<NS + 1>(p, toffL, L.rb, L.xt, L.tv, Fc, so, fo);
         int cvar[CS];
         // gather lists as LDS-base offsets (GatherR): A' w for the rhs, A x~ for the rows
         extern __shared__ __attribute__((aligned(16))) double smb[];
@@ -975,7 +1222,8 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
 #else
             long long* pacc = nullptr;
 #endif
-            if constexpr (TTK == 512) twisted_solve<NS + 1>(RF, p, Fc, Gc, toffL, so, fo, L.rb, L.xt, L.tv, pacc);
+            if constexpr (IF) iface_solve<NS + 1>(RF, p, Fc, Gc, toffL, L.rb, L.xt, L.tv, pacc);
+            else if constexpr (TTK == 512) twisted_solve<NS + 1>(RF, p, Fc, Gc, toffL, so, fo, L.rb, L.xt, L.tv, pacc);
             else wave_twisted_solve<NS>(RF, p, Fc, Gc, toffL, L.rb, L.xt, L.cor, pacc);
             PH(2)
             // z~ = A x~ ; relaxed + projected z ; y ; next w.   x update; deltas for the checks.
@@ -1075,10 +1323,21 @@ size_t lds_solve_bytes_big(const KParams& p) {
     return lds_solve_bytes(p) + 16 + sizeof(double) * (size_t)big_fg_len(p) + sizeof(int) * (size_t)p.nb;
 }
 
+// the interface form (iface_solve) unless MPCQP_BIG_FORM=twisted (A/B against round 4's sweep)
+static bool big_iface() {
+    static const bool on = [] {
+        const char* e = getenv("MPCQP_BIG_FORM");
+        return !(e && !strcmp(e, "twisted"));
+    }();
+    return on;
+}
+
 template <int TTK, int NS, int K, int CS, int RS>
 static hipError_t go_b(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st, KernelRef* ref) {
     const size_t lds = lds_solve_bytes_big(p);
     auto k = k_solve_b<TTK, NS, K, CS, RS>;
+    if constexpr (TTK == 512)
+        if (big_iface() && p.amax <= 16 && p.bmax <= 16) k = k_solve_b<TTK, NS, K, CS, RS, true>;
     if (ref) { *ref = {(const void*)k, TTK, lds}; return hipSuccess; }
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
