@@ -87,6 +87,8 @@ def parse(argv=None):
                     help="skip the identity-dispatch diagnostic (rocprof passes: one handle's launches only)")
     ap.add_argument("--no-pcie", action="store_true",
                     help="skip the PCIe-inclusive diagnostic (host buffers in, host buffers out)")
+    ap.add_argument("--no-latency", action="store_true",
+                    help="skip the per-call latency diagnostic (one cfg-5 QP through the osqp shim)")
     return ap.parse_args(argv)
 
 
@@ -402,6 +404,49 @@ def pcie_leg(solver, dev, local, bufs, host_in, outs, pin, steps, mode, warmup=4
             gc.enable()
 
 
+def latency_leg(reps=30, warmup=3):
+    """Per-call latency of the reference's Control/MPC call pattern, never `value`: a fresh
+    osqp.OSQP() + setup() + solve() of ONE QP every call (Control/MPC/mpc_dynamics.py:392-396,
+    mpc_kinematics.py:194-198), through the `import osqp` shim on the GPU, beside the oracle
+    (one host thread) doing the same calls on the same QP.  The QP: instance 0 of the cfg-5
+    generator (incremental dynamic MPC, N = 50, cold start as mpc_increment sets it).  Medians
+    over `reps` calls; per-iteration figures divide the whole call by the ADMM iterations."""
+    import pyoracle
+    from osqp_amd import OSQP, mpc
+    b = mpc.make_batch(5, B=1, seed=1)
+    P, A = b["P"].copy(), b["A"].copy()
+    P.data, A.data = b["Px"][0].copy(), b["Ax"][0].copy()
+    q, l, u = b["q"][0].copy(), b["l"][0].copy(), b["u"][0].copy()
+    settings = {k: v for k, v in b["settings"].items() if k != "verbose"}
+    out = {}
+    for name, cls in (("gpu", OSQP), ("cpu", pyoracle.OSQP)):
+        ts, tv, it = [], [], 0
+        for r in range(warmup + reps):
+            t0 = time.perf_counter()
+            o = cls()
+            o.setup(P, q, A, l, u, **settings)
+            t1 = time.perf_counter()
+            res = o.solve()
+            t2 = time.perf_counter()
+            del o
+            if r >= warmup:
+                ts.append(t1 - t0)
+                tv.append(t2 - t1)
+                it = int(res.info.iter)
+                st = res.info.status
+        tot = float(np.median(np.add(ts, tv)))
+        out[name] = {"call_ms": tot * 1e3, "setup_ms": float(np.median(ts)) * 1e3,
+                     "solve_ms": float(np.median(tv)) * 1e3, "iters": it, "status": st,
+                     "us_per_iter": tot * 1e6 / max(1, it), "solve_us_per_iter": float(np.median(tv)) * 1e6 / max(1, it)}
+    out["cpu"]["threads"] = 1
+    out.update(workload="incremental-dynamic-N50, ONE QP (n 508, m 916), fresh OSQP()+setup()+solve() per call, "
+                        "cold (mpc_dynamics.py:392-396)",
+               reps=reps, gpu_over_cpu_call=out["gpu"]["call_ms"] / out["cpu"]["call_ms"],
+               method="host arrays through the osqp shim (osqp_amd.OSQP) vs oracle/osqp_oracle.c (pyoracle.OSQP, one "
+                      "thread); medians; us_per_iter = the whole call / ADMM iterations")
+    return out
+
+
 def main(argv=None, solver_cls=None, device=None):
     """argv: the command line (default sys.argv[1:]).  solver_cls / device: a stand-in for
     osqp_amd.DeviceBatch and its torch device -- only tests/test_multiproc.py passes them,
@@ -688,6 +733,10 @@ def main(argv=None, solver_cls=None, device=None):
                # the sampled instances' control blocks (GPU base-batch solve vs the oracle's)
                "parity_max_du": float(np.nanmax(np.abs(u_base[:nc] - rc.x[:, b["u_block"]])))}
 
+    latency = None
+    if rank == 0 and world == 1 and on_gpu and not args.no_cpu and not args.no_latency:
+        latency = latency_leg()
+
     if rank == 0:
         kname = solve_kernel_name(info, fused=fused)
         line = {
@@ -738,6 +787,7 @@ def main(argv=None, solver_cls=None, device=None):
                          "fp64_tflops_model": fp64_tflops, "fp64_peak_tflops": FP64_PEAK_TFLOPS},
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
+            "latency": latency,
         }
         if json_fd == 1:
             print(json.dumps(line), flush=True)

@@ -35,10 +35,12 @@
 namespace mpcqp {
 
 constexpr int TB = kThreadsBig;
-// row stride of the F / G rows in LDS: 40 doubles, so the 8 rows a wave reads at once
-// (and the 8 columns it reads transposed) fall on different banks (stride 32: 8-way
-// conflicts)
-constexpr int FGS = 40;
+// row stride of the F / G rows in LDS: 42 doubles.  The interface form's chain lanes (r, q)
+// read row r, columns [8 q, 8 q + 8) as ds_read_b128, and the backward chain / fill lanes read
+// the columns 4 q + c of row block k at row i: with a stride of 2 (mod 8) doubles both are
+// conflict-free (LDS bank model, 64 banks of 4 B: 16 LDS cycles for the four 16-byte reads of
+// a step at 34, 38, 42, ..., 64 at 40, 32, 48)
+constexpr int FGS = 42;
 
 // ---------------------------------------------------------------------------
 // Two-sided ("twisted") block factorisation of K = tridiag(E_k, D_k, E_{k+1}'),
