@@ -143,6 +143,8 @@ size_t carve(size_t& off, size_t count) {
 void shape_params(const Plan& pl, KParams& k) {
     k.n = pl.n; k.m = pl.m; k.nb = pl.nb; k.npad = pl.npad; k.nnzP = pl.nnzP; k.nnzA = pl.nnzA; k.amax = pl.amax;
     k.bmax = pl.bmax; k.pmeet = (pl.nb - 1) / 2;
+    k.ifok = pl.nb > 4 && pl.nb <= 64 && pl.amax <= 16 && pl.bmax <= 16 && pl.toff[k.pmeet] >= pl.amax &&
+             pl.toff[k.pmeet] + pl.bmax <= kS;
     k.bsz01 = k.bsz23 = 1 << 20;
     if (pl.nb == 4) {
         k.bsz01 = std::max(pl.bsize[0], pl.bsize[1]);

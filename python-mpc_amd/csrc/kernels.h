@@ -33,6 +33,8 @@ struct KParams {
     int gk1;          // most nonzeros in a row >= 128 (the two-wave kernel's second row slot)
     int gkr, gkc;     // most nonzeros in a row / a column of A (gk = the larger)
     int bmax, pmeet;  // two-sided factorisation (solve_big.hip): tail width, meeting block
+    int ifok;         // the interface form of the two-sided solve fits (solve_big.hip::iface_solve):
+                      // amax, bmax <= 16 and the meeting block's top rows and window disjoint
     int bsz01, bsz23; // largest of blocks 0 and 1 / 2 and 3 (real columns; nb = 4 plans)
     int variant;  // solve-kernel instantiation (solve.hip: launch_solve)
     int mode;     // factor storage of that variant (solve.hip: factorize)

@@ -729,10 +729,16 @@ __device__ __forceinline__ void chain_sync() {  // one wave's LDS stores before 
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// toff[k] of the lane's wave-uniform k: the window offsets are held one per lane (lane k, loaded
+// once per solve), so a step forms its addresses without an LDS round trip
+__device__ __forceinline__ int toff_of(int tv, int k) { return __builtin_amdgcn_readlane(tv, k); }
+
+// The middle block p's top rows [0, amax) and window [toff_p, toff_p + bmax) must be disjoint
+// (KParams::ifok): both chains then update w_p in place, and t_p = M^{-1} w_p needs no correction.
 template <int SL>
 __device__ __forceinline__ void iface_solve(const TwoSidedQ<SL>& R, const KParams& p, const double* Fc,
-                                            const double* Gc, const int* toffL, double* rb, double* xt,
-                                            double* corB, long long* pacc) {
+                                            const double* Gc, const int tv, double* rb, double* xt,
+                                            double* sink, long long* pacc) {
 #ifdef MPCQP_PHASE_PROF
     long long t0s = clock64();
 #define SPH(k) if (pacc && threadIdx.x == 0) { const long long t_ = clock64(); pacc[k] += t_ - t0s; t0s = t_; }
@@ -743,10 +749,10 @@ __device__ __forceinline__ void iface_solve(const TwoSidedQ<SL>& R, const KParam
     const int nb = p.nb, pm = p.pmeet, amax = p.amax, bmax = p.bmax, nbot = nb - 1 - pm;
     const int half = w >> 2;
     const int r = lane >> 2, q = lane & 3;  // chain lanes: row r, columns [8 q, 8 q + 8)
-    // ---- F: the forward chains (wave 0 top, wave 4 bottom) ----
+    // ---- F: the forward chains (wave 0 top, wave 4 bottom).  Lanes past the chain's rows take
+    // row 0 and store row 0's value again (the same sum): no lane mask in the chain ----
     if (w == 0) {
         const int ir = r < amax ? r : 0;
-        const bool wr = q == 0 && r < amax;
 #pragma unroll 1
         for (int s = 1; s <= pm; ++s) {
             const double* f = A16(Fc + ((s - 1) * amax + ir) * FGS + 8 * q);
@@ -760,21 +766,18 @@ __device__ __forceinline__ void iface_solve(const TwoSidedQ<SL>& R, const KParam
                 a0 = __builtin_fma(f2.x, v2.x, a0);
                 a1 = __builtin_fma(f2.y, v2.y, a1);
             }
-            const double acc = reduce4(a0 + a1);
-            if (wr) *dst = old - acc;
+            *dst = old - reduce4(a0 + a1);
             chain_sync();
         }
     } else if (w == 4) {
         const int ia = r < bmax ? r : 0;
-        const bool wr = q == 0 && r < bmax;
 #pragma unroll 1
         for (int s = 1; s <= nbot; ++s) {
             const int kd = nb - 1 - s;
             const double* g = A16(Gc + ((kd - pm) * bmax + ia) * FGS + 8 * q);
             const double* v = A16(rb + (kd + 1) * S + 8 * q);
-            const bool mid = kd == pm;
-            double* dst = (mid ? corB : rb) + kd * S + toffL[kd] + ia;
-            const double old = mid ? 0.0 : *dst;
+            double* dst = rb + kd * S + toff_of(tv, kd) + ia;
+            const double old = *dst;
             double a0 = 0.0, a1 = 0.0;
 #pragma unroll
             for (int c = 0; c < 8; c += 2) {
@@ -782,122 +785,105 @@ __device__ __forceinline__ void iface_solve(const TwoSidedQ<SL>& R, const KParam
                 a0 = __builtin_fma(g2.x, v2.x, a0);
                 a1 = __builtin_fma(g2.y, v2.y, a1);
             }
-            const double acc = reduce4(a0 + a1);
-            if (wr) *dst = mid ? acc : old - acc;
+            *dst = old - reduce4(a0 + a1);
             chain_sync();
         }
     }
     __syncthreads();
     SPH(12)
-    // ---- T: t_k = Inv_k w_k, every block of the half at once (quad layout) ----
-    {
-        const int u = tid & 255, sub = u >> 7, i = (u & 127) >> 2, qq = u & 3;
+    // ---- T: t_k = Inv_k w_k, every block of the half at once (quad layout; a slot past the
+    // half's blocks reads block 0 and stores to the sink) ----
+    const int u = tid & 255, sub = u >> 7, i = (u & 127) >> 2, qq = u & 3;
 #pragma unroll
-        for (int rr = 0; rr < TwoSidedQ<SL>::NR; ++rr) {
-            const int s = 2 * rr + sub;
-            const bool have = half == 0 ? s <= pm : s < nbot;
-            const int k = have ? (half == 0 ? s : nb - 1 - s) : 0;
-            const bool midb = half == 0 && s == pm;
-            const double* v = A16(rb + k * S + 8 * qq);
-            const double* cb = A16(corB + pm * S + 8 * qq);
-            double a0 = 0.0, a1 = 0.0;
+    for (int rr = 0; rr < TwoSidedQ<SL>::NR; ++rr) {
+        const int s = 2 * rr + sub;
+        const bool have = half == 0 ? s <= pm : s < nbot;
+        const int k = have ? (half == 0 ? s : nb - 1 - s) : 0;
+        const double* v = A16(rb + k * S + 8 * qq);
+        double a0 = 0.0, a1 = 0.0;
 #pragma unroll
-            for (int c = 0; c < 8; c += 2) {
-                double2 v2 = *(const double2*)(v + c);
-                if (midb) {
-                    const double2 c2 = *(const double2*)(cb + c);
-                    v2.x -= c2.x;
-                    v2.y -= c2.y;
-                }
-                a0 = __builtin_fma(R.Inv[rr][c], v2.x, a0);
-                a1 = __builtin_fma(R.Inv[rr][c + 1], v2.y, a1);
-            }
-            const double t = reduce4(a0 + a1);
-            if (have && qq == 0) xt[k * S + i] = t;
+        for (int c = 0; c < 8; c += 2) {
+            const double2 v2 = *(const double2*)(v + c);
+            a0 = __builtin_fma(R.Inv[rr][c], v2.x, a0);
+            a1 = __builtin_fma(R.Inv[rr][c + 1], v2.y, a1);
         }
+        *(have ? xt + k * S + i : sink + i) = reduce4(a0 + a1);
     }
     __syncthreads();
     SPH(13)
     // ---- B: the backward chains on the U (top) / W (bottom) rows ----
     if (w == 0) {
-        const bool wr = q == 0 && r < amax;
         const int ir = r < amax ? r : 0;
+        const int j0 = min(4 * q, amax - 1), j1 = min(4 * q + 1, amax - 1), j2 = min(4 * q + 2, amax - 1),
+                  j3 = min(4 * q + 3, amax - 1);
+        const double m0 = 4 * q < amax ? 1.0 : 0.0, m1 = 4 * q + 1 < amax ? 1.0 : 0.0,
+                     m2 = 4 * q + 2 < amax ? 1.0 : 0.0, m3 = 4 * q + 3 < amax ? 1.0 : 0.0;
 #pragma unroll 1
         for (int k = pm - 1; k >= 1; --k) {
             // x_k[r] -= sum_{j < amax} F_{k+1}[j][r] x_{k+1}[j], lane q: j = 4 q + c
-            const double* f = Fc + (k * amax + 4 * q) * FGS + ir;
+            const double* f = Fc + k * amax * FGS + ir;
             const double* xv = A16(xt + (k + 1) * S + 4 * q);
             double* dst = xt + k * S + ir;
             const double old = *dst;
-            double a0 = 0.0, a1 = 0.0;
-#pragma unroll
-            for (int c = 0; c < 4; c += 2) {
-                const double2 x2 = *(const double2*)(xv + c);
-                const double f0 = 4 * q + c < amax ? f[c * FGS] : 0.0;
-                const double f1 = 4 * q + c + 1 < amax ? f[(c + 1) * FGS] : 0.0;
-                a0 = __builtin_fma(f0, x2.x, a0);
-                a1 = __builtin_fma(f1, x2.y, a1);
-            }
-            const double acc = reduce4(a0 + a1);
-            if (wr) *dst = old - acc;
+            const double2 x01 = *(const double2*)xv, x23 = *(const double2*)(xv + 2);
+            const double f0 = m0 * f[j0 * FGS], f1 = m1 * f[j1 * FGS], f2 = m2 * f[j2 * FGS], f3 = m3 * f[j3 * FGS];
+            const double a0 = __builtin_fma(f2, x23.x, f0 * x01.x), a1 = __builtin_fma(f3, x23.y, f1 * x01.y);
+            *dst = old - reduce4(a0 + a1);
             chain_sync();
         }
     } else if (w == 4) {
-        const bool wr = q == 0 && r < bmax;
         const int ia = r < bmax ? r : 0;
+        const int j0 = min(4 * q, bmax - 1), j1 = min(4 * q + 1, bmax - 1), j2 = min(4 * q + 2, bmax - 1),
+                  j3 = min(4 * q + 3, bmax - 1);
+        const double m0 = 4 * q < bmax ? 1.0 : 0.0, m1 = 4 * q + 1 < bmax ? 1.0 : 0.0,
+                     m2 = 4 * q + 2 < bmax ? 1.0 : 0.0, m3 = 4 * q + 3 < bmax ? 1.0 : 0.0;
 #pragma unroll 1
         for (int k = pm + 1; k <= nb - 2; ++k) {
             // x_k[toff_k + a] -= sum_{a' < bmax} G_{k-1}[a'][toff_k + a] x_{k-1}[toff_{k-1} + a']
-            const int tk = toffL[k], tk1 = toffL[k - 1];
-            const double* g = Gc + ((k - 1 - pm) * bmax + 4 * q) * FGS + tk + ia;
-            const double* xv = xt + (k - 1) * S + tk1 + 4 * q;
+            const int tk = toff_of(tv, k), tk1 = toff_of(tv, k - 1);
+            const double* g = Gc + (k - 1 - pm) * bmax * FGS + tk + ia;
+            const double* xv = xt + (k - 1) * S + tk1;
             double* dst = xt + k * S + tk + ia;
             const double old = *dst;
-            double a0 = 0.0, a1 = 0.0;
-#pragma unroll
-            for (int c = 0; c < 4; c += 2) {
-                const double g0 = 4 * q + c < bmax ? g[c * FGS] : 0.0;
-                const double g1 = 4 * q + c + 1 < bmax ? g[(c + 1) * FGS] : 0.0;
-                a0 = __builtin_fma(g0, xv[c], a0);
-                a1 = __builtin_fma(g1, xv[c + 1], a1);
-            }
-            const double acc = reduce4(a0 + a1);
-            if (wr) *dst = old - acc;
+            const double g0 = m0 * g[j0 * FGS], g1 = m1 * g[j1 * FGS], g2 = m2 * g[j2 * FGS], g3 = m3 * g[j3 * FGS];
+            const double a0 = __builtin_fma(g2, xv[j2], g0 * xv[j0]), a1 = __builtin_fma(g3, xv[j3], g1 * xv[j1]);
+            *dst = old - reduce4(a0 + a1);
             chain_sync();
         }
     }
     __syncthreads();
-    // ---- X: every row the chains did not carry ----
+    // ---- X: every row the chains did not carry (rows the chains carried store to the sink) ----
     {
-        const int u = tid & 255, sub = u >> 7, i = (u & 127) >> 2, qq = u & 3;
-        const int nmine = half ? nbot : pm;  // top: blocks 0 .. p-1; bottom: p+1 .. nb-1
         const int lim = half ? bmax : amax;
-#pragma unroll 1
-        for (int s = sub; s < nmine; s += 2) {
-            const int k = half ? pm + 1 + s : s;
-            bool done;        // row i of block k was carried by the backward chain
-            const double* hv; // H_k[i][j] = F_{k+1}[j][i] (top) / G_{k-1}[j][i] (bottom), j = 4 qq + c
-            const double* xv; // x_{k+1}[j] (top) / x_{k-1}[toff_{k-1} + j] (bottom)
+        const int j0 = min(4 * qq, lim - 1), j1 = min(4 * qq + 1, lim - 1), j2 = min(4 * qq + 2, lim - 1),
+                  j3 = min(4 * qq + 3, lim - 1);
+        const double m0 = 4 * qq < lim ? 1.0 : 0.0, m1 = 4 * qq + 1 < lim ? 1.0 : 0.0,
+                     m2 = 4 * qq + 2 < lim ? 1.0 : 0.0, m3 = 4 * qq + 3 < lim ? 1.0 : 0.0;
+#pragma unroll
+        for (int rr = 0; rr < TwoSidedQ<SL>::NR; ++rr) {
+            const int s = 2 * rr + sub;
+            // top: blocks 0 .. p-1 (H_k = F_{k+1}'), bottom: p+1 .. nb-1 (G_{k-1}')
+            const bool have = half == 0 ? s < pm : s < nbot;
+            const int k = have ? (half == 0 ? s : pm + 1 + s) : (half == 0 ? 0 : pm + 1);
+            bool done;         // row i of block k was carried by the backward chain
+            const double* hv;  // H_k[i][j] = F_{k+1}[j][i] (top) / G_{k-1}[j][i] (bottom), j = 4 qq + c
+            const double* xv;  // x_{k+1}[j] (top) / x_{k-1}[toff_{k-1} + j] (bottom)
             if (half == 0) {
                 done = k >= 1 && i < amax;
-                hv = Fc + (k * amax + 4 * qq) * FGS + i;
-                xv = xt + (k + 1) * S + 4 * qq;
+                hv = Fc + k * amax * FGS + i;
+                xv = xt + (k + 1) * S;
             } else {
-                const int tk = toffL[k];
+                const int tk = toff_of(tv, k);
                 done = k <= nb - 2 && i >= tk && i < tk + bmax;
-                hv = Gc + ((k - 1 - pm) * bmax + 4 * qq) * FGS + i;
-                xv = xt + (k - 1) * S + toffL[k - 1] + 4 * qq;
+                hv = Gc + (k - 1 - pm) * bmax * FGS + i;
+                xv = xt + (k - 1) * S + toff_of(tv, k - 1);
             }
-            double a0 = 0.0, a1 = 0.0;
-#pragma unroll
-            for (int c = 0; c < 4; c += 2) {
-                const double h0 = 4 * qq + c < lim ? hv[c * FGS] : 0.0;
-                const double h1 = 4 * qq + c + 1 < lim ? hv[(c + 1) * FGS] : 0.0;
-                a0 = __builtin_fma(h0, xv[c], a0);
-                a1 = __builtin_fma(h1, xv[c + 1], a1);
-            }
+            const double h0 = m0 * hv[j0 * FGS], h1 = m1 * hv[j1 * FGS], h2 = m2 * hv[j2 * FGS], h3 = m3 * hv[j3 * FGS];
+            const double a0 = __builtin_fma(h2, xv[j2], h0 * xv[j0]), a1 = __builtin_fma(h3, xv[j3], h1 * xv[j1]);
+            double* dst = xt + k * S + i;
             const double acc = reduce4(a0 + a1);
-            if (qq == 0 && !done) xt[k * S + i] -= acc;
+            const double old = *dst;
+            *((have && !done) ? dst : sink + i) = old - acc;
         }
     }
     __syncthreads();
@@ -1174,6 +1160,12 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
         std::conditional_t<IF, TwoSidedQ<NS + 1>, std::conditional_t<TTK == 512, TwoSided<NS + 1>, TwoSidedW<NS>>> RF;
         RF.load(nb, p.pmeet, amax, p.bmax, Fg, Hg, Sg, Fc, Gc);
         int so[NS + 1], fo[NS + 1];  // (TTK == 512, NS < 10: twisted_solve's step offsets)
+        // the interface form: toff[lane] in one VGPR (iface_solve::toff_of)
+        int tvl = 0;
+        if constexpr (IF) {
+            tvl = (tid & 63) < nb ? toffL[tid & 63] : 0;
+            asm volatile("" : "+v"(tvl));
+        }
         if constexpr (!IF && TTK == 512 && NS < 10) step_offsets<NS + 1>(p, toffL, L.rb, L.xt, L.tv, Fc, so, fo);
         int cvar[CS];
         // gather lists as LDS-base offsets (GatherR): A' w for the rhs, A x~ for the rows
@@ -1224,7 +1216,7 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
 #else
             long long* pacc = nullptr;
 #endif
-            if constexpr (IF) iface_solve<NS + 1>(RF, p, Fc, Gc, toffL, L.rb, L.xt, L.tv, pacc);
+            if constexpr (IF) iface_solve<NS + 1>(RF, p, Fc, Gc, tvl, L.rb, L.xt, L.tv, pacc);
             else if constexpr (TTK == 512) twisted_solve<NS + 1>(RF, p, Fc, Gc, toffL, so, fo, L.rb, L.xt, L.tv, pacc);
             else wave_twisted_solve<NS>(RF, p, Fc, Gc, toffL, L.rb, L.xt, L.cor, pacc);
             PH(2)
@@ -1339,7 +1331,7 @@ static hipError_t go_b(const KParams& p, long B, double* xo, double* yo, int fo,
     const size_t lds = lds_solve_bytes_big(p);
     auto k = k_solve_b<TTK, NS, K, CS, RS>;
     if constexpr (TTK == 512)
-        if (big_iface() && p.amax <= 16 && p.bmax <= 16) k = k_solve_b<TTK, NS, K, CS, RS, true>;
+        if (big_iface() && p.ifok) k = k_solve_b<TTK, NS, K, CS, RS, true>;
     if (ref) { *ref = {(const void*)k, TTK, lds}; return hipSuccess; }
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
