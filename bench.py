@@ -325,7 +325,7 @@ class PinnedHost:
         self.owned = []
 
 
-def pcie_leg(solver, dev, local, bufs, host_in, outs, pin, steps, mode, warmup=4):
+def pcie_leg(solver, dev, local, bufs, host_in, outs, pin, steps, mode, warmup=8, ctx=None):
     """PCIe-inclusive rate (diagnostic, never `value`): every step copies
     the batch's Px, Ax, q, l, u from pinned host memory (PinnedHost) to HBM, runs the same
     mpcqp_setup_solve_device call as the timed step, and copies x, y, status, iters back to
@@ -342,7 +342,9 @@ def pcie_leg(solver, dev, local, bufs, host_in, outs, pin, steps, mode, warmup=4
     kernel.  A variant with the downloads behind each kernel on its own stream measured no
     better, profiles/r4s2_pcie/.)  Python's cyclic collector is off inside the timed loop.
     bufs: [(dPx, dAx, dq, dl, du, dx, dy, dst, dit)] x (1 or 2); host_in: [(hPx, hAx, hq,
-    hl, hu)] cycled over the steps; outs: two sets of host outputs.  Returns s per step."""
+    hl, hu)] cycled over the steps; outs: two sets of host outputs.  ctx: a dict that keeps the
+    copy stream and the events from pass to pass (round 5: a stream created per pass made the
+    first pipelined pass of a run the slowest, 0.75-0.85 ms against 0.45-0.57).  Returns s per step."""
     import gc
     import torch
     H2D, D2H = 1, 2
@@ -350,12 +352,14 @@ def pcie_leg(solver, dev, local, bufs, host_in, outs, pin, steps, mode, warmup=4
     # it may share (GPU_MAX_HW_QUEUES = 4) with the handle's stream -- a shared queue runs the
     # copies and kernels in one order and the pipelined leg fell to the serial rate in about
     # one pass of three (0.72 against 0.45 ms per step, round 4)
-    cs = torch.cuda.Stream(dev, priority=-1)
+    ctx = {} if ctx is None else ctx
+    if "cs" not in ctx:
+        ctx["cs"] = torch.cuda.Stream(dev, priority=-1)
+        ctx["ks"] = torch.cuda.ExternalStream(solver.stream_handle().value, device=torch.device("cuda", local))
+        ctx["ready"] = [torch.cuda.Event() for _ in range(2)]
+        ctx["done"] = [torch.cuda.Event() for _ in range(2)]
+    cs, ks, ready, done = ctx["cs"], ctx["ks"], ctx["ready"], ctx["done"]
     piped = mode == "pipelined"
-    if piped:
-        ks = torch.cuda.ExternalStream(solver.stream_handle().value, device=torch.device("cuda", local))
-        ready = [torch.cuda.Event() for _ in range(2)]
-        done = [torch.cuda.Event() for _ in range(2)]
 
     def down(i):
         for hh, dd in zip(outs[i % 2], bufs[i % len(bufs)][5:]):
@@ -651,11 +655,14 @@ def main(argv=None, solver_cls=None, device=None):
             set0 = (dPx, dAx, dq, dl.clone(), du.clone(), dx, dy, dst, dit)
             set1 = tuple(t.clone() for t in set0)
             outs = [tuple(ph.like(t) for t in set0[5:]) for _ in range(2)]
-            # three passes of each, alternated (single passes varied by tens of percent)
-            ser, pip = [], []
-            for _ in range(3):
-                ser.append(pcie_leg(solver, dev, local, [set0], host_in, outs, ph, args.steps, "serial"))
-                pip.append(pcie_leg(solver, dev, local, [set0, set1], host_in, outs, ph, args.steps, "pipelined"))
+            # five passes of each, alternated, on one copy stream (a warm-up pass of each first)
+            ser, pip, ctx = [], [], {}
+            pcie_leg(solver, dev, local, [set0], host_in, outs, ph, args.steps, "serial", ctx=ctx)
+            pcie_leg(solver, dev, local, [set0, set1], host_in, outs, ph, args.steps, "pipelined", ctx=ctx)
+            for _ in range(5):
+                ser.append(pcie_leg(solver, dev, local, [set0], host_in, outs, ph, args.steps, "serial", ctx=ctx))
+                pip.append(pcie_leg(solver, dev, local, [set0, set1], host_in, outs, ph, args.steps, "pipelined",
+                                    ctx=ctx))
         finally:
             _t.cuda.synchronize(dev)
             solver.synchronize()
@@ -671,7 +678,10 @@ def main(argv=None, solver_cls=None, device=None):
                 "method": "hipHostMalloc host buffers: H2D of Px, Ax, q, l, u, the same setup_solve call, D2H "
                           "of x, y, status, iters every step; serial on one stream / pipelined over two "
                           "buffer sets, copies on their own stream beside the kernels (bench.py::pcie_leg); "
-                          "the median of three alternated passes of each; never `value`"}
+                          "the median of five alternated passes of each after an untimed one, one copy stream "
+                          "for all; never `value`",
+                "spread_pipelined": (max(pip) - min(pip)) / float(np.median(pip)),
+                "spread_serial": (max(ser) - min(ser)) / float(np.median(ser))}
         del set1
 
     value = B_global * args.steps / dt

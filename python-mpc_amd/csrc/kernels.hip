@@ -184,6 +184,20 @@ __global__ __launch_bounds__(T) void k_setup_r(KParams p, const double* __restri
     setup_r_body<T, K, KP, 1, AS, PS, KEEP>(p, (long)blockIdx.x, Px_in, Ax_in, q_in, l_in, u_in, sm);
 }
 
+// the same for the long-horizon plans (cfg 5: npad 544, m 916, nnz(A) 2666): 1024 threads, one
+// padded column and one row per thread, three A values -- the register-list setup instead of
+// k_setup's index chains (one cfg-5 instance: ten Ruiz passes ~165 us there)
+constexpr int TWIDE = 1024;
+template <int K, int KP, int AS, int PS, bool KEEP>
+__global__ __launch_bounds__(TWIDE) void k_setup_rw(KParams p, const double* __restrict__ Px_in,
+                                                    const double* __restrict__ Ax_in,
+                                                    const double* __restrict__ q_in,
+                                                    const double* __restrict__ l_in,
+                                                    const double* __restrict__ u_in) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    setup_r_body<TWIDE, K, KP, 1, AS, PS, KEEP>(p, (long)blockIdx.x, Px_in, Ax_in, q_in, l_in, u_in, sm);
+}
+
 // ------------------------------------------------------- matrix update --
 // osqp_update_P / osqp_update_A / osqp_update_P_A (OSQP 0.6; the call the reference's
 // commented-out update(Px=, Px_idx=) at vehicle_lateral_mpc_slack_increment.py:236 would
@@ -354,6 +368,10 @@ static int setup_r_variant(const KParams& p) {
     if (p.gk <= 8 && p.nnzA <= 3 * T && p.nnzP <= T) return 2;
     return 0;
 }
+// the 1024-thread one (k_setup_rw): 1 when it fits
+static int setup_rw_fits(const KParams& p) {
+    return p.npad <= TWIDE && p.m <= TWIDE && p.pk <= 4 && p.gk <= 8 && p.nnzA <= 3 * TWIDE && p.nnzP <= TWIDE;
+}
 
 hipError_t launch_setup(const KParams& p, long B, const double* Px, const double* Ax, const double* q,
                         const double* l, const double* u, hipStream_t st, bool keep) {
@@ -364,6 +382,14 @@ hipError_t launch_setup(const KParams& p, long B, const double* Px, const double
         hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(T), lds, st, p, Px, Ax, q, l, u);
+        return hipGetLastError();
+    }
+    if (setup_rw_fits(p) && !getenv_flag("MPCQP_SETUP_STAGED")) {
+        const size_t lds = lds_setup_r_bytes(p.nnzP, p.nnzA, p.npad, p.m, TWIDE);
+        auto k = keep ? k_setup_rw<8, 4, 3, 1, true> : k_setup_rw<8, 4, 3, 1, false>;
+        hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(TWIDE), lds, st, p, Px, Ax, q, l, u);
         return hipGetLastError();
     }
     size_t lds = lds_setup_bytes(p);

@@ -17,7 +17,7 @@
 // K: gather-list length (>= gather_k), KP (>= p_k), AS / PS: A / P values per thread.
 // KEEP: a matrix update (kernels.hip::k_unscale_mat, OSQP 0.6 osqp_update_P_A) -- the data
 // is scaled afresh but the iterates x, z, y, the row classes and rho are left as they are.
-// sm: LDS, sizeof(double) * (nnzP + nnzA + npad + m + 10) + 16 bytes.
+// sm: LDS, lds_setup_r_bytes(nnzP, nnzA, npad, m, TT).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -26,8 +26,8 @@
 
 namespace mpcqp {
 
-__host__ __device__ inline size_t lds_setup_r_bytes(int nnzP, int nnzA, int npad, int m) {
-    return sizeof(double) * ((size_t)nnzP + 1 + nnzA + 1 + npad + m + 8) + 16;
+__host__ __device__ inline size_t lds_setup_r_bytes(int nnzP, int nnzA, int npad, int m, int tt = 256) {
+    return sizeof(double) * ((size_t)nnzP + 1 + nnzA + 1 + npad + m + (tt > 512 ? tt / 64 : 8)) + 16;
 }
 
 template <int TT, int K, int KP, int RS, int AS, int PS, bool KEEP = false>
@@ -41,8 +41,9 @@ __device__ __forceinline__ void setup_r_body(const KParams& p, const long b, con
     double* Ac = Pv + nnzP + 1;    // [nnzA + 1]  padded-CSC order, Ac[nnzA] = 0
     double* Dt = Ac + nnzA + 1;    // [npad]
     double* Et = Dt + npad;        // [m]
-    double* red = Et + m;          // [8]
-    int* flag = (int*)(red + 8);
+    constexpr int NRED = TT > 512 ? TT / 64 : 8;  // block_sum / block_max: one slot per wave
+    double* red = Et + m;          // [NRED]
+    int* flag = (int*)(red + NRED);
     const unsigned pbase = lds_addr(Pv), abase = lds_addr(Ac);
     // registers: the thread's column pc = tid and rows tid + s * TT
     const int pc = tid;

@@ -736,9 +736,13 @@ __device__ __forceinline__ int toff_of(int tv, int k) { return __builtin_amdgcn_
 // The middle block p's top rows [0, amax) and window [toff_p, toff_p + bmax) must be disjoint
 // (KParams::ifok): both chains then update w_p in place, and t_p = M^{-1} w_p needs no correction.
 template <int SL>
-__device__ __forceinline__ void iface_solve(const TwoSidedQ<SL>& R, const KParams& p, const double* Fc,
-                                            const double* Gc, const int tv, double* rb, double* xt,
-                                            double* sink, long long* pacc) {
+__device__ __forceinline__ void iface_solve(const TwoSidedQ<SL>& R, const KParams& p, const double* __restrict__ Fc,
+                                            const double* __restrict__ Gc, const int tv, double* __restrict__ rb,
+                                            double* __restrict__ xt, double* __restrict__ tt,
+                                            double* __restrict__ xu, long long* pacc) {
+    // rb: the rhs, updated in place by the forward chains; tt: t_k = Inv_k w_k (T); xu: the
+    // backward chains' U / W rows; xt: x~ (X writes every row).  Four distinct LDS arrays, so
+    // each phase's loads issue ahead of its stores.
 #ifdef MPCQP_PHASE_PROF
     long long t0s = clock64();
 #define SPH(k) if (pacc && threadIdx.x == 0) { const long long t_ = clock64(); pacc[k] += t_ - t0s; t0s = t_; }
@@ -792,8 +796,8 @@ __device__ __forceinline__ void iface_solve(const TwoSidedQ<SL>& R, const KParam
     __syncthreads();
     SPH(12)
     // ---- T: t_k = Inv_k w_k, every block of the half at once (quad layout; a slot past the
-    // half's blocks reads block 0 and stores to the sink) ----
-    const int u = tid & 255, sub = u >> 7, i = (u & 127) >> 2, qq = u & 3;
+    // half's blocks reads block 0 and stores to the spare row of tt) ----
+    const int u = tid & 255, sub = __builtin_amdgcn_readfirstlane(u >> 7), i = (u & 127) >> 2, qq = u & 3;
 #pragma unroll
     for (int rr = 0; rr < TwoSidedQ<SL>::NR; ++rr) {
         const int s = 2 * rr + sub;
@@ -807,11 +811,12 @@ __device__ __forceinline__ void iface_solve(const TwoSidedQ<SL>& R, const KParam
             a0 = __builtin_fma(R.Inv[rr][c], v2.x, a0);
             a1 = __builtin_fma(R.Inv[rr][c + 1], v2.y, a1);
         }
-        *(have ? xt + k * S + i : sink + i) = reduce4(a0 + a1);
+        const double t = reduce4(a0 + a1);
+        if (have) tt[k * S + i] = t;
     }
     __syncthreads();
     SPH(13)
-    // ---- B: the backward chains on the U (top) / W (bottom) rows ----
+    // ---- B: the backward chains on the U (top) / W (bottom) rows, into xu (block p: t_p) ----
     if (w == 0) {
         const int ir = r < amax ? r : 0;
         const int j0 = min(4 * q, amax - 1), j1 = min(4 * q + 1, amax - 1), j2 = min(4 * q + 2, amax - 1),
@@ -820,15 +825,13 @@ __device__ __forceinline__ void iface_solve(const TwoSidedQ<SL>& R, const KParam
                      m2 = 4 * q + 2 < amax ? 1.0 : 0.0, m3 = 4 * q + 3 < amax ? 1.0 : 0.0;
 #pragma unroll 1
         for (int k = pm - 1; k >= 1; --k) {
-            // x_k[r] -= sum_{j < amax} F_{k+1}[j][r] x_{k+1}[j], lane q: j = 4 q + c
+            // x_k[r] = t_k[r] - sum_{j < amax} F_{k+1}[j][r] x_{k+1}[j], lane q: j = 4 q + c
             const double* f = Fc + k * amax * FGS + ir;
-            const double* xv = A16(xt + (k + 1) * S + 4 * q);
-            double* dst = xt + k * S + ir;
-            const double old = *dst;
-            const double2 x01 = *(const double2*)xv, x23 = *(const double2*)(xv + 2);
+            const double* xv = (k + 1 == pm ? tt : xu) + (k + 1) * S;
+            const double tk = tt[k * S + ir];
             const double f0 = m0 * f[j0 * FGS], f1 = m1 * f[j1 * FGS], f2 = m2 * f[j2 * FGS], f3 = m3 * f[j3 * FGS];
-            const double a0 = __builtin_fma(f2, x23.x, f0 * x01.x), a1 = __builtin_fma(f3, x23.y, f1 * x01.y);
-            *dst = old - reduce4(a0 + a1);
+            const double a0 = __builtin_fma(f2, xv[j2], f0 * xv[j0]), a1 = __builtin_fma(f3, xv[j3], f1 * xv[j1]);
+            xu[k * S + ir] = tk - reduce4(a0 + a1);
             chain_sync();
         }
     } else if (w == 4) {
@@ -839,51 +842,56 @@ __device__ __forceinline__ void iface_solve(const TwoSidedQ<SL>& R, const KParam
                      m2 = 4 * q + 2 < bmax ? 1.0 : 0.0, m3 = 4 * q + 3 < bmax ? 1.0 : 0.0;
 #pragma unroll 1
         for (int k = pm + 1; k <= nb - 2; ++k) {
-            // x_k[toff_k + a] -= sum_{a' < bmax} G_{k-1}[a'][toff_k + a] x_{k-1}[toff_{k-1} + a']
+            // x_k[toff_k + a] = t_k[..] - sum_{a' < bmax} G_{k-1}[a'][toff_k + a] x_{k-1}[toff_{k-1} + a']
             const int tk = toff_of(tv, k), tk1 = toff_of(tv, k - 1);
             const double* g = Gc + (k - 1 - pm) * bmax * FGS + tk + ia;
-            const double* xv = xt + (k - 1) * S + tk1;
-            double* dst = xt + k * S + tk + ia;
-            const double old = *dst;
+            const double* xv = (k - 1 == pm ? tt : xu) + (k - 1) * S + tk1;
+            const double t0 = tt[k * S + tk + ia];
             const double g0 = m0 * g[j0 * FGS], g1 = m1 * g[j1 * FGS], g2 = m2 * g[j2 * FGS], g3 = m3 * g[j3 * FGS];
             const double a0 = __builtin_fma(g2, xv[j2], g0 * xv[j0]), a1 = __builtin_fma(g3, xv[j3], g1 * xv[j1]);
-            *dst = old - reduce4(a0 + a1);
+            xu[k * S + tk + ia] = t0 - reduce4(a0 + a1);
             chain_sync();
         }
     }
     __syncthreads();
-    // ---- X: every row the chains did not carry (rows the chains carried store to the sink) ----
+    SPH(8)
+    // ---- X: every row of x~ -- the chains' rows from xu, block p from tt, the rest
+    //   top:    x_k = t_k - H_k x_{k+1}[U]       (H_k = F_{k+1}'),   k = 0 .. p-1
+    //   bottom: x_k = t_k - G_{k-1}' x_{k-1}[W], k = p+1 .. nb-1;  the middle block p = t_p ----
     {
         const int lim = half ? bmax : amax;
         const int j0 = min(4 * qq, lim - 1), j1 = min(4 * qq + 1, lim - 1), j2 = min(4 * qq + 2, lim - 1),
                   j3 = min(4 * qq + 3, lim - 1);
         const double m0 = 4 * qq < lim ? 1.0 : 0.0, m1 = 4 * qq + 1 < lim ? 1.0 : 0.0,
                      m2 = 4 * qq + 2 < lim ? 1.0 : 0.0, m3 = 4 * qq + 3 < lim ? 1.0 : 0.0;
+        // the top half takes blocks 0 .. p (block p: a copy of t_p), the bottom half p+1 .. nb-1
+        const int nmine = half ? nbot : pm + 1;
 #pragma unroll
         for (int rr = 0; rr < TwoSidedQ<SL>::NR; ++rr) {
             const int s = 2 * rr + sub;
-            // top: blocks 0 .. p-1 (H_k = F_{k+1}'), bottom: p+1 .. nb-1 (G_{k-1}')
-            const bool have = half == 0 ? s < pm : s < nbot;
-            const int k = have ? (half == 0 ? s : pm + 1 + s) : (half == 0 ? 0 : pm + 1);
-            bool done;         // row i of block k was carried by the backward chain
-            const double* hv;  // H_k[i][j] = F_{k+1}[j][i] (top) / G_{k-1}[j][i] (bottom), j = 4 qq + c
-            const double* xv;  // x_{k+1}[j] (top) / x_{k-1}[toff_{k-1} + j] (bottom)
-            if (half == 0) {
-                done = k >= 1 && i < amax;
-                hv = Fc + k * amax * FGS + i;
-                xv = xt + (k + 1) * S;
-            } else {
-                const int tk = toff_of(tv, k);
-                done = k <= nb - 2 && i >= tk && i < tk + bmax;
-                hv = Gc + (k - 1 - pm) * bmax * FGS + i;
-                xv = xt + (k - 1) * S + toff_of(tv, k - 1);
+            if (s < nmine) {
+                const int k = half == 0 ? s : pm + 1 + s;
+                const bool mid = half == 0 && k == pm;
+                bool done;         // row i of block k was carried by the backward chain
+                const double* hv;  // H_k[i][j] (top) / G_{k-1}[j][i] (bottom), j = 4 qq + c
+                const double* xv;  // x_{k+1}[j] (top) / x_{k-1}[toff_{k-1} + j] (bottom)
+                if (half == 0) {
+                    done = k >= 1 && i < amax;
+                    hv = Fc + (mid ? 0 : k * amax) * FGS + i;
+                    xv = (k + 1 == pm ? tt : xu) + (mid ? 0 : (k + 1) * S);
+                } else {
+                    const int tk = toff_of(tv, k);
+                    done = k <= nb - 2 && i >= tk && i < tk + bmax;
+                    hv = Gc + (k - 1 - pm) * bmax * FGS + i;
+                    xv = (k - 1 == pm ? tt : xu) + (k - 1) * S + toff_of(tv, k - 1);
+                }
+                const double tk = tt[k * S + i], xc = xu[k * S + i];
+                const double h0 = m0 * hv[j0 * FGS], h1 = m1 * hv[j1 * FGS], h2 = m2 * hv[j2 * FGS],
+                             h3 = m3 * hv[j3 * FGS];
+                const double a0 = __builtin_fma(h2, xv[j2], h0 * xv[j0]), a1 = __builtin_fma(h3, xv[j3], h1 * xv[j1]);
+                const double acc = reduce4(a0 + a1);
+                xt[k * S + i] = mid ? tk : (done ? xc : tk - acc);
             }
-            const double h0 = m0 * hv[j0 * FGS], h1 = m1 * hv[j1 * FGS], h2 = m2 * hv[j2 * FGS], h3 = m3 * hv[j3 * FGS];
-            const double a0 = __builtin_fma(h2, xv[j2], h0 * xv[j0]), a1 = __builtin_fma(h3, xv[j3], h1 * xv[j1]);
-            double* dst = xt + k * S + i;
-            const double acc = reduce4(a0 + a1);
-            const double old = *dst;
-            *((have && !done) ? dst : sink + i) = old - acc;
         }
     }
     __syncthreads();
@@ -1216,7 +1224,7 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
 #else
             long long* pacc = nullptr;
 #endif
-            if constexpr (IF) iface_solve<NS + 1>(RF, p, Fc, Gc, tvl, L.rb, L.xt, L.tv, pacc);
+            if constexpr (IF) iface_solve<NS + 1>(RF, p, Fc, Gc, tvl, L.rb, L.xt, L.tv, L.cor, pacc);
             else if constexpr (TTK == 512) twisted_solve<NS + 1>(RF, p, Fc, Gc, toffL, so, fo, L.rb, L.xt, L.tv, pacc);
             else wave_twisted_solve<NS>(RF, p, Fc, Gc, toffL, L.rb, L.xt, L.cor, pacc);
             PH(2)
