@@ -207,7 +207,7 @@ print(json.dumps(dict(nb=int(nb), bsize=[int(v) for v in bsize], span=span, amax
 def test_cfg2_workspace_carries_no_dense_inverse_rows():
     """The production library carves no dense-inverse rows (KParams::Kd, 256 x 54 doubles per
     instance) for cfg 2's four-block plan: that form is compiled into the experimental build
-    only.  Pinned: 120,760 bytes per instance (231,352 with the rows), with and
+    only.  About 121 kB per instance (231 kB with the rows' 110,592 B), with and
     without MPCQP_DENSE_W4=1 (read once per process: children)."""
     code = r"""
 import json
@@ -221,7 +221,8 @@ print(json.dumps(osqp_amd.plan_preview(P, A, **b["settings"])["bytes_per_instanc
     for dk in ("0", "1"):
         env = dict(os.environ, MPCQP_DENSE_W4=dk, MPCQP_BUILD="", PYTHONPATH=os.path.join(ROOT, "python-mpc_amd"))
         out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
-        assert json.loads(out.stdout.strip().splitlines()[-1]) == 120760
+        bpi = json.loads(out.stdout.strip().splitlines()[-1])
+        assert 115_000 < bpi < 125_000, bpi
 
 
 def test_plan_preview_reports_a_rejected_elimination():
