@@ -317,7 +317,7 @@ size_t workspace_bytes(const Plan& pl, long B, bool with_io) {
     carve<double>(off, B * m); carve<double>(off, B * n);              // certificates
     for (int i = 0; i < 4; ++i) carve<double>(off, B);
     carve<signed char>(off, B * m);
-    for (int i = 0; i < 6; ++i) carve<int>(off, B);
+    for (int i = 0; i < 7; ++i) carve<int>(off, B);
     carve<int>(off, 1);  // done (fused order epilogue)
     carve<long long>(off, B * kProfSlots);
     carve<KParams>(off, 1);
@@ -377,6 +377,8 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
     k.rho_upd = (int*)(base + carve<int>(off, B));
     k.pstat = (int*)(base + carve<int>(off, B));
     k.err = (int*)(base + carve<int>(off, B));
+    k.ffresh = (int*)(base + carve<int>(off, B));  // zero from the memset above
+    k.reuse = !(getenv("MPCQP_FACTOR_REUSE") && getenv("MPCQP_FACTOR_REUSE")[0] == '0');
     {  // dispatch order (kernels.hip::k_order), identity until the first solve
         int* ord = (int*)(base + carve<int>(off, B));
         HIPCHK(launch_iota(ord, B, s.stream));
@@ -1130,6 +1132,7 @@ int mpcqp_update_settings(mpcqp_handle* h, const mpcqp_settings* s, int32_t set_
         if (int e = stream_enter(sh, sh.stream)) return e;
         HIPCHK(hipMemcpyAsync((void*)k.self, &k, sizeof(KParams), hipMemcpyHostToDevice, sh.stream));
         if (rho_changed) {  // every instance's current rho (scal[2]); the solve refactors with it
+            HIPCHK(hipMemsetAsync(k.ffresh, 0, sizeof(int) * sh.B, sh.stream));
             std::vector<double> r(sh.B, rho);
             HIPCHK(hipMemcpy2DAsync(k.scal + 2, 4 * sizeof(double), r.data(), sizeof(double), sizeof(double), sh.B,
                                     hipMemcpyHostToDevice, sh.stream));

@@ -54,6 +54,12 @@ struct KParams {
     double *obj, *pri, *dua, *rho_est;
     signed char* ct;
     int *status, *iter, *rho_upd, *err;
+    // per instance: 1 while the workspace factor (F / H / Si: the long-horizon kernel, mode 3)
+    // is the one of the current data, rho and row classes, so that k_solve_b's next solve starts
+    // without refactoring (a setup's convexity check, a previous solve).  Cleared by every setup,
+    // by an update that moves a row's class, by a rho set through update_settings and by polish
+    int* ffresh;
+    int reuse;  // k_solve_b may start from a fresh workspace factor (MPCQP_FACTOR_REUSE=0: never, A/B)
     int *ostat, *oiter;  // per-call copies of status / iter (mpcqp_solve_device's outputs), or null
     const struct KParams* self;  // device copy of this block (read by the out-of-line device functions)
     long long* prof;  // optional per-instance phase timers (MPCQP_PHASE_PROF=1), kProfSlots each

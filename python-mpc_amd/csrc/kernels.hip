@@ -164,6 +164,7 @@ __global__ __launch_bounds__(T) void k_setup(KParams p, const double* __restrict
         p.scal[b * 4 + 1] = 1.0 / c;
         p.status[b] = MPCQP_UNSOLVED_;
         p.err[b] = bad ? 1 : 0;
+        p.ffresh[b] = 0;
         if (!KEEP) {
             p.scal[b * 4 + 2] = rho;
             p.iter[b] = 0;
@@ -277,6 +278,7 @@ __global__ __launch_bounds__(T) void k_update(KParams p, const double* __restric
     const long b = blockIdx.x;
     const int n = p.n, m = p.m, npad = p.npad;
     const double c = p.scal[b * 4 + 0];
+    bool moved = false;  // a row changed class: the workspace factor (ffresh) no longer fits
     if (q_in)
         for (int pc = tid; pc < npad; pc += T) {
             int j = p.pad_var[pc];
@@ -310,13 +312,16 @@ __global__ __launch_bounds__(T) void k_update(KParams p, const double* __restric
             if (li < -OSQP_INFTY * MIN_SCALING && ui > OSQP_INFTY * MIN_SCALING) t = -1;
             else if (ui - li < RHO_TOL) t = 1;
             else t = 0;
+            moved = moved || p.ct[b * m + i] != t;
             p.ct[b * m + i] = t;
         }
     }
     bad = block_any<T>(bad, flag);
+    moved = block_any<T>(moved, flag);
     if (tid == 0) {
         p.status[b] = MPCQP_UNSOLVED_;
         if (l_in || u_in) p.err[b] = bad ? 1 : 0;
+        if (moved) p.ffresh[b] = 0;
     }
 }
 

@@ -201,6 +201,7 @@ __device__ __forceinline__ void setup_r_body(const KParams& p, const long b, con
         p.scal[b * 4 + 1] = 1.0 / c;
         p.status[b] = MPCQP_UNSOLVED_;
         p.err[b] = bad ? 1 : 0;
+        p.ffresh[b] = 0;
         if (!KEEP) {
             p.scal[b * 4 + 2] = rho;
             p.iter[b] = 0;

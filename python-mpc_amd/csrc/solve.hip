@@ -566,6 +566,7 @@ __global__ __launch_bounds__(T) void k_polish(KParams p, double* __restrict__ xo
         L.ct[i] = (signed char)((z - lo < -y ? 1 : 0) | (up - z < y ? 2 : 0));
     }
     for (int pc = tid; pc < npad; pc += T) L.qv[pc] = p.q[b * npad + pc];
+    if (tid == 0) p.ffresh[b] = 0;  // the polish system's factor takes the workspace tiles
     __syncthreads();
     const bool ok = factorize_pol_nl<T>(p.self, b);
     if (!ok) {  // the reduced KKT matrix is not quasi-definite: polish fails

@@ -1136,7 +1136,12 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
     for (int e = tid; e < 2 * npad; e += TTK) L.cor[e] = 0.0;  // corT | corB of the sweep (cor, tv)
 
     int status = MPCQP_UNSOLVED_, rho_updates = 0, iter = 0, info_iter = 0;
-    bool can_check = false, need_factor = true;
+    // the workspace factor is the current one (KParams::ffresh: this instance's convexity check
+    // at setup, or its previous solve, factored K at this rho and these row classes): start
+    // without refactoring -- the single-QP path's setup() + solve() factored twice before
+    const bool fresh = p.reuse && p.ffresh[b] == 1;
+    if (fresh && factor_only) return;
+    bool can_check = false, need_factor = !fresh;
     // y in registers for the whole solve (ys is its LDS copy for the out-of-line phases)
     double y[RS];
 #pragma unroll
@@ -1151,6 +1156,7 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
             need_factor = false;
             const bool ok = factorize2_nl<TTK>(p.self, b, rho, Fc);  // scratch tiles in the F/G region
             if (!ok) {
+                if (tid == 0) p.ffresh[b] = 0;
                 if (iter == 0) {
                     for (int j = tid; j < n; j += TTK) if (xo) xo[b * n + j] = __builtin_nan("");
                     for (int i = tid; i < m; i += TTK) if (yo) yo[b * m + i] = __builtin_nan("");
@@ -1161,7 +1167,10 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
                 can_check = true;  // skip the final check_termination
                 break;
             }
-            if (factor_only) return;
+            if (factor_only) {
+                if (tid == 0) p.ffresh[b] = 1;
+                return;
+            }
             PH(0)
         }
         // ---- run state (re-derived at every run start; nothing but scalars lives across calls) ----
@@ -1304,6 +1313,9 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
         if (status == MPCQP_UNSOLVED_) status = MPCQP_MAX_ITER_REACHED_;
     }
     finalize_nl<TTK>(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates, p.ostat, p.oiter);
+    // the workspace now holds the factor of the final rho (the next solve's): fresh unless the
+    // last factorisation failed
+    if (tid == 0) p.ffresh[b] = status == MPCQP_NON_CVX_ ? 0 : 1;
 #ifdef MPCQP_PHASE_PROF
     if (prof) {
         __syncthreads();

@@ -1240,3 +1240,58 @@ def test_shim_update_settings_polish_demo():
     assert rg.info.iter == ro.info.iter and rg.info.status_polish == ro.info.status_polish == 1
     assert np.abs(rg.x - np.array([0.3, 0.7])).max() < 1e-9
     assert np.abs(rg.x - ro.x).max() < 1e-12
+
+
+def test_long_horizon_factor_reuse_is_exact(monkeypatch):
+    """The long-horizon kernel starts a solve from the workspace factor when it is the current
+    one (KParams::ffresh: set by setup()'s convexity check and by every solve, cleared by a
+    setup, by an update that moves a row between the equality / inequality / loose classes, by
+    a rho from update_settings and by polish).  A cfg-5 handle that reuses it and one that
+    refactors at every solve (MPCQP_FACTOR_REUSE=0) go through the same calls -- solve, update
+    of q, update of l / u that turns rows into equalities (classes move), update_settings(rho),
+    update of q again -- and agree bit for bit; both against the oracle doing the same."""
+    b = mpc.make_batch(5, B=6, seed=17)
+    s = dict(warm_start=True, polish=False)
+    P, A = b["P"], b["A"]
+    handles = []
+    for reuse in ("1", "0"):
+        monkeypatch.setenv("MPCQP_FACTOR_REUSE", reuse)
+        h = OSQPBatch()
+        h.setup(P, b["q"], A, b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
+        handles.append(h)
+    monkeypatch.delenv("MPCQP_FACTOR_REUSE")
+    orc = []
+    for k in range(b["Px"].shape[0]):
+        o = pyoracle.OSQP()
+        Pk, Ak = P.copy(), A.copy()
+        Pk.data, Ak.data = b["Px"][k].copy(), b["Ax"][k].copy()
+        o.setup(Pk, b["q"][k], Ak, b["l"][k], b["u"][k], **s)
+        orc.append(o)
+    q2 = b["q"] * 1.01
+    l3, u3 = b["l"].copy(), b["u"].copy()
+    fin = np.isfinite(l3[0]) & np.isfinite(u3[0]) & (u3[0] - l3[0] > 1e-3)
+    rows = np.flatnonzero(fin)[-6:]  # inequality rows made equalities: their class moves
+    mid = 0.5 * (l3[:, rows] + u3[:, rows])
+    l3[:, rows] = mid
+    u3[:, rows] = mid
+    calls = [dict(), dict(q=q2), dict(l=l3, u=u3), dict(rho=0.3), dict(q=b["q"])]
+    for step, kw in enumerate(calls):
+        for h in handles:
+            if "rho" in kw:
+                h.update_settings(**kw)
+            elif kw:
+                h.update(**kw)
+        for k, o in enumerate(orc):
+            if "rho" in kw:
+                o.update_settings(**kw)
+            elif kw:
+                o.update(**{n: v[k] for n, v in kw.items()})
+        r1, r0 = handles[0].solve(), handles[1].solve()
+        assert np.array_equal(r1.iter, r0.iter) and np.array_equal(r1.status_val, r0.status_val), step
+        assert np.array_equal(r1.x, r0.x) and np.array_equal(r1.y, r0.y), step
+        ro = [o.solve() for o in orc]
+        it = np.array([r.info.iter for r in ro])
+        assert np.mean(r1.iter == it) >= 5 / 6, (step, r1.iter, it)
+        same = r1.iter == it
+        du = np.array([np.abs(r1.x[k, b["u_block"]] - ro[k].x[b["u_block"]]).max() for k in range(len(ro))])
+        assert np.all(du[same] < U_TOL), (step, du[same].max())
