@@ -345,3 +345,36 @@ def test_rotated_tile_row_network_round_trips():
         assert out == row
     for s in range(8):
         assert len({s ^ (i & 7) for i in range(8)}) == 8
+
+
+def test_canonical_data_matches_scipy():
+    """osqp_amd.canonical_data takes P's upper triangle from the CSC arrays directly and
+    _drop_common_zeros drops the all-zero entries the same way: the same pattern, values and
+    order as scipy.sparse.triu / eliminate_zeros (osqp-python's prepare_data), on random
+    symmetric patterns with unsorted indices and explicit zeros."""
+    from scipy import sparse
+    rng = np.random.default_rng(0)
+    for t in range(40):
+        n, m = int(rng.integers(1, 40)), int(rng.integers(1, 40))
+        M = sparse.random(n, n, density=0.3, random_state=int(rng.integers(1 << 30)), format="coo")
+        M = (M + M.T).tocsc()
+        if t % 3 == 0:
+            M = sparse.csc_matrix((M.data[::-1].copy(), M.indices, M.indptr), shape=M.shape)
+            M.has_sorted_indices = False
+        A = sparse.random(m, n, density=0.2, random_state=int(rng.integers(1 << 30)), format="csc")
+        P1, A1 = osqp_amd.canonical_data(M, A)
+        P0 = sparse.triu(sparse.csc_matrix(M), format="csc")
+        P0.sort_indices()
+        assert np.array_equal(P1.indptr, P0.indptr) and np.array_equal(P1.indices, P0.indices)
+        assert np.array_equal(P1.data, P0.data)
+        V = rng.normal(size=(3, P1.nnz))
+        V[:, ::4] = 0.0
+        Mk, Vk = osqp_amd._drop_common_zeros(P1, V)
+        keep = np.any(V != 0, axis=0)
+        M0 = P1.copy()
+        M0.data = keep.astype(float)
+        M0.eliminate_zeros()
+        M0.sort_indices()
+        assert np.array_equal(Mk.indptr, M0.indptr) and np.array_equal(Mk.indices, M0.indices)
+        assert np.array_equal(Vk, V[:, keep])
+        assert np.array_equal(osqp_amd._kept_index(V)[keep], np.arange(int(keep.sum())))
