@@ -755,42 +755,46 @@ __device__ __forceinline__ void iface_solve(const TwoSidedQ<SL>& R, const KParam
     const int r = lane >> 2, q = lane & 3;  // chain lanes: row r, columns [8 q, 8 q + 8)
     // ---- F: the forward chains (wave 0 top, wave 4 bottom).  Lanes past the chain's rows take
     // row 0 and store row 0's value again (the same sum): no lane mask in the chain ----
-    if (w == 0) {
-        const int ir = r < amax ? r : 0;
-#pragma unroll 1
-        for (int s = 1; s <= pm; ++s) {
-            const double* f = A16(Fc + ((s - 1) * amax + ir) * FGS + 8 * q);
-            const double* v = A16(rb + (s - 1) * S + 8 * q);
-            double* dst = rb + s * S + ir;
+    // Each step's F / G row (static) is loaded one step ahead, after the step's dynamic reads, so
+    // the step waits only for the rows the previous step wrote (LDS returns in order); two steps
+    // per loop pass with two row buffers (a copy between them made the compiler wait for the
+    // prefetch before the step's sum).
+    if (w == 0 || w == 4) {
+        const bool top = w == 0;
+        const int lim = top ? amax : bmax, ir = r < lim ? r : 0, nst = top ? pm : nbot;
+        // step s (1-based): the row block and its source / destination
+        auto rowp = [&](int s) __attribute__((always_inline)) {
+            return A16((top ? Fc + ((s - 1) * amax + ir) * FGS : Gc + ((nb - 1 - s - pm) * bmax + ir) * FGS) + 8 * q);
+        };
+        auto load = [&](int s, double2 (&f)[4]) __attribute__((always_inline)) {
+            const double* fp = rowp(s);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) f[c] = *(const double2*)(fp + 2 * c);
+        };
+        auto step = [&](int s, const double2 (&fc)[4], double2 (&fn)[4]) __attribute__((always_inline)) {
+            const int src = top ? s - 1 : nb - s, dsb = top ? s : nb - 1 - s;
+            const double* v = A16(rb + src * S + 8 * q);
+            double* dst = rb + dsb * S + (top ? 0 : toff_of(tv, dsb)) + ir;
+            double2 v2[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v2[c] = *(const double2*)(v + 2 * c);
             const double old = *dst;
+            load(s < nst ? s + 1 : s, fn);
             double a0 = 0.0, a1 = 0.0;
 #pragma unroll
-            for (int c = 0; c < 8; c += 2) {
-                const double2 f2 = *(const double2*)(f + c), v2 = *(const double2*)(v + c);
-                a0 = __builtin_fma(f2.x, v2.x, a0);
-                a1 = __builtin_fma(f2.y, v2.y, a1);
+            for (int c = 0; c < 4; ++c) {
+                a0 = __builtin_fma(fc[c].x, v2[c].x, a0);
+                a1 = __builtin_fma(fc[c].y, v2[c].y, a1);
             }
             *dst = old - reduce4(a0 + a1);
             chain_sync();
-        }
-    } else if (w == 4) {
-        const int ia = r < bmax ? r : 0;
+        };
+        double2 fa[4], fb[4];
+        load(1, fa);
 #pragma unroll 1
-        for (int s = 1; s <= nbot; ++s) {
-            const int kd = nb - 1 - s;
-            const double* g = A16(Gc + ((kd - pm) * bmax + ia) * FGS + 8 * q);
-            const double* v = A16(rb + (kd + 1) * S + 8 * q);
-            double* dst = rb + kd * S + toff_of(tv, kd) + ia;
-            const double old = *dst;
-            double a0 = 0.0, a1 = 0.0;
-#pragma unroll
-            for (int c = 0; c < 8; c += 2) {
-                const double2 g2 = *(const double2*)(g + c), v2 = *(const double2*)(v + c);
-                a0 = __builtin_fma(g2.x, v2.x, a0);
-                a1 = __builtin_fma(g2.y, v2.y, a1);
-            }
-            *dst = old - reduce4(a0 + a1);
-            chain_sync();
+        for (int s = 1; s <= nst; s += 2) {
+            step(s, fa, fb);
+            if (s + 1 <= nst) step(s + 1, fb, fa);
         }
     }
     __syncthreads();
