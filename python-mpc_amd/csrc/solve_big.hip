@@ -820,41 +820,49 @@ __device__ __forceinline__ void iface_solve(const TwoSidedQ<SL>& R, const KParam
     }
     __syncthreads();
     SPH(13)
-    // ---- B: the backward chains on the U (top) / W (bottom) rows, into xu (block p: t_p) ----
-    if (w == 0) {
-        const int ir = r < amax ? r : 0;
-        const int j0 = min(4 * q, amax - 1), j1 = min(4 * q + 1, amax - 1), j2 = min(4 * q + 2, amax - 1),
-                  j3 = min(4 * q + 3, amax - 1);
-        const double m0 = 4 * q < amax ? 1.0 : 0.0, m1 = 4 * q + 1 < amax ? 1.0 : 0.0,
-                     m2 = 4 * q + 2 < amax ? 1.0 : 0.0, m3 = 4 * q + 3 < amax ? 1.0 : 0.0;
-#pragma unroll 1
-        for (int k = pm - 1; k >= 1; --k) {
-            // x_k[r] = t_k[r] - sum_{j < amax} F_{k+1}[j][r] x_{k+1}[j], lane q: j = 4 q + c
-            const double* f = Fc + k * amax * FGS + ir;
-            const double* xv = (k + 1 == pm ? tt : xu) + (k + 1) * S;
-            const double tk = tt[k * S + ir];
-            const double f0 = m0 * f[j0 * FGS], f1 = m1 * f[j1 * FGS], f2 = m2 * f[j2 * FGS], f3 = m3 * f[j3 * FGS];
-            const double a0 = __builtin_fma(f2, xv[j2], f0 * xv[j0]), a1 = __builtin_fma(f3, xv[j3], f1 * xv[j1]);
-            xu[k * S + ir] = tk - reduce4(a0 + a1);
+    // ---- B: the backward chains on the U (top) / W (bottom) rows, into xu (block p: t_p).  The
+    // step's H column (four strided reads) and t value are static: loaded one step ahead, two
+    // steps per loop pass with two buffers (as the forward chains) ----
+    if (w == 0 || w == 4) {
+        const bool top = w == 0;
+        const int lim = top ? amax : bmax, ir = r < lim ? r : 0;
+        const int j0 = min(4 * q, lim - 1), j1 = min(4 * q + 1, lim - 1), j2 = min(4 * q + 2, lim - 1),
+                  j3 = min(4 * q + 3, lim - 1);
+        const double m0 = 4 * q < lim ? 1.0 : 0.0, m1 = 4 * q + 1 < lim ? 1.0 : 0.0,
+                     m2 = 4 * q + 2 < lim ? 1.0 : 0.0, m3 = 4 * q + 3 < lim ? 1.0 : 0.0;
+        // step s = 1 .. nst: block k = p - s (top, x_k[U] from x_{k+1}[U]) or p + s (bottom,
+        // x_k[W_k] from x_{k-1}[W_{k-1}])
+        const int nst = top ? pm - 1 : nbot - 1;
+        struct Ops { double h0, h1, h2, h3, t; };
+        auto blk = [&](int s) __attribute__((always_inline)) { return top ? pm - s : pm + s; };
+        auto load = [&](int s, Ops& o) __attribute__((always_inline)) {
+            const int k = blk(s);
+            const int tk = top ? 0 : toff_of(tv, k);
+            // H_k[r][j]: F_{k+1}[j][r] (top) / G_{k-1}[j][toff_k + r] (bottom)
+            const double* h = top ? Fc + k * amax * FGS + ir : Gc + (k - 1 - pm) * bmax * FGS + tk + ir;
+            o.h0 = m0 * h[j0 * FGS];
+            o.h1 = m1 * h[j1 * FGS];
+            o.h2 = m2 * h[j2 * FGS];
+            o.h3 = m3 * h[j3 * FGS];
+            o.t = tt[k * S + tk + ir];
+        };
+        auto step = [&](int s, const Ops& oc, Ops& on) __attribute__((always_inline)) {
+            const int k = blk(s), kn = top ? k + 1 : k - 1;
+            const double* xv = (kn == pm ? tt : xu) + kn * S + (top ? 0 : toff_of(tv, kn));
+            const double x0 = xv[j0], x1 = xv[j1], x2 = xv[j2], x3 = xv[j3];
+            load(s < nst ? s + 1 : s, on);
+            const double a0 = __builtin_fma(oc.h2, x2, oc.h0 * x0), a1 = __builtin_fma(oc.h3, x3, oc.h1 * x1);
+            xu[k * S + (top ? 0 : toff_of(tv, k)) + ir] = oc.t - reduce4(a0 + a1);
             chain_sync();
-        }
-    } else if (w == 4) {
-        const int ia = r < bmax ? r : 0;
-        const int j0 = min(4 * q, bmax - 1), j1 = min(4 * q + 1, bmax - 1), j2 = min(4 * q + 2, bmax - 1),
-                  j3 = min(4 * q + 3, bmax - 1);
-        const double m0 = 4 * q < bmax ? 1.0 : 0.0, m1 = 4 * q + 1 < bmax ? 1.0 : 0.0,
-                     m2 = 4 * q + 2 < bmax ? 1.0 : 0.0, m3 = 4 * q + 3 < bmax ? 1.0 : 0.0;
+        };
+        if (nst >= 1) {
+            Ops oa, ob;
+            load(1, oa);
 #pragma unroll 1
-        for (int k = pm + 1; k <= nb - 2; ++k) {
-            // x_k[toff_k + a] = t_k[..] - sum_{a' < bmax} G_{k-1}[a'][toff_k + a] x_{k-1}[toff_{k-1} + a']
-            const int tk = toff_of(tv, k), tk1 = toff_of(tv, k - 1);
-            const double* g = Gc + (k - 1 - pm) * bmax * FGS + tk + ia;
-            const double* xv = (k - 1 == pm ? tt : xu) + (k - 1) * S + tk1;
-            const double t0 = tt[k * S + tk + ia];
-            const double g0 = m0 * g[j0 * FGS], g1 = m1 * g[j1 * FGS], g2 = m2 * g[j2 * FGS], g3 = m3 * g[j3 * FGS];
-            const double a0 = __builtin_fma(g2, xv[j2], g0 * xv[j0]), a1 = __builtin_fma(g3, xv[j3], g1 * xv[j1]);
-            xu[k * S + tk + ia] = t0 - reduce4(a0 + a1);
-            chain_sync();
+            for (int s = 1; s <= nst; s += 2) {
+                step(s, oa, ob);
+                if (s + 1 <= nst) step(s + 1, ob, oa);
+            }
         }
     }
     __syncthreads();
