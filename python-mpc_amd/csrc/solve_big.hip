@@ -687,9 +687,11 @@ template <int SL>
 struct TwoSidedQ {
     static constexpr int NR = (SL + 1) / 2;  // rounds: two blocks per round and half
     double Inv[NR][8];  // round r, this thread's block slot s = 2 r + sub: Inv_s[i][8 q + c]
+    // frows: also copy the F / G rows into LDS (after a factorisation, which uses that region as
+    // scratch; a termination check leaves it alone, so a run start after one need not)
     __device__ __forceinline__ void load(int nb, int pm, int amax, int bmax, const double* __restrict__ Fg,
                                          const double* __restrict__ Hg, const double* __restrict__ Sg,
-                                         double* __restrict__ Fc, double* __restrict__ Gc) {
+                                         double* __restrict__ Fc, double* __restrict__ Gc, bool frows = true) {
         const int tid = threadIdx.x, half = __builtin_amdgcn_readfirstlane(tid >> 8), u = tid & 255;
         const int sub = u >> 7, i = (u & 127) >> 2, q = u & 3;
         const int nbot = nb - 1 - pm;
@@ -706,6 +708,7 @@ struct TwoSidedQ {
                 Inv[r][c + 1] = t2.y;
             }
         }
+        if (!frows) return;
         for (int o = tid; o < pm * amax * S; o += TB) {  // row q = k amax + r of F_{k+1}
             const int qq = o >> 5, j = o & (S - 1), k = qq / amax, r = qq - k * amax;
             Fc[qq * FGS + j] = Fg[(long)(k + 1) * SS + r * S + j];
@@ -1154,6 +1157,7 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
     const bool fresh = p.reuse && p.ffresh[b] == 1;
     if (fresh && factor_only) return;
     bool can_check = false, need_factor = !fresh;
+    bool frows = true;  // the F / G rows must be (re)loaded into LDS at the next run start
     // y in registers for the whole solve (ys is its LDS copy for the out-of-line phases)
     double y[RS];
 #pragma unroll
@@ -1167,6 +1171,7 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
         if (need_factor) {  // start, and after a rho change
             need_factor = false;
             const bool ok = factorize2_nl<TTK>(p.self, b, rho, Fc);  // scratch tiles in the F/G region
+            frows = true;
             if (!ok) {
                 if (tid == 0) p.ffresh[b] = 0;
                 if (iter == 0) {
@@ -1187,7 +1192,12 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
         }
         // ---- run state (re-derived at every run start; nothing but scalars lives across calls) ----
         std::conditional_t<IF, TwoSidedQ<NS + 1>, std::conditional_t<TTK == 512, TwoSided<NS + 1>, TwoSidedW<NS>>> RF;
-        RF.load(nb, p.pmeet, amax, p.bmax, Fg, Hg, Sg, Fc, Gc);
+        if constexpr (IF) {
+            RF.load(nb, p.pmeet, amax, p.bmax, Fg, Hg, Sg, Fc, Gc, frows);
+            frows = false;
+        } else {
+            RF.load(nb, p.pmeet, amax, p.bmax, Fg, Hg, Sg, Fc, Gc);
+        }
         int so[NS + 1], fo[NS + 1];  // (TTK == 512, NS < 10: twisted_solve's step offsets)
         // the interface form: toff[lane] in one VGPR (iface_solve::toff_of)
         int tvl = 0;
