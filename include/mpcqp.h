@@ -222,11 +222,11 @@ int mpcqp_timing_read(mpcqp_handle *h, double *setup_ms, int32_t *n_setup, doubl
                       int32_t *n_solve);
 
 int mpcqp_get_plan_info(const mpcqp_handle *h, mpcqp_plan_info *info);
-/* Diagnostics: per-instance phase timers of the last solve (16 int64 per instance:
+/* Diagnostics: per-instance phase timers of the last solve (24 int64 per instance:
  * factor, rhs, bt_solve, update, checks, tail shader-clock cycles, total cycles,
  * total 100 MHz wall ticks, then the factorisation split: assembly, F/S products,
  * Gauss-Jordan, block epilogue, then the block-solve split of the wave kernels:
- * phase A, B, C, spare).  Only when MPCQP_PHASE_PROF=1 was set at creation. */
+ * phase A, B, C, spare, then eight per-wave sub-phase times of the long-horizon kernel).  Only when MPCQP_PHASE_PROF=1 was set at creation. */
 int mpcqp_debug_phase_times(mpcqp_handle *h, int64_t *out);
 /* Diagnostics: the dispatch order the next solve will use (B int32 instance indices, each
  * shard's own order offset by its first instance): after a solve, that solve's instances by

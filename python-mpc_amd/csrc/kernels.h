@@ -9,9 +9,11 @@ namespace mpcqp {
 constexpr int kThreads = 256;
 constexpr int kThreadsBig = 512;  // solve_big.hip (long horizons)
 constexpr int kDenseR = 104;      // solve_dense.hip: register row length of M^{-1} (variables per QP)
-constexpr int kProfSlots = 16;  // factor, rhs, bt_solve, update, checks, tail, total cycles, total 100 MHz ticks,
+constexpr int kProfSlots = 24;  // factor, rhs, bt_solve, update, checks, tail, total cycles, total 100 MHz ticks,
                                 // factor split: assembly, F/S products, Gauss-Jordan, block epilogue,
-                                // solve split (wave kernels): phase A, phase B, phase C, spare
+                                // solve split (wave kernels): phase A, phase B, phase C, spare,
+                                // 16-23: per-wave sub-phase times (solve_big.hip's interface form: the
+                                // chain waves' own forward / backward times, wave 0's T and X)
 
 // status values (OSQP constants.h)
 enum : int {

@@ -742,19 +742,28 @@ template <int SL>
 __device__ __forceinline__ void iface_solve(const TwoSidedQ<SL>& R, const KParams& p, const double* __restrict__ Fc,
                                             const double* __restrict__ Gc, const int tv, double* __restrict__ rb,
                                             double* __restrict__ xt, double* __restrict__ tt,
-                                            double* __restrict__ xu, long long* pacc) {
+                                            double* __restrict__ xu, long long* pacc, long long* pw) {
     // rb: the rhs, updated in place by the forward chains; tt: t_k = Inv_k w_k (T); xu: the
     // backward chains' U / W rows; xt: x~ (X writes every row).  Four distinct LDS arrays, so
     // each phase's loads issue ahead of its stores.
 #ifdef MPCQP_PHASE_PROF
     long long t0s = clock64();
 #define SPH(k) if (pacc && threadIdx.x == 0) { const long long t_ = clock64(); pacc[k] += t_ - t0s; t0s = t_; }
+    // a wave's own time in a sub-phase (lane 0 keeps it: pw[] in its registers)
+    long long tw = clock64();
+#define WPH(k) if (pw && (threadIdx.x & 63) == 0) { const long long t_ = clock64(); pw[k] += t_ - tw; tw = t_; }
+#define WRS() if (pw) tw = clock64();
 #else
 #define SPH(k)
+#define WPH(k)
+#define WRS()
 #endif
     const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int nb = p.nb, pm = p.pmeet, amax = p.amax, bmax = p.bmax, nbot = nb - 1 - pm;
     const int half = w >> 2;
+    // the chains: wave 0 the top one, wave 1 the bottom one (waves 0 and 1 sit on different
+    // SIMDs -- a workgroup's waves go round the SIMDs 0, 2, 1, 3 -- where waves 0 and 4 share one)
+    constexpr int WB = 1;
     const int r = lane >> 2, q = lane & 3;  // chain lanes: row r, columns [8 q, 8 q + 8)
     // ---- F: the forward chains (wave 0 top, wave 4 bottom).  Lanes past the chain's rows take
     // row 0 and store row 0's value again (the same sum): no lane mask in the chain ----
@@ -762,7 +771,7 @@ __device__ __forceinline__ void iface_solve(const TwoSidedQ<SL>& R, const KParam
     // the step waits only for the rows the previous step wrote (LDS returns in order); two steps
     // per loop pass with two row buffers (a copy between them made the compiler wait for the
     // prefetch before the step's sum).
-    if (w == 0 || w == 4) {
+    if (w == 0 || w == WB) {
         const bool top = w == 0;
         const int lim = top ? amax : bmax, ir = r < lim ? r : 0, nst = top ? pm : nbot;
         // step s (1-based): the row block and its source / destination
@@ -799,9 +808,11 @@ __device__ __forceinline__ void iface_solve(const TwoSidedQ<SL>& R, const KParam
             step(s, fa, fb);
             if (s + 1 <= nst) step(s + 1, fb, fa);
         }
+        WPH(0)
     }
     __syncthreads();
     SPH(12)
+    WRS()
     // ---- T: t_k = Inv_k w_k, every block of the half at once (quad layout; a slot past the
     // half's blocks reads block 0 and stores to the spare row of tt) ----
     const int u = tid & 255, sub = __builtin_amdgcn_readfirstlane(u >> 7), i = (u & 127) >> 2, qq = u & 3;
@@ -821,12 +832,14 @@ __device__ __forceinline__ void iface_solve(const TwoSidedQ<SL>& R, const KParam
         const double t = reduce4(a0 + a1);
         if (have) tt[k * S + i] = t;
     }
+    if (w == 0) WPH(4)
     __syncthreads();
     SPH(13)
+    WRS()
     // ---- B: the backward chains on the U (top) / W (bottom) rows, into xu (block p: t_p).  The
     // step's H column (four strided reads) and t value are static: loaded one step ahead, two
     // steps per loop pass with two buffers (as the forward chains) ----
-    if (w == 0 || w == 4) {
+    if (w == 0 || w == WB) {
         const bool top = w == 0;
         const int lim = top ? amax : bmax, ir = r < lim ? r : 0;
         const int j0 = min(4 * q, lim - 1), j1 = min(4 * q + 1, lim - 1), j2 = min(4 * q + 2, lim - 1),
@@ -867,9 +880,11 @@ __device__ __forceinline__ void iface_solve(const TwoSidedQ<SL>& R, const KParam
                 if (s + 1 <= nst) step(s + 1, ob, oa);
             }
         }
+        WPH(2)
     }
     __syncthreads();
     SPH(8)
+    WRS()
     // ---- X: every row of x~ -- the chains' rows from xu, block p from tt, the rest
     //   top:    x_k = t_k - H_k x_{k+1}[U]       (H_k = F_{k+1}'),   k = 0 .. p-1
     //   bottom: x_k = t_k - G_{k-1}' x_{k-1}[W], k = p+1 .. nb-1;  the middle block p = t_p ----
@@ -909,9 +924,12 @@ __device__ __forceinline__ void iface_solve(const TwoSidedQ<SL>& R, const KParam
             }
         }
     }
+    if (w == 0) WPH(5)
     __syncthreads();
     SPH(14)
 #undef SPH
+#undef WPH
+#undef WRS
 }
 
 // ---------------------------------------------------------------------------
@@ -1151,6 +1169,9 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
     for (int e = tid; e < 2 * npad; e += TTK) L.cor[e] = 0.0;  // corT | corB of the sweep (cor, tv)
 
     int status = MPCQP_UNSOLVED_, rho_updates = 0, iter = 0, info_iter = 0;
+#ifdef MPCQP_PHASE_PROF
+    long long pwr[6] = {0, 0, 0, 0, 0, 0};  // the interface form's per-wave sub-phase times (iface_solve)
+#endif
     // the workspace factor is the current one (KParams::ffresh: this instance's convexity check
     // at setup, or its previous solve, factored K at this rho and these row classes): start
     // without refactoring -- the single-QP path's setup() + solve() factored twice before
@@ -1255,7 +1276,12 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
 #else
             long long* pacc = nullptr;
 #endif
-            if constexpr (IF) iface_solve<NS + 1>(RF, p, Fc, Gc, tvl, L.rb, L.xt, L.tv, L.cor, pacc);
+#ifdef MPCQP_PHASE_PROF
+            long long* pwp = prof ? pwr : nullptr;
+#else
+            long long* pwp = nullptr;
+#endif
+            if constexpr (IF) iface_solve<NS + 1>(RF, p, Fc, Gc, tvl, L.rb, L.xt, L.tv, L.cor, pacc, pwp);
             else if constexpr (TTK == 512) twisted_solve<NS + 1>(RF, p, Fc, Gc, toffL, so, fo, L.rb, L.xt, L.tv, pacc);
             else wave_twisted_solve<NS>(RF, p, Fc, Gc, toffL, L.rb, L.xt, L.cor, pacc);
             PH(2)
@@ -1349,6 +1375,16 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
             for (int k = 8; k < 15; ++k) p.prof[b * kProfSlots + k] = L.pacc[k];
             p.prof[b * kProfSlots + 6] = clock64() - t0c;
             p.prof[b * kProfSlots + 7] = wall_clock64() - t0w;
+            if constexpr (IF) {  // wave 0: its chain, T and X; wave 1 (below): its chain
+                p.prof[b * kProfSlots + 16] = pwr[0];
+                p.prof[b * kProfSlots + 18] = pwr[2];
+                p.prof[b * kProfSlots + 20] = pwr[4];
+                p.prof[b * kProfSlots + 21] = pwr[5];
+            }
+        }
+        if (IF && tid == 64) {
+            p.prof[b * kProfSlots + 17] = pwr[0];
+            p.prof[b * kProfSlots + 19] = pwr[2];
         }
     }
 #endif

@@ -460,9 +460,9 @@ class OSQPBatch:
         return {f[0]: getattr(info, f[0]) for f in _PlanInfo._fields_}
 
     def phase_times(self):
-        """Per-instance phase timers of the last solve, shape (B, 16) int64 (diagnostic;
+        """Per-instance phase timers of the last solve, shape (B, 24) int64 (diagnostic;
         needs MPCQP_PHASE_PROF=1 in the environment before setup)."""
-        out = np.zeros((self.B, 16), dtype=np.int64)
+        out = np.zeros((self.B, 24), dtype=np.int64)
         _check(lib().mpcqp_debug_phase_times(self._need(), out.ctypes.data_as(_P(C.c_int64))), "phase_times")
         return out
 
@@ -632,9 +632,9 @@ class DeviceBatch:
         return {f[0]: getattr(info, f[0]) for f in _PlanInfo._fields_}
 
     def phase_times(self):
-        """Per-instance phase timers of the last solve, shape (B, 16) int64 (diagnostic;
+        """Per-instance phase timers of the last solve, shape (B, 24) int64 (diagnostic;
         needs MPCQP_PHASE_PROF=1 in the environment when the batch was created)."""
-        out = np.zeros((self.B, 16), dtype=np.int64)
+        out = np.zeros((self.B, 24), dtype=np.int64)
         _check(lib().mpcqp_debug_phase_times(self._h.ptr, out.ctypes.data_as(_P(C.c_int64))), "phase_times")
         return out
 

@@ -74,6 +74,9 @@ def main():
         if row[12:15].any():
             for k, nm in zip(range(12, 15), ["s.A", "s.B", "s.C"]):
                 print(f"     {nm:7s} {row[k]:12.0f} cyc  {row[k] / max(its, 1):8.0f} /iter")
+        if row.size > 16 and row[16:24].any():  # the long-horizon interface form's own per-wave times
+            for k, nm in zip(range(16, 22), ["fwd.top", "fwd.bot", "bwd.top", "bwd.bot", "T.w0", "X.w0"]):
+                print(f"     {nm:7s} {row[k]:12.0f} cyc  {row[k] / max(its, 1):8.0f} /iter (own)")
 
 
 if __name__ == "__main__":
