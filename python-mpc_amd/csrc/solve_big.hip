@@ -832,7 +832,7 @@ __device__ __forceinline__ void iface_solve(const TwoSidedQ<SL>& R, const KParam
         const double t = reduce4(a0 + a1);
         if (have) tt[k * S + i] = t;
     }
-    if (w == 0) WPH(4)
+    if (w == 0) { WPH(4) }
     __syncthreads();
     SPH(13)
     WRS()
@@ -924,7 +924,7 @@ __device__ __forceinline__ void iface_solve(const TwoSidedQ<SL>& R, const KParam
             }
         }
     }
-    if (w == 0) WPH(5)
+    if (w == 0) { WPH(5) }
     __syncthreads();
     SPH(14)
 #undef SPH
