@@ -660,7 +660,7 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
 }
 
 // ---------------------------------------------------------------------------
-// The interface form of the two-sided solve (round 5; the default for k_solve_b<512>).
+// The interface form of the two-sided solve (round 5; opt-in, MPCQP_BIG_FORM=iface).
 // twisted_solve runs every forward and backward step of both chains on all 512 threads, one
 // workgroup barrier a step: 2 max(p, nb-1-p) + 1 barriers, ~820 cycles a forward step on cfg
 // 5 (profiles/r4s2_phase_cfg5.txt, s.A).  But a step only carries a few rows forward: F_s
@@ -1396,10 +1396,12 @@ size_t lds_solve_bytes_big(const KParams& p) {
 }
 
 // the interface form (iface_solve) unless MPCQP_BIG_FORM=twisted (A/B against round 4's sweep)
+// The interface form is opt-in (MPCQP_BIG_FORM=iface, read once per process): exact, but slower
+// than the twisted sweep on cfg 5 (38.0 against 36.2 ms per launch)
 static bool big_iface() {
     static const bool on = [] {
         const char* e = getenv("MPCQP_BIG_FORM");
-        return !(e && !strcmp(e, "twisted"));
+        return e && !strcmp(e, "iface");
     }();
     return on;
 }

@@ -404,6 +404,27 @@ def test_dense_inverse_form(tmp_path):
         _batch_parity(mpc.make_batch(2, B=1024), s, rg=rg)
 
 
+def test_long_horizon_interface_form(tmp_path):
+    """The long-horizon kernel's interface form of the two-sided solve (solve_big.hip::iface_solve,
+    opt-in MPCQP_BIG_FORM=iface, read once per process: the amax / bmax-row recurrences run by one
+    wave per chain, everything else between four barriers) against the oracle on cfg 5, in a
+    child process; and the same batch through the default twisted sweep agrees with it."""
+    import build_cases
+    s = dict(polish=False, warm_start=False)
+    got = build_cases.in_build("", [("batch", "if", 5, 64, None, s)], tmp_path / "if.npz",
+                               extra_env={"MPCQP_BIG_FORM": "iface"})
+    assert int(got["if_variant"]) == 12
+    b = mpc.make_batch(5, B=64)
+    rg = SimpleNamespace(x=got["if_x"], iter=got["if_iter"], status_val=got["if_status_val"])
+    _batch_parity(b, s, rg=rg)
+    h = OSQPBatch()
+    h.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
+    r = h.solve()
+    same = r.iter == rg.iter
+    assert same.mean() >= 0.9 and np.array_equal(r.status_val, rg.status_val)
+    assert np.abs(r.x[same] - rg.x[same]).max() < 1e-6 * max(1.0, np.abs(r.x).max())
+
+
 @pytest.mark.parametrize("variant", [v for v, _, _ in EXPERIMENTAL])
 def test_production_library_refuses_experimental_variants(monkeypatch, variant):
     cfg = next(c for v, c, _ in EXPERIMENTAL if v == variant)
