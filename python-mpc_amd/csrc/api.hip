@@ -105,8 +105,9 @@ struct Shard {
     // info, the certificates, the statuses), filled by mpcqp_solve_batch with one
     // synchronisation; the info / certificate / polish getters then read it (mpcqp_handle::staged)
     char* hstage = nullptr;
+    char* dstage = nullptr;  // the device side of hstage (launch_gather)
     char* hin = nullptr;  // ... and of update()'s q, l, u and the error flags it reads back
-    size_t dws_bytes = 0, dplan_bytes = 0, hstage_bytes = 0, hin_bytes = 0;  // (resource pool keys)
+    size_t dws_bytes = 0, dplan_bytes = 0, hstage_bytes = 0, hin_bytes = 0, dstage_bytes = 0;  // (resource pool keys)
     unsigned long long dplan_tag = 0;  // Plan::uid of the device plan copy
     KParams kp{};
 };
@@ -114,7 +115,7 @@ struct Shard {
 }  // namespace
 
 struct mpcqp_handle {
-    Plan plan;
+    std::shared_ptr<const Plan> plan;  // shared with the plan cache (read-only)
     std::vector<int32_t> Pp, Pi, Ap, Ai;  // the user's pattern (a re-plan: replan_plain)
     mpcqp_settings set{};
     int n = 0, m = 0;
@@ -282,17 +283,24 @@ int upload_plan(const Plan& pl, Shard& s) {
         &pl.asm_blk_ptr, &pl.asm_tgt, &pl.tterm, &pl.acsr_pos, &pl.gcol, &pl.grow, &pl.gpsym, &pl.toff, &pl.bsize, &pl.tcnt,
         &pl.eown, &pl.etterm};
     std::vector<size_t> offs;
-    std::vector<int> flat;
+    size_t total = 0;
     for (auto* v : parts) {
-        offs.push_back(flat.size());
-        flat.insert(flat.end(), v->begin(), v->end());
-        flat.push_back(0);  // never allocate zero-length parts
+        offs.push_back(total);
+        total += v->size() + 1;  // never allocate zero-length parts
     }
-    s.dplan_bytes = flat.size() * sizeof(int);
+    s.dplan_bytes = total * sizeof(int);
     s.dplan_tag = pl.uid;
     bool have = false;  // a pooled copy of this very plan (a fresh handle of the same pattern)
     HIPCHK(pool_malloc(s.dev, s.dplan_bytes, (void**)&s.dplan, false, pl.uid, &have));
-    if (!have) HIPCHK(hipMemcpy(s.dplan, flat.data(), flat.size() * sizeof(int), hipMemcpyHostToDevice));
+    if (!have) {  // (the flat image is built only when it is uploaded)
+        std::vector<int> flat;
+        flat.reserve(total);
+        for (auto* v : parts) {
+            flat.insert(flat.end(), v->begin(), v->end());
+            flat.push_back(0);
+        }
+        HIPCHK(hipMemcpy(s.dplan, flat.data(), flat.size() * sizeof(int), hipMemcpyHostToDevice));
+    }
     const int** dst[] = {&s.kp.pad_var, &s.kp.acsc_ptr, &s.kp.acsc_row, &s.kp.acsc_v, &s.kp.acsr_ptr,
                          &s.kp.acsr_col, &s.kp.acsr_v, &s.kp.psym_ptr, &s.kp.psym_col, &s.kp.psym_v,
                          &s.kp.p_r, &s.kp.p_c, &s.kp.a_r, &s.kp.a_c, &s.kp.asm_blk_ptr, &s.kp.asm_tgt,
@@ -329,8 +337,11 @@ size_t workspace_bytes(const Plan& pl, long B, bool with_io) {
     return off + 256;
 }
 
-int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
-    const Plan& pl = h->plan;
+// sync: wait for the zeroing, the identity order and the parameter block before returning (the
+// device API's callers may use the workspace from any stream; the host batch setup queues all
+// its work on the shard's stream behind them and waits once, in check_setup)
+int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io, bool sync = true) {
+    const Plan& pl = *h->plan;
     HIPCHK(hipSetDevice(s.dev));
     if (int e = pool_stream(s)) return e;
     strace().mark("stream");
@@ -372,11 +383,11 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
     k.dua = (double*)(base + carve<double>(off, B));
     k.rho_est = (double*)(base + carve<double>(off, B));
     k.ct = (signed char*)(base + carve<signed char>(off, B * m));
+    k.err = (int*)(base + carve<int>(off, B));  // (err right before status: check_setup reads both in one copy)
     k.status = (int*)(base + carve<int>(off, B));
     k.iter = (int*)(base + carve<int>(off, B));
     k.rho_upd = (int*)(base + carve<int>(off, B));
     k.pstat = (int*)(base + carve<int>(off, B));
-    k.err = (int*)(base + carve<int>(off, B));
     k.ffresh = (int*)(base + carve<int>(off, B));  // zero from the memset above
     k.reuse = !(getenv("MPCQP_FACTOR_REUSE") && getenv("MPCQP_FACTOR_REUSE")[0] == '0');
     {  // dispatch order (kernels.hip::k_order), identity until the first solve
@@ -435,7 +446,7 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io) {
     // the zeroing, the identity order and the parameter block in stream order, one wait for
     // all three (callers then use the workspace from any stream or from the host)
     HIPCHK(hipMemcpyAsync((void*)k.self, &k, sizeof(KParams), hipMemcpyHostToDevice, s.stream));
-    HIPCHK(hipStreamSynchronize(s.stream));
+    if (sync) HIPCHK(hipStreamSynchronize(s.stream));
     strace().mark("params upload");
     if (size_t lds = lds_kernel_bytes(k); lds > 160 * 1024)
         return fail(MPCQP_EUNSUPPORTED, "problem needs %zu bytes of LDS per instance (> 160 KiB)", lds);
@@ -534,12 +545,18 @@ struct PlanKey {
     }
 };
 std::mutex g_plan_mu;
-std::vector<std::pair<PlanKey, Plan>> g_plans;  // most recently used last
+std::vector<std::pair<PlanKey, std::shared_ptr<const Plan>>> g_plans;  // most recently used last
 constexpr size_t kPlanCache = 8;
 
 std::string cached_plan(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi, const int32_t* Ap,
-                        const int32_t* Ai, const mpcqp_settings& st, Plan& pl) {
-    if (n <= 0 || m < 0 || Pp[n] < 0 || Ap[n] < 0) return choose_plan(n, m, Pp, Pi, Ap, Ai, st, pl);
+                        const int32_t* Ai, const mpcqp_settings& st, std::shared_ptr<const Plan>& out) {
+    auto fresh = [&]() {
+        auto pl = std::make_shared<Plan>();
+        std::string err = choose_plan(n, m, Pp, Pi, Ap, Ai, st, *pl);
+        out = pl;
+        return err;
+    };
+    if (n <= 0 || m < 0 || Pp[n] < 0 || Ap[n] < 0) return fresh();
     PlanKey k;
     k.n = n;
     k.m = m;
@@ -556,15 +573,15 @@ std::string cached_plan(int32_t n, int32_t m, const int32_t* Pp, const int32_t* 
         std::lock_guard<std::mutex> lk(g_plan_mu);
         for (size_t i = g_plans.size(); i-- > 0;)
             if (g_plans[i].first == k) {
-                pl = g_plans[i].second;
+                out = g_plans[i].second;  // shared, not copied (a cfg-5 plan copy took ~35 us)
                 std::rotate(g_plans.begin() + i, g_plans.begin() + i + 1, g_plans.end());
                 return std::string();
             }
     }
-    std::string err = choose_plan(n, m, Pp, Pi, Ap, Ai, st, pl);
+    std::string err = fresh();
     if (err.empty()) {
         std::lock_guard<std::mutex> lk(g_plan_mu);
-        g_plans.emplace_back(std::move(k), pl);
+        g_plans.emplace_back(std::move(k), out);
         if (g_plans.size() > kPlanCache) g_plans.erase(g_plans.begin());
     }
     return err;
@@ -616,7 +633,7 @@ int make_handle(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi, cons
         h->shards.push_back(s);
     }
     for (auto& s : h->shards)
-        if (int e = alloc_shard(h.get(), s, with_io)) { mpcqp_free(h.release()); return e; }
+        if (int e = alloc_shard(h.get(), s, with_io, !with_io)) { mpcqp_free(h.release()); return e; }
     *out = h.release();
     return 0;
 }
@@ -715,20 +732,23 @@ int check_setup(mpcqp_handle* h) {
     const long n = h->n, m = h->m;
     std::vector<int*> got(h->shards.size(), nullptr);
     std::vector<std::vector<int>> host(h->shards.size());
+    std::vector<long> stoff(h->shards.size(), 0);  // status's offset from err in got[]
     for (size_t si = 0; si < h->shards.size(); ++si) {
         Shard& s = h->shards[si];
         HIPCHK(hipSetDevice(s.dev));
         if (int e = stream_enter(s, s.stream)) return e;
         HIPCHK(launch_solve(s.kp, s.B, s.out_x, s.out_y, 1, s.stream));
-        const size_t ib = sizeof(double) * (size_t)s.B * (n + 2 * m) + sizeof(int) * (size_t)s.B;
+        // err and status in one copy: the workspace carves err right before status
+        const size_t span = (size_t)((const char*)(s.kp.status + s.B) - (const char*)s.kp.err);
+        const size_t ib = std::max(span, sizeof(double) * (size_t)s.B * (n + 2 * m) + sizeof(int) * (size_t)s.B);
         if (ib <= kStageMax) {
             if (!s.hin) {
                 HIPCHK(pool_malloc(s.dev, ib, (void**)&s.hin, true));
                 s.hin_bytes = ib;
             }
-            got[si] = (int*)s.hin;  // err (B), then status (B)
-            HIPCHK(hipMemcpyAsync(got[si], s.kp.err, sizeof(int) * s.B, hipMemcpyDeviceToHost, s.stream));
-            HIPCHK(hipMemcpyAsync(got[si] + s.B, s.kp.status, sizeof(int) * s.B, hipMemcpyDeviceToHost, s.stream));
+            got[si] = (int*)s.hin;  // err (B), then status (B) at stoff[si]
+            HIPCHK(hipMemcpyAsync(got[si], s.kp.err, span, hipMemcpyDeviceToHost, s.stream));
+            stoff[si] = s.kp.status - s.kp.err;
         }
         if (int e = stream_leave(s, s.stream)) return e;
     }
@@ -741,6 +761,7 @@ int check_setup(mpcqp_handle* h) {
             HIPCHK(hipMemcpy(host[si].data(), s.kp.err, sizeof(int) * s.B, hipMemcpyDeviceToHost));
             HIPCHK(hipMemcpy(host[si].data() + s.B, s.kp.status, sizeof(int) * s.B, hipMemcpyDeviceToHost));
             got[si] = host[si].data();
+            stoff[si] = s.B;
         }
     }
     for (size_t si = 0; si < h->shards.size(); ++si)
@@ -749,7 +770,7 @@ int check_setup(mpcqp_handle* h) {
                 return fail(MPCQP_EINVAL, "instance %ld: invalid data (l > u or NaN bounds)", h->shards[si].b0 + i);
     for (size_t si = 0; si < h->shards.size(); ++si)
         for (long i = 0; i < h->shards[si].B; ++i)
-            if (got[si][h->shards[si].B + i] == MPCQP_NON_CVX_)
+            if (got[si][stoff[si] + i] == MPCQP_NON_CVX_)
                 return fail(MPCQP_ENONCVX, "instance %ld: P is not convex (the KKT matrix is not quasi-definite)",
                             h->shards[si].b0 + i);
     return 0;
@@ -783,6 +804,7 @@ void free_shard(Shard& s) {
     pool_free(s.dev, s.dws_bytes, s.dws, false);
     pool_free(s.dev, s.dplan_bytes, s.dplan, false, s.dplan_tag);
     pool_free(s.dev, s.hstage_bytes, s.hstage, true);
+    pool_free(s.dev, s.dstage_bytes, s.dstage, false);
     pool_free(s.dev, s.hin_bytes, s.hin, true);
     pool_stream_release(s);
     s = Shard{};
@@ -801,12 +823,13 @@ int replan_plain(mpcqp_handle* h) {
     if (int e = sync_all(h)) return e;
     mpcqp_settings st = h->set;
     st.polish = 1;
-    Plan npl;
-    std::string err = choose_plan(h->n, h->m, h->Pp.data(), h->Pi.data(), h->Ap.data(), h->Ai.data(), st, npl);
+    auto npl = std::make_shared<Plan>();
+    std::string err = choose_plan(h->n, h->m, h->Pp.data(), h->Pi.data(), h->Ap.data(), h->Ai.data(), st, *npl);
     if (!err.empty()) return fail(MPCQP_EUNSUPPORTED, "re-plan for polish: %s", err.c_str());
-    Plan old = std::move(h->plan);
-    h->plan = std::move(npl);
-    const long n = h->n, m = h->m, npo = old.npad, npn = h->plan.npad;
+    std::shared_ptr<const Plan> oldp = h->plan;
+    const Plan& old = *oldp;
+    h->plan = npl;
+    const long n = h->n, m = h->m, npo = old.npad, npn = h->plan->npad;
     std::vector<Shard> fresh;
     int rc = 0;
     for (auto& os : h->shards) {
@@ -854,7 +877,7 @@ int replan_plain(mpcqp_handle* h) {
             }
             std::fill(hn.begin(), hn.end(), t == 1 ? 1.0 : 0.0);
             for (long i = 0; i < B; ++i)
-                for (long j = 0; j < n; ++j) hn[i * npn + h->plan.var_pad[j]] = ho[i * npo + old.var_pad[j]];
+                for (long j = 0; j < n; ++j) hn[i * npn + h->plan->var_pad[j]] = ho[i * npo + old.var_pad[j]];
             if (hipMemcpy(cols_new[t], hn.data(), D8 * B * npn, hipMemcpyHostToDevice) != hipSuccess)
                 rc = fail(MPCQP_EDEVICE, "re-plan: copy-in failed");
         }
@@ -867,7 +890,7 @@ int replan_plain(mpcqp_handle* h) {
                 rc = fail(MPCQP_EDEVICE, "re-plan: copy-out failed");
             } else {
                 for (long i = 0; i < B; ++i)
-                    for (long v = 0; v < nz; ++v) an[i * nz + h->plan.csc_pos[v]] = ao[i * nz + old.csc_pos[v]];
+                    for (long v = 0; v < nz; ++v) an[i * nz + h->plan->csc_pos[v]] = ao[i * nz + old.csc_pos[v]];
                 if (hipMemcpy(b.Ax, an.data(), D8 * B * nz, hipMemcpyHostToDevice) != hipSuccess)
                     rc = fail(MPCQP_EDEVICE, "re-plan: copy-in failed");
             }
@@ -881,7 +904,7 @@ int replan_plain(mpcqp_handle* h) {
     }
     if (rc) {  // the handle keeps its old plan and workspace
         for (auto& s : fresh) free_shard(s);
-        h->plan = std::move(old);
+        h->plan = oldp;
         return rc;
     }
     for (auto& s : h->shards) free_shard(s);
@@ -946,15 +969,37 @@ int mpcqp_setup_batch(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi
     mpcqp_handle* h = nullptr;
     if (int e = make_handle(n, m, Pp, Pi, Ap, Ai, B, settings, devs, true, &h)) return e;
     if (int e = check_bounds_host(h, l, u, B)) { mpcqp_free(h); return e; }
-    const Plan& pl = h->plan;
+    const Plan& pl = *h->plan;
     auto upload = [&](Shard& s) -> int {
         const long b0 = s.b0, Bs = s.B;
         HIPCHK(hipSetDevice(s.dev));
-        HIPCHK(hipMemcpyAsync(s.in_Px, Px + b0 * pl.nnzP, sizeof(double) * Bs * pl.nnzP, hipMemcpyHostToDevice, s.stream));
-        HIPCHK(hipMemcpyAsync(s.in_Ax, Ax + b0 * pl.nnzA, sizeof(double) * Bs * pl.nnzA, hipMemcpyHostToDevice, s.stream));
-        HIPCHK(hipMemcpyAsync(s.in_q, q + b0 * n, sizeof(double) * Bs * n, hipMemcpyHostToDevice, s.stream));
-        HIPCHK(hipMemcpyAsync(s.in_l, l + b0 * m, sizeof(double) * Bs * m, hipMemcpyHostToDevice, s.stream));
-        HIPCHK(hipMemcpyAsync(s.in_u, u + b0 * m, sizeof(double) * Bs * m, hipMemcpyHostToDevice, s.stream));
+        // the five inputs lie one after another in the workspace (alloc_shard's carve): a small
+        // shard stages them in pinned memory with the same layout and goes up in one copy (five
+        // pageable copies cost ~4 us each on a one-QP setup)
+        const size_t span = (size_t)((const char*)(s.in_u + Bs * m) - (const char*)s.in_Px);
+        const size_t upd = sizeof(double) * (size_t)Bs * (n + 2 * m) + sizeof(int) * (size_t)Bs;  // (update's use)
+        if (span <= kStageMax) {
+            if (!s.hin) {
+                HIPCHK(pool_malloc(s.dev, std::max(span, upd), (void**)&s.hin, true));
+                s.hin_bytes = std::max(span, upd);
+            }
+            char* const hb = (char*)s.hin;
+            auto put = [&](const double* dst, const double* src, size_t cnt) {
+                memcpy(hb + ((const char*)dst - (const char*)s.in_Px), src, sizeof(double) * cnt);
+            };
+            put(s.in_Px, Px + b0 * pl.nnzP, (size_t)Bs * pl.nnzP);
+            put(s.in_Ax, Ax + b0 * pl.nnzA, (size_t)Bs * pl.nnzA);
+            put(s.in_q, q + b0 * n, (size_t)Bs * n);
+            put(s.in_l, l + b0 * m, (size_t)Bs * m);
+            put(s.in_u, u + b0 * m, (size_t)Bs * m);
+            HIPCHK(hipMemcpyAsync(s.in_Px, hb, span, hipMemcpyHostToDevice, s.stream));
+        } else {
+            HIPCHK(hipMemcpyAsync(s.in_Px, Px + b0 * pl.nnzP, sizeof(double) * Bs * pl.nnzP, hipMemcpyHostToDevice, s.stream));
+            HIPCHK(hipMemcpyAsync(s.in_Ax, Ax + b0 * pl.nnzA, sizeof(double) * Bs * pl.nnzA, hipMemcpyHostToDevice, s.stream));
+            HIPCHK(hipMemcpyAsync(s.in_q, q + b0 * n, sizeof(double) * Bs * n, hipMemcpyHostToDevice, s.stream));
+            HIPCHK(hipMemcpyAsync(s.in_l, l + b0 * m, sizeof(double) * Bs * m, hipMemcpyHostToDevice, s.stream));
+            HIPCHK(hipMemcpyAsync(s.in_u, u + b0 * m, sizeof(double) * Bs * m, hipMemcpyHostToDevice, s.stream));
+        }
         HIPCHK(launch_setup(s.kp, Bs, s.in_Px, s.in_Ax, s.in_q, s.in_l, s.in_u, s.stream));
         return stream_leave(s, s.stream);
     };
@@ -1033,7 +1078,7 @@ int mpcqp_update_matrices_batch(mpcqp_handle* h, const double* Px, const int32_t
     if (!h) return fail(MPCQP_EINVAL, "NULL handle");
     h->staged = false;  // (device work: the staged results of the last solve are stale)
     if (!Px && !Ax) return fail(MPCQP_EINVAL, "no matrix values given");
-    const Plan& pl = h->plan;
+    const Plan& pl = *h->plan;
     // the columns of the value arrays that are written: all, or per index its last
     // occurrence (OSQP's sequential loop: a repeated index takes the last value)
     auto pick_cols = [&](const int32_t* idx, int32_t k, int nnz, const char* name, std::vector<int>& col,
@@ -1115,7 +1160,7 @@ int mpcqp_update_settings(mpcqp_handle* h, const mpcqp_settings* s, int32_t set_
         s->adaptive_rho_tolerance != o.adaptive_rho_tolerance || s->adaptive_rho_interval != o.adaptive_rho_interval)
         return fail(MPCQP_EINVAL, "sigma, scaling and the adaptive-rho settings cannot be changed after setup");
     if (int e = validate_settings(*s)) return e;  // (polish's delta / refinement steps included)
-    if (s->polish && h->plan.ne > 0)  // polish factors all of K: the plain plan, state kept
+    if (s->polish && h->plan->ne > 0)  // polish factors all of K: the plain plan, state kept
         if (int e = replan_plain(h)) return e;
     const bool rho_changed = set_rho != 0;
     const double rho = std::min(std::max(s->rho, 1e-6), 1e6);  // osqp_update_rho: RHO_MIN / RHO_MAX
@@ -1190,28 +1235,36 @@ int mpcqp_solve_batch(mpcqp_handle* h, double* x, double* y, int32_t* status, in
                 HIPCHK(pool_malloc(s.dev, sb, (void**)&s.hstage, true));
                 s.hstage_bytes = sb;
             }
+            if (!s.dstage) {
+                HIPCHK(pool_malloc(s.dev, sb, (void**)&s.dstage, false));
+                s.dstage_bytes = sb;
+            }
             const Stage g = stage_of(h, s);
             const long Bs = s.B;
-            auto cp = [&](void* dst, const void* src, size_t bytes) -> int {
-                HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s.stream));
-                return 0;
+            // one gather kernel into the device twin of the staging layout, one copy down
+            GatherList gl{};
+            auto add = [&](const void* hdst, const void* src, long cnt, int sz) {
+                GatherSeg& e = gl.seg[gl.nseg++];
+                e.src = src;
+                e.off = (long)((const char*)hdst - s.hstage);
+                e.cnt = cnt;
+                e.sz = sz;
+                gl.most = std::max(gl.most, cnt);
             };
-            if (int e = cp(g.x, s.out_x, sizeof(double) * Bs * n)) return e;
-            if (int e = cp(g.y, s.out_y, sizeof(double) * Bs * m)) return e;
-            if (int e = cp(g.obj, s.kp.obj, sizeof(double) * Bs)) return e;
-            if (int e = cp(g.pri, s.kp.pri, sizeof(double) * Bs)) return e;
-            if (int e = cp(g.dua, s.kp.dua, sizeof(double) * Bs)) return e;
-            if (int e = cp(g.rho_est, s.kp.rho_est, sizeof(double) * Bs)) return e;
-            if (int e = cp(g.dxc, s.kp.dxc, sizeof(double) * Bs * n)) return e;
-            if (int e = cp(g.dyc, s.kp.dyc, sizeof(double) * Bs * m)) return e;
-            if (int e = cp(g.status, s.kp.status, sizeof(int) * Bs)) return e;
-            if (int e = cp(g.iter, s.kp.iter, sizeof(int) * Bs)) return e;
-            if (int e = cp(g.rho_upd, s.kp.rho_upd, sizeof(int) * Bs)) return e;
-            if (h->set.polish) {
-                if (int e = cp(g.pstat, s.kp.pstat, sizeof(int) * Bs)) return e;
-            } else {
-                std::fill(g.pstat, g.pstat + Bs, 0);
-            }
+            add(g.x, s.out_x, Bs * n, 8);
+            add(g.y, s.out_y, Bs * m, 8);
+            add(g.obj, s.kp.obj, Bs, 8);
+            add(g.pri, s.kp.pri, Bs, 8);
+            add(g.dua, s.kp.dua, Bs, 8);
+            add(g.rho_est, s.kp.rho_est, Bs, 8);
+            add(g.dxc, s.kp.dxc, Bs * n, 8);
+            add(g.dyc, s.kp.dyc, Bs * m, 8);
+            add(g.status, s.kp.status, Bs, 4);
+            add(g.iter, s.kp.iter, Bs, 4);
+            add(g.rho_upd, s.kp.rho_upd, Bs, 4);
+            add(g.pstat, h->set.polish ? (const void*)s.kp.pstat : nullptr, Bs, 4);  // (no polish: zeros)
+            HIPCHK(launch_gather(gl, s.dstage, s.stream));
+            HIPCHK(hipMemcpyAsync(s.hstage, s.dstage, sb, hipMemcpyDeviceToHost, s.stream));
         } else {
             all_staged = false;
             if (x) HIPCHK(hipMemcpyAsync(x + s.b0 * n, s.out_x, sizeof(double) * s.B * n, hipMemcpyDeviceToHost, s.stream));
@@ -1484,17 +1537,17 @@ int mpcqp_timing_read(mpcqp_handle* h, double* setup_ms, int32_t* n_setup, doubl
 
 int mpcqp_get_plan_info(const mpcqp_handle* h, mpcqp_plan_info* info) {
     if (!h || !info) return fail(MPCQP_EINVAL, "NULL argument");
-    info->n = h->n; info->m = h->m; info->nb = h->plan.nb; info->block = kS;
-    info->npad = h->plan.npad; info->max_level = h->plan.max_level;
+    info->n = h->n; info->m = h->m; info->nb = h->plan->nb; info->block = kS;
+    info->npad = h->plan->npad; info->max_level = h->plan->max_level;
     info->batch = h->B; info->n_devices = (int)h->shards.size();
     info->lds_bytes_solve = h->shards.empty() ? 0 : (int64_t)lds_kernel_bytes(h->shards[0].kp);
-    info->bytes_per_instance = (int64_t)(workspace_bytes(h->plan, 1, false));
-    info->amax = h->plan.amax;
-    info->gather_k = h->plan.gather_k;
+    info->bytes_per_instance = (int64_t)(workspace_bytes(*h->plan, 1, false));
+    info->amax = h->plan->amax;
+    info->gather_k = h->plan->gather_k;
     info->variant = h->shards.empty() ? -1 : h->shards[0].kp.variant;
     info->threads_per_qp = h->shards.empty() ? 0 : solve_threads(h->shards[0].kp.variant);
-    info->n_eliminated = h->plan.ne;
-    info->plan_choice = h->plan.choice;
+    info->n_eliminated = h->plan->ne;
+    info->plan_choice = h->plan->choice;
     return 0;
 }
 

@@ -108,6 +108,22 @@ hipError_t launch_warm(const KParams& p, long B, const double* x, const double* 
 hipError_t launch_order(const KParams& p, long B, hipStream_t st);
 // order[i] = i (the identity dispatch order of a fresh workspace), enqueued on st
 hipError_t launch_iota(int* order, long B, hipStream_t st);
+// Small host calls' result staging (api.hip::mpcqp_solve_batch): every array a solve returns
+// gathered into one device buffer by one kernel, so that one copy brings it to pinned memory
+// (eleven D2H copies ran as eleven ~5 us blit kernels one after another)
+struct GatherSeg {
+    const void* src;  // nullptr: fill with zeros
+    long off;         // byte offset in the destination
+    long cnt;         // elements
+    int sz;           // element bytes: 8 or 4
+};
+constexpr int kGatherMax = 12;
+struct GatherList {
+    GatherSeg seg[kGatherMax];
+    int nseg;
+    long most;  // the largest cnt
+};
+hipError_t launch_gather(const GatherList& g, void* dst, hipStream_t st);
 // streaming device copy of n doubles (n % 16384 == 0) in one of three forms (kernels.hip),
 // mpcqp_debug_copy
 hipError_t launch_copy16(const double* src, double* dst, long n, hipStream_t st, int form);

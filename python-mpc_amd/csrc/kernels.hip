@@ -20,6 +20,8 @@
 // z~ = A x~).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "device_common.h"
 #include "setup_r.h"
 #include "wave_util.h"
@@ -427,6 +429,29 @@ __global__ void k_iota(int* __restrict__ order, long B) {
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < B) order[i] = (int)i;
 }
+__global__ __launch_bounds__(256) void k_gather(GatherList g, char* __restrict__ dst) {
+    const long t0 = (long)blockIdx.x * 256 + threadIdx.x, stride = (long)gridDim.x * 256;
+    for (int s = 0; s < g.nseg; ++s) {
+        const GatherSeg& sg = g.seg[s];
+        if (sg.sz == 8) {
+            const double* src = (const double*)sg.src;
+            double* d = (double*)(dst + sg.off);
+            for (long i = t0; i < sg.cnt; i += stride) d[i] = src ? src[i] : 0.0;
+        } else {
+            const int* src = (const int*)sg.src;
+            int* d = (int*)(dst + sg.off);
+            for (long i = t0; i < sg.cnt; i += stride) d[i] = src ? src[i] : 0;
+        }
+    }
+}
+
+hipError_t launch_gather(const GatherList& g, void* dst, hipStream_t st) {
+    if (g.nseg <= 0 || g.nseg > kGatherMax) return hipErrorInvalidValue;
+    const long blocks = std::min<long>(std::max<long>((g.most + 255) / 256, 1), 1024);
+    hipLaunchKernelGGL(k_gather, dim3((unsigned)blocks), dim3(256), 0, st, g, (char*)dst);
+    return hipGetLastError();
+}
+
 hipError_t launch_iota(int* order, long B, hipStream_t st) {
     hipLaunchKernelGGL(k_iota, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, order, B);
     return hipGetLastError();

@@ -261,21 +261,26 @@ def plan_preview(P, A, **settings):
     return out
 
 
-def _kept_index(V):
+def _keep_mask(V):
+    """The value indices of the user's pattern that are nonzero in some instance."""
+    V = np.asarray(V)
+    return (V != 0).any(axis=0) if V.shape[0] > 1 else V[0] != 0
+
+
+def _kept_index(V, keep=None):
     """Per value index of the user's pattern: its index once the entries zero in every
     instance are dropped (_drop_common_zeros), or -1."""
-    V = np.asarray(V)
-    keep = (V != 0).any(axis=0) if V.shape[0] > 1 else V[0] != 0
+    keep = _keep_mask(V) if keep is None else keep
     out = np.full(keep.size, -1, np.int64)
     out[keep] = np.arange(int(keep.sum()))
     return out
 
 
-def _drop_common_zeros(M, V):
+def _drop_common_zeros(M, V, keep=None):
     """Entries zero in every instance dropped from the pattern M (CSC, sorted) and from the
     values V (B x nnz), without scipy's copies (the kept entries keep their order)."""
     V = np.asarray(V)
-    keep = (V != 0).any(axis=0) if V.shape[0] > 1 else V[0] != 0
+    keep = _keep_mask(V) if keep is None else keep
     if keep.all():
         return M, V
     n = M.shape[1]
@@ -330,11 +335,13 @@ class OSQPBatch:
         # zeros of the reference's assembly (e.g. C~'QC~ at mpc_dynamics.py:296-297)
         # out of the sparsity plan.
         # user value index -> index in the kept pattern (-1: dropped), for update(Px_idx=, Ax_idx=)
-        self._pmap = _kept_index(Px)
-        self._amap = _kept_index(Ax)
+        # (the index maps are formed on the first update(Px=/Ax=), not at every setup)
+        kp, ka = _keep_mask(Px), _keep_mask(Ax)
+        self._keep = (kp, ka)
+        self._pmap = self._amap = None
         self._nnz_user = (P.nnz, A.nnz)
-        P, Px = _drop_common_zeros(P, Px)
-        A, Ax = _drop_common_zeros(A, Ax)
+        P, Px = _drop_common_zeros(P, Px, kp)
+        A, Ax = _drop_common_zeros(A, Ax, ka)
         Px = np.ascontiguousarray(Px, np.float64)
         Ax = np.ascontiguousarray(Ax, np.float64)
         q = np.ascontiguousarray(q); l = np.ascontiguousarray(l); u = np.ascontiguousarray(u)
@@ -368,6 +375,8 @@ class OSQPBatch:
         if q is not None or l is not None or u is not None:
             self._update_vectors(h, q, l, u)
         if Px is not None or Ax is not None:
+            if self._pmap is None:
+                self._pmap, self._amap = _kept_index(None, self._keep[0]), _kept_index(None, self._keep[1])
             P = self._matrix_values(Px, Px_idx, self._pmap, self._nnz_user[0], "P")
             A = self._matrix_values(Ax, Ax_idx, self._amap, self._nnz_user[1], "A")
             pv, pi = P if P else (None, None)
