@@ -1619,7 +1619,7 @@ int mpcqp_debug_copy(const double* src, double* dst, int64_t n, int32_t reps, vo
     HIPCHK(hipEventCreate(&a));
     HIPCHK(hipEventCreate(&b));
     double best = 0.0;
-    for (int form = 0; form < 3; ++form) {  // the fastest of the three forms
+    for (int form = 0; form < 5; ++form) {  // the fastest of the five forms (kernels.hip::launch_copy16)
         HIPCHK(launch_copy16(src, dst, n, st, form));  // (warm-up)
         HIPCHK(hipEventRecord(a, st));
         for (int r = 0; r < reps; ++r) HIPCHK(launch_copy16(src, dst, n, st, form));

@@ -524,14 +524,17 @@ __global__ __launch_bounds__(256) void k_copy16(const v2d* __restrict__ s, v2d* 
 }
 
 // form: 0 non-temporal, 4 granules per lane, 2048 workgroups; 1 default policy, 4 granules,
-// 2048; 2 default policy, 8 granules, 4096 (n % 8192 == 0)
+// 2048; 2 default policy, 8 granules, 4096; 3 / 4 default policy / non-temporal, 4 granules, one
+// pass (a workgroup per 16 KiB, no grid-stride loop) (n % 8192 == 0)
 hipError_t launch_copy16(const double* src, double* dst, long n, hipStream_t st, int form) {
     const v2d* s = (const v2d*)src;
     v2d* d = (v2d*)dst;
     switch (form) {
         case 0: hipLaunchKernelGGL((k_copy16<true, 4>), dim3(2048), dim3(256), 0, st, s, d, n / 2); break;
         case 1: hipLaunchKernelGGL((k_copy16<false, 4>), dim3(2048), dim3(256), 0, st, s, d, n / 2); break;
-        default: hipLaunchKernelGGL((k_copy16<false, 8>), dim3(4096), dim3(256), 0, st, s, d, n / 2); break;
+        case 2: hipLaunchKernelGGL((k_copy16<false, 8>), dim3(4096), dim3(256), 0, st, s, d, n / 2); break;
+        case 3: hipLaunchKernelGGL((k_copy16<false, 4>), dim3((unsigned)(n / 2048)), dim3(256), 0, st, s, d, n / 2); break;
+        default: hipLaunchKernelGGL((k_copy16<true, 4>), dim3((unsigned)(n / 2048)), dim3(256), 0, st, s, d, n / 2); break;
     }
     return hipGetLastError();
 }
