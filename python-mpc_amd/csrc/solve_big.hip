@@ -650,6 +650,10 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
                 const double a0 = j0 < lim ? h0 * x0 : 0.0;
                 const double a1 = j0 + 8 < lim ? h1 * x8 : 0.0;
                 const double c = reduce8(a0 + a1);
+                // t_k used by every lane here (an empty asm), so its read stays with the step's
+                // other reads: the compiler had sunk it into the writer's branch, behind the
+                // reduction -- an LDS round trip on every backward step's critical path
+                asm volatile("" ::"v"(tk));
                 if (writer) xt[k * S + i] = tk - c;
             }
             __syncthreads();
