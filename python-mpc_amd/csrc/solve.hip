@@ -675,7 +675,7 @@ size_t lds_kernel_bytes(const KParams& p) {
     if (p.variant == 16) return lds_dense_bytes(p);
 #endif
     if (p.variant == 10 || p.variant == 17) return lds_w2_bytes(p);
-    return p.variant >= 11 && p.variant <= 14 ? lds_solve_bytes_big(p) : lds_solve_bytes(p);
+    return (p.variant >= 11 && p.variant <= 15) ? lds_solve_bytes_big(p) : lds_solve_bytes(p);
 }
 
 template <int NB, int A, int K, int CS, int RS, int W, bool TRI = false>
@@ -699,9 +699,10 @@ bool variant_fits(const KParams& p, int v) {
     const int cs = (p.npad + T - 1) / T, rs = (p.m + T - 1) / T;
     if (p.ne && v != 17) return false;  // eliminated variables: the four-wave kernel only
 #ifndef MPCQP_EXPERIMENTAL
-    // measured and not taken: one-wave 8 / 9, two-wave two-sided 14, dense
-    // inverse 16, eight-wave 18 -- only in the exp / diagnostic builds (MPCQP_BUILD=exp)
-    if (v == 8 || v == 9 || v == 14 || v == 16 || v == 18) return false;
+    // measured and not taken: one-wave 8 / 9, two-wave two-sided 14,
+    // 256-thread twisted 15, dense inverse 16, eight-wave 18 -- only in the exp / diagnostic
+    // builds (MPCQP_BUILD=exp)
+    if (v == 8 || v == 9 || v == 14 || v == 15 || v == 16 || v == 18) return false;
 #endif
     switch (v) {
         case 0: case 7: return p.nb == 4 && p.amax <= 8 && p.gk <= 6 && cs <= 1 && rs <= 1;
@@ -721,6 +722,11 @@ bool variant_fits(const KParams& p, int v) {
             const int nbm = v == 11 ? 12 : v == 12 ? 18 : 24, csm = v == 11 ? 1 : 2, rsm = v == 13 ? 3 : 2;
             const int csb = (p.npad + kThreadsBig - 1) / kThreadsBig, rsb = (p.m + kThreadsBig - 1) / kThreadsBig;
             return p.nb > 4 && p.nb <= nbm && p.amax <= 16 && p.bmax <= 16 && p.gk <= 8 && csb <= csm && rsb <= rsm &&
+                   lds_solve_bytes_big(p) <= 160 * 1024;
+        }
+        case 15: {  // 256 threads, one wave per SIMD (twisted_solve4): nb <= 18
+            const int csb = (p.npad + 255) / 256, rsb = (p.m + 255) / 256;
+            return p.nb > 4 && p.nb <= 18 && p.amax <= 16 && p.bmax <= 16 && p.gk <= 8 && csb <= 3 && rsb <= 4 &&
                    lds_solve_bytes_big(p) <= 160 * 1024;
         }
         case 14:
@@ -767,6 +773,7 @@ int solve_threads(int variant) {
         case 10: return 128;
         case 11: case 12: case 13: return kThreadsBig;
         case 14: return 128;
+        case 15: return 256;
         case 16: return 256;
         case 17: return 256;
         case 18: return 512;
@@ -778,7 +785,7 @@ int solve_mode(int variant) {  // what factorize stores for the variant (KParams
     switch (variant) {
         case 0: case 8: case 9: case 10: case 17: case 18: return 2;
         case 1: case 2: case 3: case 7: case 16: return 1;  // (16: no factor stored; dx aliases rb)
-        case 11: case 12: case 13: case 14: return 3;  // two-sided factor (solve_big.hip)
+        case 11: case 12: case 13: case 14: case 15: return 3;  // two-sided factor (solve_big.hip)
         default: return 0;
     }
 }
@@ -799,7 +806,7 @@ static hipError_t launch_solve_only(const KParams& p, long B, double* xo, double
 #ifdef MPCQP_EXPERIMENTAL
         case 16: return launch_solve_dense(p, B, xo, yo, factor_only, st, ref);
 #endif
-        case 11: case 12: case 13: case 14: return launch_solve_big(p, B, xo, yo, factor_only, st, ref);
+        case 11: case 12: case 13: case 14: case 15: return launch_solve_big(p, B, xo, yo, factor_only, st, ref);
         default: return hipErrorInvalidValue;
     }
 }

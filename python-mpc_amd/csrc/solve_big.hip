@@ -475,7 +475,7 @@ template <int TT, class KP>
 __device__ __noinline__ bool factorize2_nl(const KP* gp, long b, double rho, double* X2) {
     const KPc& p = kconst(gp);
     SL2 C = carve(p);
-    if constexpr (TT == 512)  // (the two-wave variant 14 keeps the unsplit form)
+    if constexpr (TT >= 256)  // (the two-wave variant 14 keeps the unsplit form)
         return factorize2s<TT>(p, C.L, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
                                p.Si + b * (long)p.nb * SS);
     return factorize2<TT>(p, C.L, X2, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
@@ -540,11 +540,11 @@ __device__ __forceinline__ double dot4c(const double (&a)[4], const double (&v)[
 //   so: bits 0-15 the forward step's destination row (rb or corB, + kd S + toff), bits 16-31
 //       the backward step's x_{k+-1} (xt + ...);  fo: the F / G rows of the forward step,
 //       bits 16-31 the backward step's H rows.
-template <int SL>
+template <int SL, int TT = 512>
 __device__ __forceinline__ void step_offsets(const KParams& p, const int* toffL, const double* rb, const double* xt,
                                              const double* corB, const double* Fc, int (&so)[SL], int (&fo)[SL]) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    const int half = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8));
+    const int half = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / (TT / 2)));
     const int nb = p.nb, pm = p.pmeet, nmine = half ? nb - 1 - pm : pm;
     const int amax = p.amax, bmax = p.bmax, g0 = pm * amax;  // (Gc = Fc + g0 FGS)
     const int orb = (int)(rb - sm), oxt = (int)(xt - sm), ocb = (int)(corB - sm), ofc = (int)(Fc - sm);
@@ -664,6 +664,169 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
 }
 
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ double reduce4(double v) {  // sum over an aligned quad, result in all 4
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    return v;
+}
+
+// The twisted sweep on 256 threads (k_solve_b<256>, variant 15, experimental build only: measured
+// 43.0 against 35.7 ms on cfg 5, DESIGN.md §10 -- the steps are latency-bound, not issue-bound,
+// and one wave per SIMD hides none of it): one wave per SIMD, four lanes per tile row.  Thread t: half h = t / 128 (0 top, 1 bottom), (i, q) = (t % 128 / 4, t % 4):
+// lane q of row i holds columns [8 q, 8 q + 8) of every tile of its chain, so a forward step is
+// four 16-byte reads of w and four of the F / G row, 16 FMAs and two 2-level quad sums per lane
+// -- against twisted_solve's 8 lanes of 4 columns, 3-level sums and two waves per SIMD: the
+// 512-thread step issues ~78 instructions on each of two waves per SIMD, which is what a step
+// costs there (~940 cycles on cfg 5).  The same sums (association aside) in the same steps.
+template <int SL>
+struct TwoSided4 {
+    double Inv[SL][8];
+    __device__ __forceinline__ void load(int nb, int pm, int amax, int bmax, const double* __restrict__ Fg,
+                                         const double* __restrict__ Hg, const double* __restrict__ Sg,
+                                         double* __restrict__ Fc, double* __restrict__ Gc) {
+        constexpr int TT = 256;
+        const int tid = threadIdx.x, half = __builtin_amdgcn_readfirstlane(tid >> 7), u = tid & 127, i = u >> 2,
+                  q = u & 3;
+        const int nbot = nb - 1 - pm;
+#pragma unroll
+        for (int s = 0; s < SL; ++s) {
+            const bool have = half == 0 ? s <= pm : s < nbot;
+            const int k = half == 0 ? s : nb - 1 - s;
+            const double* src = Sg + (long)(have ? k : 0) * SS + i * S + 8 * q;
+#pragma unroll
+            for (int c = 0; c < 8; c += 2) {
+                const double2 t2 = have ? *(const double2*)(src + c) : make_double2(0.0, 0.0);
+                Inv[s][c] = t2.x;
+                Inv[s][c + 1] = t2.y;
+            }
+        }
+        for (int o = tid; o < pm * amax * S; o += TT) {  // row q = k amax + r of F_{k+1}
+            const int qq = o >> 5, j = o & (S - 1), k = qq / amax, r = qq - k * amax;
+            Fc[qq * FGS + j] = Fg[(long)(k + 1) * SS + r * S + j];
+        }
+        for (int o = tid; o < nbot * bmax * S; o += TT) {
+            const int qq = o >> 5, j = o & (S - 1), k = qq / bmax, r = qq - k * bmax;
+            Gc[qq * FGS + j] = Hg[(long)(pm + k) * SS + r * S + j];
+        }
+    }
+};
+
+__device__ __forceinline__ double dot8(const double (&a)[8], const double (&v)[8]) {
+    return ((a[0] * v[0] + a[1] * v[1]) + (a[2] * v[2] + a[3] * v[3])) +
+           ((a[4] * v[4] + a[5] * v[5]) + (a[6] * v[6] + a[7] * v[7]));
+}
+
+template <int SL>
+__device__ __forceinline__ void twisted_solve4(const TwoSided4<SL>& R, const KParams& p, const double* Fc,
+                                               const double* Gc, const int* toffL, const int (&so)[SL],
+                                               const int (&fo)[SL], double* rb, double* xt, double* corB,
+                                               long long* pacc) {
+    constexpr bool PRE = SL <= 10;  // (step offsets formed at the run start: step_offsets<SL, 256>)
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+#ifdef MPCQP_PHASE_PROF
+    long long t0s = clock64();
+#define SPH(k) if (pacc && threadIdx.x == 0) { const long long t_ = clock64(); pacc[k] += t_ - t0s; t0s = t_; }
+#else
+#define SPH(k)
+#endif
+    int opq = 0;
+    asm volatile("" : "+s"(opq));  // keep per-block LDS addresses out of the register budget
+    const int tid = threadIdx.x, half = __builtin_amdgcn_readfirstlane(tid >> 7), u = tid & 127, i = u >> 2,
+              q = u & 3, c8 = 8 * q + opq;
+    const int nb = p.nb, pm = p.pmeet, amax = p.amax, bmax = p.bmax, nbot = nb - 1 - pm;
+    const int nst = nbot > pm ? nbot : pm;
+    const int nmine = half ? nbot : pm, lim = half ? bmax : amax;
+    const bool writer = q == 0, lowrank = i < lim;
+    const int ir = lowrank ? i : 0;  // F / G row this thread sums (row 0 for the rest: reads stay in range)
+    auto ld8 = [](const double* a, double (&v)[8]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int c = 0; c < 8; c += 2) {
+            const double2 t2 = *(const double2*)(a + c);
+            v[c] = t2.x;
+            v[c + 1] = t2.y;
+        }
+    };
+    // forward: top step s: t_{s-1} = S_{s-1}^{-1} w_{s-1}, w_s -= F_s w_{s-1};
+    //          bottom step s (k = nb-1-s): t~_{k+1} = T_{k+1}^{-1} w~_{k+1}, w~_k -= G_k w~_{k+1}
+#pragma unroll
+    for (int s = 1; s < SL; ++s) {
+        if (s <= nst) {
+            if (s <= nmine) {
+                const int ks = half ? nb - s : s - 1, kd = half ? nb - 1 - s : s;
+                const int woff = PRE ? 0 : kd * S + (half ? toffL[kd] : 0);
+                const bool mid = half && kd == pm;
+                double* dst = PRE ? sm + (so[s] & 0xFFFF) + i : (mid ? corB : rb) + woff + i;
+                const double old = (writer && lowrank && !mid) ? *dst : 0.0;
+                double v8[8], f8[8];
+                ld8(rb + ks * S + c8, v8);
+                const double* f = PRE ? sm + (fo[s] & 0xFFFF) + ir * FGS
+                                           : (half ? Gc + (kd - pm) * bmax * FGS : Fc + (s - 1) * amax * FGS) + ir * FGS;
+                ld8(f + c8, f8);
+                const double t = reduce4(dot8(R.Inv[s - 1], v8));
+                const double c = reduce4(dot8(f8, v8));
+                if (writer) {
+                    xt[ks * S + i] = t;
+                    if (lowrank) *dst = mid ? c : old - c;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    SPH(12)
+    // middle: x_p = M^{-1} w_p with both chains' corrections, by the top half
+    if (half == 0) {
+        double w8[8], b8[8];
+        ld8(rb + pm * S + c8, w8);
+        ld8(corB + pm * S + c8, b8);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) w8[c] -= b8[c];
+#pragma unroll
+        for (int s = 0; s < SL; ++s) {
+            if (s == pm) {
+                const double t = reduce4(dot8(R.Inv[s], w8));
+                if (writer) xt[pm * S + i] = t;
+            }
+        }
+    }
+    __syncthreads();
+    SPH(13)
+    // backward: top x_k = t_k - H_k x_{k+1}[0, amax) (k = p-1 .. 0);
+    //           bottom x_k = t~_k - G_{k-1}' x_{k-1}[toff_{k-1} + (0, bmax)] (k = p+1 .. nb-1);
+    // lane q takes the rows r = q + 4 c (< lim) of the sum
+#pragma unroll
+    for (int s = 1; s < SL; ++s) {
+        if (s <= nst) {
+            if (s <= nmine) {
+                const int k = half ? pm + s : pm - s;
+                const double* x1 = PRE ? sm + (so[s] >> 16) : xt + (half ? (k - 1) * S + toffL[k - 1] : (k + 1) * S);
+                // H_k[i][r] = F_{k+1}[r][i] (top), G_{k-1}[r][i] (bottom); rows >= lim read as 0
+                const double* h = PRE ? sm + (fo[s] >> 16) + i
+                                           : (half ? Gc + (k - 1 - pm) * bmax * FGS : Fc + k * amax * FGS) + i;
+                const double tk = xt[k * S + i];
+                double hv[4], xv[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int r = q + 4 * c, rr = r < lim ? r : 0;
+                    hv[c] = h[rr * FGS];
+                    xv[c] = x1[rr];
+                }
+                double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+                for (int c = 0; c < 4; c += 2) {
+                    a0 += q + 4 * c < lim ? hv[c] * xv[c] : 0.0;
+                    a1 += q + 4 * c + 4 < lim ? hv[c + 1] * xv[c + 1] : 0.0;
+                }
+                const double cs = reduce4(a0 + a1);
+                asm volatile("" ::"v"(tk));  // (t_k's read stays with the step's other reads)
+                if (writer) xt[k * S + i] = tk - cs;
+            }
+            __syncthreads();
+        }
+    }
+    SPH(14)
+#undef SPH
+}
+
 // The interface form of the two-sided solve (round 5; opt-in, MPCQP_BIG_FORM=iface).
 // twisted_solve runs every forward and backward step of both chains on all 512 threads, one
 // workgroup barrier a step: 2 max(p, nb-1-p) + 1 barriers, ~820 cycles a forward step on cfg
@@ -723,12 +886,6 @@ struct TwoSidedQ {
         }
     }
 };
-
-__device__ __forceinline__ double reduce4(double v) {  // sum over an aligned quad, result in all 4
-    v += dpp<0xB1>(v);
-    v += dpp<0x4E>(v);
-    return v;
-}
 
 __device__ __forceinline__ void chain_sync() {  // one wave's LDS stores before its later loads
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1216,7 +1373,9 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
             PH(0)
         }
         // ---- run state (re-derived at every run start; nothing but scalars lives across calls) ----
-        std::conditional_t<IF, TwoSidedQ<NS + 1>, std::conditional_t<TTK == 512, TwoSided<NS + 1>, TwoSidedW<NS>>> RF;
+        std::conditional_t<IF, TwoSidedQ<NS + 1>,
+                           std::conditional_t<TTK == 512, TwoSided<NS + 1>,
+                                              std::conditional_t<TTK == 256, TwoSided4<NS + 1>, TwoSidedW<NS>>>> RF;
         if constexpr (IF) {
             RF.load(nb, p.pmeet, amax, p.bmax, Fg, Hg, Sg, Fc, Gc, frows);
             frows = false;
@@ -1230,7 +1389,8 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
             tvl = (tid & 63) < nb ? toffL[tid & 63] : 0;
             asm volatile("" : "+v"(tvl));
         }
-        if constexpr (!IF && TTK == 512 && NS < 10) step_offsets<NS + 1>(p, toffL, L.rb, L.xt, L.tv, Fc, so, fo);
+        if constexpr (!IF && (TTK == 512 || TTK == 256) && NS < 10)
+            step_offsets<NS + 1, TTK>(p, toffL, L.rb, L.xt, L.tv, Fc, so, fo);
         int cvar[CS];
         // gather lists as LDS-base offsets (GatherR): A' w for the rhs, A x~ for the rows
         extern __shared__ __attribute__((aligned(16))) double smb[];
@@ -1287,6 +1447,7 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
 #endif
             if constexpr (IF) iface_solve<NS + 1>(RF, p, Fc, Gc, tvl, L.rb, L.xt, L.tv, L.cor, pacc, pwp);
             else if constexpr (TTK == 512) twisted_solve<NS + 1>(RF, p, Fc, Gc, toffL, so, fo, L.rb, L.xt, L.tv, pacc);
+            else if constexpr (TTK == 256) twisted_solve4<NS + 1>(RF, p, Fc, Gc, toffL, so, fo, L.rb, L.xt, L.tv, pacc);
             else wave_twisted_solve<NS>(RF, p, Fc, Gc, toffL, L.rb, L.xt, L.cor, pacc);
             PH(2)
             // z~ = A x~ ; relaxed + projected z ; y ; next w.   x update; deltas for the checks.
@@ -1430,6 +1591,8 @@ hipError_t launch_solve_big(const KParams& p, long B, double* xo, double* yo, in
         case 12: return go_b<512, 9, 8, 2, 2>(p, B, xo, yo, factor_only, st, ref);   // nb <= 18
         case 13: return go_b<512, 12, 8, 2, 3>(p, B, xo, yo, factor_only, st, ref);  // nb <= 24
 #ifdef MPCQP_EXPERIMENTAL
+        // 256 threads, one wave per SIMD (twisted_solve4): measured and not taken
+        case 15: return go_b<256, 9, 8, 3, 4>(p, B, xo, yo, factor_only, st, ref);   // nb <= 18
         case 14: return go_b<128, 4, 8, 2, 2>(p, B, xo, yo, factor_only, st, ref);   // nb <= 8, two waves
 #endif
         default: return hipErrorInvalidValue;

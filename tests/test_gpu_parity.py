@@ -367,18 +367,19 @@ def test_alternative_kernel_variants(monkeypatch, variant, cfg, B):
     _batch_parity(b, settings)
 
 
-EXPERIMENTAL = [(14, 3, 256), (8, 2, 256), (16, 2, 256), (18, 3, 256)]
+EXPERIMENTAL = [(14, 3, 256), (8, 2, 256), (16, 2, 256), (18, 3, 256), (15, 5, 64)]
 
 
 def test_experimental_kernel_variants(tmp_path):
     """The variants measured and not taken are built only into the exp
     library (python-mpc_amd/csrc/Makefile, MPCQP_EXPERIMENTAL): the two-wave two-sided
     kernel on the slack layout (14), the one-wave kernel (8) and the dense-inverse kernel
-    (16) on cfg 2, the eight-wave kernel (18) on the slack layout.  They stay exact against
+    (16) on cfg 2, the eight-wave kernel (18) on the slack layout, the 256-thread twisted
+    long-horizon kernel (15) on cfg 5.  They stay exact against
     the oracle, solved in a child process under MPCQP_BUILD=exp; and the production
     library refuses them (MPCQP_VARIANT=v does not fit)."""
     import build_cases
-    sets = {2: dict(polish=False, warm_start=False), 3: dict(warm_start=True)}
+    sets = {2: dict(polish=False, warm_start=False), 3: dict(warm_start=True), 5: dict(polish=False, warm_start=False)}
     specs = [("batch", f"v{v}", cfg, B, str(v), sets[cfg]) for v, cfg, B in EXPERIMENTAL]
     got = build_cases.in_build("exp", specs, tmp_path / "exp.npz")
     for v, cfg, B in EXPERIMENTAL:

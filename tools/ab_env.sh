@@ -1,15 +1,22 @@
+#!/bin/bash
+# Same-box A/B of environment switches (through gpurun, from the repo root): the bench with
+# each "name|ENV=VAL ..." spec (empty env: the default) alternated `reps` times.
+# usage: bash tools/ab_env.sh <tag> <reps> "<bench args>" "name|env" "name|env" ...
 set -o pipefail
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-out=gpurun_out/r5ab2; mkdir -p $out
-for i in 1 2 3; do
-  timeout -k 10 200 python3 bench.py --no-cpu --no-dispatch-ab --no-pcie --no-latency > $out/base_$i.json 2> $out/base_$i.err || exit 1
-  MPCQP_BALANCE=1 timeout -k 10 200 python3 bench.py --no-cpu --no-dispatch-ab --no-pcie --no-latency > $out/bal_$i.json 2> $out/bal_$i.err || exit 1
+tag=$1; reps=$2; bargs=$3; shift 3
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+out=gpurun_out/$tag; mkdir -p $out
+for i in $(seq 1 $reps); do
+  for spec in "$@"; do
+    name=${spec%%|*}; envs=${spec#*|}
+    env $envs timeout -k 10 200 python3 bench.py --no-cpu --no-dispatch-ab --no-pcie --no-latency $bargs > $out/${name}_$i.json 2> $out/${name}_$i.err || { echo "$name failed"; tail -5 $out/${name}_$i.err; exit 1; }
+  done
 done
-MPCQP_BALANCE=1 MPCQP_PHASE_PROF=1 timeout -k 10 200 python3 tools/phase_prof.py --config 2 > $out/ph_bal.txt 2>&1 || exit 1
-python3 - <<'PY'
-import json
-for k in ("base","bal"):
-    v=[json.loads(open(f"gpurun_out/r5ab2/{k}_{i}.json").read().strip().splitlines()[-1]) for i in (1,2,3)]
-    print(k, [round(x["value"]) for x in v], [round(x["roofline"]["kernel_ms"],4) for x in v], [x["config"].get("iter_match_gpu") for x in v])
+python3 - $out $reps "$@" <<'PY'
+import json, sys
+out, reps = sys.argv[1], int(sys.argv[2])
+for spec in sys.argv[3:]:
+    k = spec.split("|")[0]
+    v = [json.loads(open(f"{out}/{k}_{i}.json").read().strip().splitlines()[-1]) for i in range(1, reps + 1)]
+    print(k, "value", [round(x["value"]) for x in v], "kernel_ms", [round(x["roofline"]["kernel_ms"], 4) for x in v])
 PY
-head -20 $out/ph_bal.txt
