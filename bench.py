@@ -408,16 +408,25 @@ def pcie_leg(solver, dev, local, bufs, host_in, outs, pin, steps, mode, warmup=8
             gc.enable()
 
 
-def latency_leg(reps=30, warmup=3):
+LATENCY_WORKLOAD = {
+    5: "incremental-dynamic-N50, ONE QP (n 508, m 916), fresh OSQP()+setup()+solve() per call, cold "
+       "(mpc_dynamics.py:392-396)",
+    2: "vanilla-lateral-N20, ONE QP (n 104, m 188), fresh OSQP()+setup()+solve() per call "
+       "(mpc_kinematics.py:194-198)",
+}
+
+
+def latency_leg(cfg=5, reps=30, warmup=3):
     """Per-call latency of the reference's Control/MPC call pattern, never `value`: a fresh
     osqp.OSQP() + setup() + solve() of ONE QP every call (Control/MPC/mpc_dynamics.py:392-396,
     mpc_kinematics.py:194-198), through the `import osqp` shim on the GPU, beside the oracle
     (one host thread) doing the same calls on the same QP.  The QP: instance 0 of the cfg-5
-    generator (incremental dynamic MPC, N = 50, cold start as mpc_increment sets it).  Medians
-    over `reps` calls; per-iteration figures divide the whole call by the ADMM iterations."""
+    generator (incremental dynamic MPC, N = 50, cold start as mpc_increment sets it), or of the
+    cfg-2 generator (the vanilla lateral layout of mpc_kinematics.mpc, N = 20).  Medians over
+    `reps` calls; per-iteration figures divide the whole call by the ADMM iterations."""
     import pyoracle
     from osqp_amd import OSQP, mpc
-    b = mpc.make_batch(5, B=1, seed=1)
+    b = mpc.make_batch(cfg, B=1, seed=1)
     P, A = b["P"].copy(), b["A"].copy()
     P.data, A.data = b["Px"][0].copy(), b["Ax"][0].copy()
     q, l, u = b["q"][0].copy(), b["l"][0].copy(), b["u"][0].copy()
@@ -443,8 +452,7 @@ def latency_leg(reps=30, warmup=3):
                      "solve_ms": float(np.median(tv)) * 1e3, "iters": it, "status": st,
                      "us_per_iter": tot * 1e6 / max(1, it), "solve_us_per_iter": float(np.median(tv)) * 1e6 / max(1, it)}
     out["cpu"]["threads"] = 1
-    out.update(workload="incremental-dynamic-N50, ONE QP (n 508, m 916), fresh OSQP()+setup()+solve() per call, "
-                        "cold (mpc_dynamics.py:392-396)",
+    out.update(workload=LATENCY_WORKLOAD[cfg],
                reps=reps, gpu_over_cpu_call=out["gpu"]["call_ms"] / out["cpu"]["call_ms"],
                method="host arrays through the osqp shim (osqp_amd.OSQP) vs oracle/osqp_oracle.c (pyoracle.OSQP, one "
                       "thread); medians; us_per_iter = the whole call / ADMM iterations")
@@ -745,7 +753,8 @@ def main(argv=None, solver_cls=None, device=None):
 
     latency = None
     if rank == 0 and world == 1 and on_gpu and not args.no_cpu and not args.no_latency:
-        latency = latency_leg()
+        latency = latency_leg(5)
+        latency["cfg2"] = latency_leg(2)  # (the kinematic scripts' call, the headline layout)
 
     if rank == 0:
         kname = solve_kernel_name(info, fused=fused)
