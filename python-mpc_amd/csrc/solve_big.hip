@@ -926,7 +926,7 @@ __device__ __forceinline__ void iface_solve(const TwoSidedQ<SL>& R, const KParam
     // SIMDs -- a workgroup's waves go round the SIMDs 0, 2, 1, 3 -- where waves 0 and 4 share one)
     constexpr int WB = 1;
     const int r = lane >> 2, q = lane & 3;  // chain lanes: row r, columns [8 q, 8 q + 8)
-    // ---- F: the forward chains (wave 0 top, wave 4 bottom).  Lanes past the chain's rows take
+    // ---- F: the forward chains (wave 0 top, wave 1 bottom).  Lanes past the chain's rows take
     // row 0 and store row 0's value again (the same sum): no lane mask in the chain ----
     // Each step's F / G row (static) is loaded one step ahead, after the step's dynamic reads, so
     // the step waits only for the rows the previous step wrote (LDS returns in order); two steps
@@ -1560,7 +1560,6 @@ size_t lds_solve_bytes_big(const KParams& p) {
     return lds_solve_bytes(p) + 16 + sizeof(double) * (size_t)big_fg_len(p) + sizeof(int) * (size_t)p.nb;
 }
 
-// the interface form (iface_solve) unless MPCQP_BIG_FORM=twisted (A/B against round 4's sweep)
 // The interface form is opt-in (MPCQP_BIG_FORM=iface, read once per process): exact, but slower
 // than the twisted sweep on cfg 5 (38.0 against 36.2 ms per launch)
 static bool big_iface() {
