@@ -837,7 +837,7 @@ __device__ __forceinline__ void twisted_solve4(const TwoSided4<SL>& R, const KPa
 //     w_s[U] = b_s[U] - F_s[:, R] b_{s-1}[R] - F_s[:, U] w_{s-1}[U]        (top, s = 1..p)
 // (the bottom chain likewise on the window rows W_k = [toff_k, toff_k + bmax) with G_k), and
 // backward x_k[U] = t_k[U] - F_{k+1}[:, U]' x_{k+1}[U].  Each chain is run by ONE wave -- wave
-// 0 the top, wave 4 the bottom -- ordered by its own instruction stream (LDS fence + wave
+// 0 the top, wave 1 the bottom -- ordered by its own instruction stream (LDS fence + wave
 // barrier, no s_barrier), lane (r, q) = (lane / 4, lane % 4) taking row r and columns
 // [8 q, 8 q + 8) (a quad sum); everything that is not on the recurrence runs on all threads
 // between four workgroup barriers:
