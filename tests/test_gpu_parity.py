@@ -1245,6 +1245,36 @@ def test_replan_matches_a_handle_set_up_on_the_plain_plan(monkeypatch):
     assert np.abs(ra.y - rc.y).max() <= 1e-12 * max(1.0, np.abs(rc.y).max())
 
 
+def test_handles_share_a_cached_plan_through_a_replan():
+    """Handles of one sparsity pattern share the plan cache's read-only plan (api.hip::cached_plan
+    hands out a shared pointer, no copy).  Re-planning one of them (update_settings(polish=True):
+    replan_plain) must leave the others on the shared plan, solving as before: a second handle of
+    the same pattern keeps its eliminated plan and its results are bit-identical to a third,
+    untouched one; and a fourth handle set up after the re-plan still gets the eliminated plan."""
+    b = mpc.make_batch(3, B=64, seed=43)
+    s = dict(warm_start=True)
+    hs = []
+    for _ in range(3):
+        h = OSQPBatch()
+        h.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
+        assert h.plan_info()["n_eliminated"] == 105
+        hs.append(h)
+    hs[0].solve()
+    hs[0].update_settings(polish=True)
+    assert hs[0].plan_info()["n_eliminated"] == 0
+    r1, r2 = hs[1].solve(), hs[2].solve()
+    assert hs[1].plan_info()["n_eliminated"] == 105 and hs[2].plan_info()["n_eliminated"] == 105
+    assert np.array_equal(r1.x, r2.x) and np.array_equal(r1.iter, r2.iter)
+    assert (r1.status_val == 1).all()
+    h4 = OSQPBatch()
+    h4.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
+    assert h4.plan_info()["n_eliminated"] == 105
+    r4 = h4.solve()
+    assert np.array_equal(r4.x, r1.x)
+    ra = hs[0].solve()
+    assert (ra.status_val == 1).all()
+
+
 def test_shim_update_settings_polish_demo():
     """osqp.OSQP().update_settings(polish=True, eps_abs=, eps_rel=) through the shim on the
     osqp documentation's demo problem: polished like the oracle, the closed-form optimum."""
