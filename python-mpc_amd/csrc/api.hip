@@ -521,7 +521,7 @@ std::string choose_plan(int32_t n, int32_t m, const int32_t* Pp, const int32_t* 
             if (!err.empty()) note = "eliminated plan failed: " + err;
         }
     }
-    std::string err = build_plan(n, m, Pp, Pi, Ap, Ai, pl, false, dense_w4_on());
+    std::string err = build_plan(n, m, Pp, Pi, Ap, Ai, pl, false, true);  // (balanced four-block merge: plan.cpp)
     pl.uid = next_plan_uid();
     pl.choice = choice;
     pl.choice_note = note;
@@ -937,7 +937,7 @@ int mpcqp_analyze_ex(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi,
                      const int32_t* Ai, int32_t eliminate, int32_t* nb, int32_t* block, int32_t* var_pad,
                      int32_t* bsize, int32_t* n_eliminated) {
     Plan pl;
-    std::string err = build_plan(n, m, Pp, Pi, Ap, Ai, pl, eliminate != 0, !eliminate && dense_w4_on());
+    std::string err = build_plan(n, m, Pp, Pi, Ap, Ai, pl, eliminate != 0, !eliminate);
     if (n_eliminated) *n_eliminated = pl.ne;
     if (!err.empty()) return fail(err.rfind("unsupported", 0) == 0 ? MPCQP_EUNSUPPORTED : MPCQP_EINVAL, "%s", err.c_str());
     if (nb) *nb = pl.nb;

@@ -37,8 +37,8 @@ std::vector<std::vector<int>> bfs_levels(const Graph& g, int s, std::vector<int>
     return levels;
 }
 
-// balanced four-block merge (build_plan's balance4: the caller's choice -- the experimental
-// builds' dense-inverse form, solve_wave.hip::dense_w4_on); MPCQP_BALANCE overrides it
+// balanced four-block merge (build_plan's balance4: the caller's choice -- api.hip asks for it on
+// every plain plan); MPCQP_BALANCE=0 / 1 overrides it
 bool balance_blocks(bool balance4) {
     static const int ov = [] {
         const char* b = getenv("MPCQP_BALANCE");  // (diagnostic override)
@@ -162,11 +162,14 @@ std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const
             blocks.push_back(L);
     }
     if (!eliminate && blocks.size() == 4 && balance_blocks(balance4)) {
-        // balanced merge for the four-wave kernel's dense-inverse form (solve_wave.hip, DK):
-        // the smallest block capacity that still merges the levels into four blocks, so that
-        // no block has more real columns than the kernel's static per-block count (cfg 2:
-        // 31 / 30 / 30 / 13 -> 27 / 26 / 26 / 25).  Levels stay whole: the blocks stay
-        // block-tridiagonal with the same coupling rows at each block's top.
+        // balanced merge: the smallest block capacity that still merges the levels into four
+        // blocks (cfg 2: 31 / 30 / 30 / 13 -> 26 / 25 / 25 / 28).  Levels stay whole: the blocks
+        // stay block-tridiagonal with the same coupling rows at each block's top.  The four-wave
+        // factorisation's stage 1 pre-pivots block 0 whole and the others past their coupling
+        // rows, one wave each, so its critical path is max(bsize_0, bsize_k - amax): 31 -> 26
+        // pivots on cfg 2 (factorisation 43.5 k -> 42.1 k cycles, the cfg-2 kernel 0.4308 ->
+        // 0.4290 ms, same-box A/B of five runs each); it also keeps every block
+        // within the dense-inverse form's static column counts (experimental build, DK).
         size_t tot = 0;
         for (auto& L : all_levels) tot += L.size();
         for (size_t cap = (tot + 3) / 4; cap < (size_t)kS; ++cap) {

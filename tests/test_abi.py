@@ -170,11 +170,13 @@ def test_plan_preview_pins_each_workloads_kernel(cfg, nb, amax_max, variant, cho
     assert pol["plan_choice"] == 0 and pol["n_eliminated"] == 0
 
 
-def test_balanced_four_block_merge_for_the_dense_form():
-    """With the four-wave kernel's dense-inverse form on (MPCQP_DENSE_W4=1 in the experimental
-    build, read once per process: a child), the planner merges cfg 2's BFS levels into four balanced blocks
-    (26 / 25 / 25 / 28 instead of 31 / 30 / 30 / 13: every block within the form's static
-    26 / 28 columns per half) that stay block-tridiagonal with the same coupling rows."""
+def test_balanced_four_block_merge():
+    """The planner merges cfg 2's BFS levels into four balanced blocks (26 / 25 / 25 / 28 instead
+    of the greedy 31 / 30 / 30 / 13: the four-wave factorisation's stage-1 critical path 31 -> 26
+    pivots, and every block within the experimental dense-inverse form's static 26 / 28 columns
+    per half) that stay block-tridiagonal with the same coupling rows -- in the production and
+    the experimental build alike; MPCQP_BALANCE=0 (read once per process: a child) restores the
+    greedy merge."""
     code = r"""
 import json, sys
 import numpy as np
@@ -197,11 +199,15 @@ print(json.dumps(dict(nb=int(nb), bsize=[int(v) for v in bsize], span=span, amax
     assert got["nb"] == 4 and got["bsize"] == [26, 25, 25, 28], got
     assert max(got["bsize"][0], got["bsize"][1]) <= 26 and max(got["bsize"][2], got["bsize"][3]) <= 28
     assert got["span"] <= 1 and got["amax"] == 5 and got["variant"] == 17, got
-    # the production library has no dense-inverse form: the switch changes nothing there
     env["MPCQP_BUILD"] = ""
+    env.pop("MPCQP_DENSE_W4")
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
     prod = json.loads(out.stdout.strip().splitlines()[-1])
-    assert prod["bsize"] == [31, 30, 30, 13], prod
+    assert prod["bsize"] == [26, 25, 25, 28] and prod["span"] <= 1 and prod["amax"] == 5, prod
+    env["MPCQP_BALANCE"] = "0"
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
+    greedy = json.loads(out.stdout.strip().splitlines()[-1])
+    assert greedy["bsize"] == [31, 30, 30, 13], greedy
 
 
 def test_cfg2_workspace_carries_no_dense_inverse_rows():
