@@ -1166,7 +1166,11 @@ __device__ __forceinline__ void form_dense_rows(__attribute__((address_space(1))
 // K: row-list length, KC: column-list length (even: the rhs splits it over the half-waves).
 // factor_only: return after the first factorisation (the setup-time convexity check of
 // api.hip::check_convex); the fused setup + solve kernel passes 0
-template <int K, int KPK, int QR, bool EL = false, int KC = K, bool DK = false>
+// RU (the stand-alone solve kernel, k_solve_w4, not the fused setup + solve): the first
+// factorisation of a solve takes setup()'s convexity factor when it is current (KParams::ffresh:
+// the factor-only launch leaves the S_k^{-1} tiles in the instance's Si region, the G blocks in H
+// and the eliminated columns' ec / ed in F); the factor-only launch (factor_only) persists them
+template <int K, int KPK, int QR, bool EL = false, int KC = K, bool DK = false, bool RU = false>
 __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restrict__ xo, double* __restrict__ yo,
                                               int factor_only = 0) {
     static_assert(!(DK && EL), "the dense inverse covers plans without eliminated columns");
@@ -1276,7 +1280,23 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
             // the slack layouts' (EL) factorisation with rotated tile rows: cfg 3
             // 43.38 -> 43.16 ms; cfg 2's build lost 1.6 % to the register assignment it moved
             // (profiles/r3s3_ab/ab_swz*.json)
-            const bool ok = factorize_nl<T4, EL>(p.self, b, rho, Sg);
+            bool ok;
+            if constexpr (RU) {
+                // the workspace factor is setup()'s (same data, rho and row classes: the same
+                // arithmetic, so the same tiles) -- used once: this solve's later factorisations,
+                // and the ones of later solves, are its own
+                if (iter == 0 && p.reuse && p.ffresh[b] == 1) {
+                    const double2* src = (const double2*)(p.Si + b * (long)p.nb * SS);
+                    for (int e = tid; e < 2 * SS; e += T4) ((double2*)Sg)[e] = src[e];
+                    ok = true;
+                } else {
+                    ok = factorize_nl<T4, EL>(p.self, b, rho, Sg);
+                }
+                __syncthreads();
+                if (tid == 0) p.ffresh[b] = 0;
+            } else {
+                ok = factorize_nl<T4, EL>(p.self, b, rho, Sg);
+            }
             if (!ok) {
                 if (iter == 0) {
                     if (xo) for (int j = tid; j < n; j += T4) opaque_ptr(xo + b * n)[j] = __builtin_nan("");
@@ -1288,7 +1308,13 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 can_check = true;
                 break;
             }
-            if (factor_only) return;
+            if (factor_only) {  // (setup()'s convexity check: its tiles for the first solve, RU)
+                __syncthreads();
+                double2* dst = (double2*)(p.Si + b * (long)p.nb * SS);
+                for (int e = tid; e < 2 * SS; e += T4) dst[e] = ((const double2*)Sg)[e];
+                if (tid == 0) p.ffresh[b] = 1;
+                return;
+            }
             __syncthreads();
             const bool have_y = iter > 0 || warm;
             {
@@ -1828,7 +1854,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
 template <int K, int KPK, int QR, bool EL = false, int KC = K, bool FO = false, bool DK = false>
 __global__ __launch_bounds__(T4, 2) void k_solve_w4(KParams p, double* __restrict__ xo, double* __restrict__ yo,
                                                     int /*factor_only: FO*/) {
-    solve_w4_body<K, KPK, QR, EL, KC, DK>(p, xo, yo, FO ? 1 : 0);
+    solve_w4_body<K, KPK, QR, EL, KC, DK, !FO && !DK>(p, xo, yo, FO ? 1 : 0);
     extern __shared__ __attribute__((aligned(16))) double sm[];
     order_epilogue<T4>(p, (int*)sm);
 }

@@ -1245,6 +1245,39 @@ def test_replan_matches_a_handle_set_up_on_the_plain_plan(monkeypatch):
     assert np.abs(ra.y - rc.y).max() <= 1e-12 * max(1.0, np.abs(rc.y).max())
 
 
+@pytest.mark.parametrize("cfg,B", [(2, 256), (3, 128)])
+def test_four_wave_factor_reuse_is_exact(monkeypatch, cfg, B):
+    """The stand-alone four-wave solve kernel (k_solve_w4, the host API's solve) starts from
+    setup()'s convexity factor -- the factor-only launch leaves its S_k^{-1} tiles in the
+    workspace -- instead of factoring again; the fused setup + solve kernel is untouched.  A handle
+    that reuses it and one that refactors (MPCQP_FACTOR_REUSE=0) agree bit for bit through solve,
+    update(q), solve, update(l, u) moving row classes, solve (cfg 2 plain, cfg 3 eliminated plan)."""
+    b = mpc.make_batch(cfg, B=B, seed=19)
+    s = dict(warm_start=True)
+    hs = []
+    for reuse in ("1", "0"):
+        monkeypatch.setenv("MPCQP_FACTOR_REUSE", reuse)
+        h = OSQPBatch()
+        h.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
+        hs.append(h)
+    monkeypatch.delenv("MPCQP_FACTOR_REUSE")
+    l3, u3 = b["l"].copy(), b["u"].copy()
+    fin = np.isfinite(l3[0]) & np.isfinite(u3[0]) & (u3[0] - l3[0] > 1e-3)
+    rows = np.flatnonzero(fin)[-4:]
+    mid = 0.5 * (l3[:, rows] + u3[:, rows])
+    l3[:, rows] = mid
+    u3[:, rows] = mid
+    for step, kw in enumerate([dict(), dict(q=b["q"] * 1.01), dict(l=l3, u=u3)]):
+        for h in hs:
+            if kw:
+                h.update(**kw)
+        r1, r0 = hs[0].solve(), hs[1].solve()
+        assert np.array_equal(r1.status_val, r0.status_val) and np.array_equal(r1.iter, r0.iter), step
+        assert np.array_equal(r1.x, r0.x) and np.array_equal(r1.y, r0.y), step
+        if step == 0:
+            assert (r1.status_val == 1).all()
+
+
 def test_handles_share_a_cached_plan_through_a_replan():
     """Handles of one sparsity pattern share the plan cache's read-only plan (api.hip::cached_plan
     hands out a shared pointer, no copy).  Re-planning one of them (update_settings(polish=True):
