@@ -1725,7 +1725,20 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 }
             }
             if (tid < npad && opaque_gptr(p.pad_var)[tid] >= 0) sm[1] = L.qv[tid + oz] * L.dx[tid + oz];
-            block_max_sum_tr<T4, 17, 2>(mx, sm, L.red);
+            if (do_rho || !unscale) {
+                block_max_sum_tr<T4, 17, 2>(mx, sm, L.red);
+            } else {
+                // a check that adapts no rho decides with the unscaled norms and the
+                // certificates' only: 10 maxima instead of 17 (R's scaled norms are then stale
+                // and unread: only a rho step restores them)
+                double m10[10] = {mx[0], mx[1], mx[2], mx[3], mx[4], mx[5], mx[6], mx[14], mx[15], mx[16]};
+                block_max_sum_tr<T4, 10, 2>(m10, sm, L.red);
+#pragma unroll
+                for (int k = 0; k < 7; ++k) mx[k] = m10[k];
+                mx[14] = m10[7];
+                mx[15] = m10[8];
+                mx[16] = m10[9];
+            }
             Res R;
             if (unscale) {
                 R.pri = mx[0]; R.dua = cscal(1) * mx[1];
