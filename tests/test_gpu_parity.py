@@ -582,6 +582,37 @@ def test_fused_dispatch_order_matches_order_kernel(monkeypatch, cfg):
     assert np.array_equal(keys["fused"][1], keys["kernel"][1])
 
 
+@pytest.mark.parametrize("cfg,B", [(2, 200), (5, 24)])
+def test_host_results_gather_matches_device_outputs(cfg, B):
+    """A host-API solve of a small batch brings everything it returns back through one gather
+    kernel into a device twin of the pinned staging layout and one copy (api.hip::
+    mpcqp_solve_batch, kernels.hip::k_gather: x, y, the info, the certificates, the statuses,
+    the polish flags as zeros).  The same batch through the device API (outputs written by the
+    solve kernel into torch tensors, no gather) agrees bit for bit on x, y, status and
+    iterations, and the info getters report the statuses and counts the kernel wrote."""
+    import torch
+    from osqp_amd import DeviceBatch
+    b = mpc.make_batch(cfg, B=B, seed=23)
+    s = {k: v for k, v in b["settings"].items() if k != "verbose"}
+    s.update(warm_start=False, polish=False)
+    h = OSQPBatch()
+    h.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
+    rh = h.solve()
+    dev = torch.device("cuda", 0)
+    X = [torch.from_numpy(np.ascontiguousarray(b[k])).to(dev) for k in ("Px", "Ax", "q", "l", "u")]
+    d = DeviceBatch(b["P"], b["A"], B, device=0, **s)
+    o = (torch.empty((B, b["n"]), dtype=torch.float64, device=dev),
+         torch.empty((B, b["m"]), dtype=torch.float64, device=dev),
+         torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev))
+    d.setup(*X)
+    d.solve(*o)
+    d.synchronize()
+    assert np.array_equal(rh.x, o[0].cpu().numpy()) and np.array_equal(rh.y, o[1].cpu().numpy())
+    assert np.array_equal(rh.status_val, o[2].cpu().numpy()) and np.array_equal(rh.iter, o[3].cpu().numpy())
+    assert (rh.status_val == 1).all() and (rh.status_polish == 0).all()
+    assert np.isfinite(rh.obj_val).all() and (rh.pri_res >= 0).all() and (rh.dua_res >= 0).all()
+
+
 def test_invalid_update_reports_zero_iterations():
     """An instance whose update() makes its bounds invalid (l > u) exits before any
     ADMM iteration: status 'non convex' with NaN outputs (osqp refuses such data) and
