@@ -827,7 +827,7 @@ __device__ __forceinline__ void twisted_solve4(const TwoSided4<SL>& R, const KPa
 #undef SPH
 }
 
-// The interface form of the two-sided solve (round 5; opt-in, MPCQP_BIG_FORM=iface).
+// The interface form of the two-sided solve (round 5; experimental build, MPCQP_BIG_FORM=iface).
 // twisted_solve runs every forward and backward step of both chains on all 512 threads, one
 // workgroup barrier a step: 2 max(p, nb-1-p) + 1 barriers, ~820 cycles a forward step on cfg
 // 5 (profiles/r4s2_phase_cfg5.txt, s.A).  But a step only carries a few rows forward: F_s
@@ -1560,8 +1560,10 @@ size_t lds_solve_bytes_big(const KParams& p) {
     return lds_solve_bytes(p) + 16 + sizeof(double) * (size_t)big_fg_len(p) + sizeof(int) * (size_t)p.nb;
 }
 
-// The interface form is opt-in (MPCQP_BIG_FORM=iface, read once per process): exact, but slower
-// than the twisted sweep on cfg 5 (38.0 against 36.2 ms per launch)
+#ifdef MPCQP_EXPERIMENTAL
+// The interface form: experimental build only, opt-in (MPCQP_BIG_FORM=iface, read once per
+// process) -- exact, but slower than the twisted sweep on cfg 5 (38.0 against
+// 36.2 ms per launch)
 static bool big_iface() {
     static const bool on = [] {
         const char* e = getenv("MPCQP_BIG_FORM");
@@ -1569,13 +1571,16 @@ static bool big_iface() {
     }();
     return on;
 }
+#endif
 
 template <int TTK, int NS, int K, int CS, int RS>
 static hipError_t go_b(const KParams& p, long B, double* xo, double* yo, int fo, hipStream_t st, KernelRef* ref) {
     const size_t lds = lds_solve_bytes_big(p);
     auto k = k_solve_b<TTK, NS, K, CS, RS>;
+#ifdef MPCQP_EXPERIMENTAL
     if constexpr (TTK == 512)
         if (big_iface() && p.ifok) k = k_solve_b<TTK, NS, K, CS, RS, true>;
+#endif
     if (ref) { *ref = {(const void*)k, TTK, lds}; return hipSuccess; }
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;

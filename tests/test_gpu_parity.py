@@ -407,12 +407,12 @@ def test_dense_inverse_form(tmp_path):
 
 def test_long_horizon_interface_form(tmp_path):
     """The long-horizon kernel's interface form of the two-sided solve (solve_big.hip::iface_solve,
-    opt-in MPCQP_BIG_FORM=iface, read once per process: the amax / bmax-row recurrences run by one
+    experimental build, MPCQP_BIG_FORM=iface, read once per process: the amax / bmax-row recurrences run by one
     wave per chain, everything else between four barriers) against the oracle on cfg 5, in a
     child process; and the same batch through the default twisted sweep agrees with it."""
     import build_cases
     s = dict(polish=False, warm_start=False)
-    got = build_cases.in_build("", [("batch", "if", 5, 64, None, s)], tmp_path / "if.npz",
+    got = build_cases.in_build("exp", [("batch", "if", 5, 64, None, s)], tmp_path / "if.npz",
                                extra_env={"MPCQP_BIG_FORM": "iface"})
     assert int(got["if_variant"]) == 12
     b = mpc.make_batch(5, B=64)
