@@ -599,18 +599,25 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
                 const int woff = PRE ? 0 : kd * S + (half ? toffL[kd] : 0);
                 const bool mid = half && kd == pm;
                 double* dst = PRE ? sm + (so[s] & 0xFFFF) + i : (mid ? corB : rb) + woff + i;
-                const double old = (writer && lowrank && !mid) ? *dst : 0.0;
+                const double old = (j0 == 4 && lowrank && !mid) ? *dst : 0.0;
                 const double* w = rb + ks * S;
                 const double v4[4] = {w[jg], w[jg + 8], w[jg + 16], w[jg + 24]};
                 const double* f = PRE ? sm + (fo[s] & 0xFFFF) + ir * FGS
                                            : (half ? Gc + (kd - pm) * bmax * FGS : Fc + (s - 1) * amax * FGS) + ir * FGS;
                 const double f4[4] = {f[jg], f[jg + 8], f[jg + 16], f[jg + 24]};
-                const double t = reduce8(dot4c(R.Inv[s - 1], v4));
-                const double c = reduce8(dot4c(f4, v4));
-                if (writer) {
-                    xt[ks * S + i] = t;
-                    if (lowrank) *dst = mid ? c : old - c;
-                }
+                // the two 8-lane sums paired: the first level (row_half_mirror, lane l with 7-l)
+                // leaves lanes 0-3 summing the S^-1 row and lanes 4-7 the F row, so each later
+                // level moves one double instead of two; lane 0 stores t and lane 4 the update,
+                // in one store instruction
+                const bool up = j0 >= 4;
+                const double tp = dot4c(R.Inv[s - 1], v4), cp = dot4c(f4, v4);
+                double x = up ? cp : tp;
+                x += dpp<0x141>(up ? tp : cp);
+                x += dpp<0xB1>(x);
+                x += dpp<0x4E>(x);
+                double* a = up ? dst : xt + ks * S + i;
+                const double val = up && !mid ? old - x : x;
+                if (writer || (j0 == 4 && lowrank)) *a = val;
             }
             __syncthreads();
         }

@@ -11,6 +11,10 @@
 //   4  LDS write -> s_barrier -> LDS read of another wave's value (the bare hand-off)
 //   5  s_barrier only
 //   6  the full step, 256 threads (one wave per SIMD)
+//   7  the full step, paired sums: the first DPP level (row_half_mirror) splits the lanes so
+//      lanes 0-3 sum the S^-1 row and lanes 4-7 the F row, and lanes 0 and 4 store in one
+//      instruction
+//   8  the full step without the stores, both sums kept live
 // Prints the median over workgroups of cycles per step.  hipcc --offload-arch=gfx950 -O3 sweep_step.hip
 #include <hip/hip_runtime.h>
 #include <algorithm>
@@ -63,11 +67,24 @@ __global__ __launch_bounds__(TT, 1) void k(long long* out, double* sink, int ite
         const double f0 = f[jg], f1 = f[jg + 8], f2 = f[jg + 16], f3 = f[jg + 24];
         double tt = (inv[0] * v0 + inv[1] * v1) + (inv[2] * v2 + inv[3] * v3);
         double c = (f0 * v0 + f1 * v1) + (f2 * v2 + f3 * v3);
+        if (MODE == 7) {
+            const bool up = jg >= 4;
+            double x = up ? c : tt;
+            x += dpp<0x141>(up ? tt : c);
+            x += dpp<0xB1>(x);
+            x += dpp<0x4E>(x);
+            const double old7 = jg == 4 ? rb[kd * 32 + i] : 0.0;
+            if ((jg & 3) == 0) rb[(up ? kd : 16) * 32 + i] = up ? old7 - 1e-9 * x : x;
+            acc += x;
+            __syncthreads();
+            continue;
+        }
         if (MODE != 1) {
             tt = reduce8(tt);
             c = reduce8(c);
         }
-        if (MODE != 3 && jg == 0) {
+        if (MODE == 8) acc += c;
+        if (MODE != 3 && MODE != 8 && jg == 0) {
             rb[32 * 16 + i] = tt;  // (the t row: a block no step reads)
             rb[kd * 32 + i] = old - 1e-9 * c;
         }
@@ -114,5 +131,7 @@ int main() {
     run<4, 512>("4 write -> s_barrier -> read", nblk, iters);
     run<5, 512>("5 s_barrier only", nblk, iters);
     run<6 == 6 ? 0 : 0, 256>("6 full step, 256 threads", nblk, iters);
+    run<7, 512>("7 paired sums, one store instruction", nblk, iters);
+    run<8, 512>("8 without the stores, sums live", nblk, iters);
     return 0;
 }
