@@ -609,15 +609,19 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
                 // leaves lanes 0-3 summing the S^-1 row and lanes 4-7 the F row, so each later
                 // level moves one double instead of two; lane 0 stores t and lane 4 the update,
                 // in one store instruction
-                const bool up = j0 >= 4;
+                const bool up = j0 >= 4, sub = up && !mid;
+                // the store's address and its value as one fma (sg x + o: t, the update
+                // old - c, or the middle block's c) settled before the sums
+                __attribute__((address_space(3))) double* a =
+                    (__attribute__((address_space(3))) double*)(up ? dst : xt + ks * S + i);
+                double sg = sub ? -1.0 : 1.0, o = sub ? old : 0.0;
+                asm volatile("" : "+v"(a), "+v"(sg), "+v"(o));
                 const double tp = dot4c(R.Inv[s - 1], v4), cp = dot4c(f4, v4);
                 double x = up ? cp : tp;
                 x += dpp<0x141>(up ? tp : cp);
                 x += dpp<0xB1>(x);
                 x += dpp<0x4E>(x);
-                double* a = up ? dst : xt + ks * S + i;
-                const double val = up && !mid ? old - x : x;
-                if (writer || (j0 == 4 && lowrank)) *a = val;
+                if (writer || (j0 == 4 && lowrank)) *a = __builtin_fma(sg, x, o);
             }
             __syncthreads();
         }
