@@ -620,8 +620,12 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
                 double x = up ? cp : tp;
                 x += dpp<0x141>(up ? tp : cp);
                 x += dpp<0xB1>(x);
-                x += dpp<0x4E>(x);
-                if (writer || (j0 == 4 && lowrank)) *a = __builtin_fma(sg, x, o);
+                // the last level's add folded into the store's fma: sg (x + y) + o as
+                // sg y + (sg x + o), the inner fma taken while y moves
+                double pre = __builtin_fma(sg, x, o);
+                asm volatile("" : "+v"(pre));  // (kept out of the store's branch)
+                const double y = dpp<0x4E>(x);
+                if (writer || (j0 == 4 && lowrank)) *a = __builtin_fma(sg, y, pre);
             }
             __syncthreads();
         }
@@ -660,12 +664,20 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
                 const double h0 = h[r0 * FGS], h1 = h[r1 * FGS], x0 = x1[r0], x8 = x1[r1];
                 const double a0 = j0 < lim ? h0 * x0 : 0.0;
                 const double a1 = j0 + 8 < lim ? h1 * x8 : 0.0;
-                const double c = reduce8(a0 + a1);
+                double c = a0 + a1;
+                c += dpp<0xB1>(c);
+                c += dpp<0x4E>(c);
                 // t_k used by every lane here (an empty asm), so its read stays with the step's
                 // other reads: the compiler had sunk it into the writer's branch, behind the
-                // reduction -- an LDS round trip on every backward step's critical path
+                // reduction -- an LDS round trip on every backward step's critical path.  The
+                // last level's add folded into the update: (t_k - c) - y, the first
+                // subtraction taken while y moves
                 asm volatile("" ::"v"(tk));
-                if (writer) xt[k * S + i] = tk - c;
+                double pre = tk - c;
+                int jo = j0;
+                asm volatile("" : "+v"(pre), "+v"(jo));  // (pre kept out of the branch; the writer test a compare, not a spilled mask)
+                const double y = dpp<0x141>(c);
+                if (jo == 0) xt[k * S + i] = pre - y;
             }
             __syncthreads();
         }
