@@ -585,8 +585,13 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
     const int tid = threadIdx.x, half = __builtin_amdgcn_readfirstlane(tid >> 8), u = tid & 255, i = u >> 3,
               jg = (u & 7) + opq, j0 = u & 7;
     const int nb = p.nb, pm = p.pmeet, amax = p.amax, bmax = p.bmax, nbot = nb - 1 - pm;
-    const int nst = nbot > pm ? nbot : pm;
-    const int nmine = half ? nbot : pm, lim = half ? bmax : amax;
+    int nst = nbot > pm ? nbot : pm, nmine = half ? nbot : pm;
+    // (through an empty asm each call: the steps' tests against them stay scalar compares in
+    // the loop -- hoisted out of the ADMM loop they were 64-bit masks spilled to VGPR lanes,
+    // read back with v_readlane on every step)
+    int nbo = nb;
+    asm volatile("" : "+s"(nst), "+s"(nmine), "+s"(nbo));
+    const int lim = half ? bmax : amax;
     const bool writer = j0 == 0, lowrank = i < lim;
     const int ir = lowrank ? i : 0;  // F / G row this thread sums (row 0 for the rest: reads stay in range)
     // forward: top step s: t_{s-1} = S_{s-1}^{-1} w_{s-1}, w_s -= F_s w_{s-1};
@@ -595,11 +600,11 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
     for (int s = 1; s < SL; ++s) {
         if (s <= nst) {
             if (s <= nmine) {
-                const int ks = half ? nb - s : s - 1, kd = half ? nb - 1 - s : s;
+                const int ks = half ? nbo - s : s - 1, kd = half ? nb - 1 - s : s;
                 const int woff = PRE ? 0 : kd * S + (half ? toffL[kd] : 0);
-                const bool mid = half && kd == pm;
+                const bool mid = half && s == nmine;  // (kd == pm: the bottom chain's last step)
                 double* dst = PRE ? sm + (so[s] & 0xFFFF) + i : (mid ? corB : rb) + woff + i;
-                const double old = (j0 == 4 && lowrank && !mid) ? *dst : 0.0;
+                const double old = *dst;  // (every lane: an unconditional read, the unused ones ignored)
                 const double* w = rb + ks * S;
                 const double v4[4] = {w[jg], w[jg + 8], w[jg + 16], w[jg + 24]};
                 const double* f = PRE ? sm + (fo[s] & 0xFFFF) + ir * FGS
