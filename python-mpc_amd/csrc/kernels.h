@@ -62,6 +62,8 @@ struct KParams {
     // by an update that moves a row's class, by a rho set through update_settings and by polish
     int* ffresh;
     int reuse;  // k_solve_b may start from a fresh workspace factor (MPCQP_FACTOR_REUSE=0: never, A/B)
+    int apart;  // k_solve_b's bottom chain may update the middle block in place (solve_big.hip::middle_apart;
+                // MPCQP_MIDDLE_APART=0: never, A/B)
     int *ostat, *oiter;  // per-call copies of status / iter (mpcqp_solve_device's outputs), or null
     const struct KParams* self;  // device copy of this block (read by the out-of-line device functions)
     long long* prof;  // optional per-instance phase timers (MPCQP_PHASE_PROF=1), kProfSlots each

@@ -540,6 +540,14 @@ __device__ __forceinline__ double dot4c(const double (&a)[4], const double (&v)[
 //   so: bits 0-15 the forward step's destination row (rb or corB, + kd S + toff), bits 16-31
 //       the backward step's x_{k+-1} (xt + ...);  fo: the F / G rows of the forward step,
 //       bits 16-31 the backward step's H rows.
+// The bottom chain's update of the middle block touches rows [toff_p, toff_p + bmax), the top
+// chain's rows [0, amax): when those are disjoint (toff_p >= amax: the middle block's first and
+// last BFS levels apart, every long-horizon workload here) the bottom chain updates rb in place
+// like every other step, and the middle step reads w_p alone (no corB reads or subtraction).
+__device__ __forceinline__ int middle_apart(const KParams& p, const int* toffL) {
+    return p.apart && p.pmeet < p.nb - 1 && toffL[p.pmeet] >= p.amax;
+}
+
 template <int SL, int TT = 512>
 __device__ __forceinline__ void step_offsets(const KParams& p, const int* toffL, const double* rb, const double* xt,
                                              const double* corB, const double* Fc, int (&so)[SL], int (&fo)[SL]) {
@@ -548,18 +556,19 @@ __device__ __forceinline__ void step_offsets(const KParams& p, const int* toffL,
     const int nb = p.nb, pm = p.pmeet, nmine = half ? nb - 1 - pm : pm;
     const int amax = p.amax, bmax = p.bmax, g0 = pm * amax;  // (Gc = Fc + g0 FGS)
     const int orb = (int)(rb - sm), oxt = (int)(xt - sm), ocb = (int)(corB - sm), ofc = (int)(Fc - sm);
+    const int apart = middle_apart(p, toffL);
 #pragma unroll
     for (int s = 0; s < SL; ++s) {
         int f = 0, bk = 0, ff = 0, fb = 0;
         if (s >= 1 && s <= nmine) {
             const int kd = half ? nb - 1 - s : s;
-            f = (half && kd == pm ? ocb : orb) + kd * S + (half ? toffL[kd] : 0);
+            f = (half && kd == pm && !apart ? ocb : orb) + kd * S + (half ? toffL[kd] : 0);
             const int k = half ? pm + s : pm - s;
             bk = oxt + (half ? (k - 1) * S + toffL[k - 1] : (k + 1) * S);
             ff = ofc + (half ? g0 + (kd - pm) * bmax : (s - 1) * amax) * FGS;
             fb = ofc + (half ? g0 + (k - 1 - pm) * bmax : k * amax) * FGS;
         }
-        so[s] = f | (bk << 16);
+        so[s] = s == 0 ? apart : f | (bk << 16);  // (so[0]: no step; it carries middle_apart)
         fo[s] = ff | (fb << 16);
         asm volatile("" : "+v"(so[s]), "+v"(fo[s]));  // (in VGPRs: the kernel's scalar registers are spoken for)
     }
@@ -589,8 +598,8 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
     // (through an empty asm each call: the steps' tests against them stay scalar compares in
     // the loop -- hoisted out of the ADMM loop they were 64-bit masks spilled to VGPR lanes,
     // read back with v_readlane on every step)
-    int nbo = nb;
-    asm volatile("" : "+s"(nst), "+s"(nmine), "+s"(nbo));
+    int nbo = nb, apart = __builtin_amdgcn_readfirstlane(PRE ? so[0] : middle_apart(p, toffL));
+    asm volatile("" : "+s"(nst), "+s"(nmine), "+s"(nbo), "+s"(apart));
     const int lim = half ? bmax : amax;
     const bool writer = j0 == 0, lowrank = i < lim;
     const int ir = lowrank ? i : 0;  // F / G row this thread sums (row 0 for the rest: reads stay in range)
@@ -602,7 +611,7 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
             if (s <= nmine) {
                 const int ks = half ? nbo - s : s - 1, kd = half ? nb - 1 - s : s;
                 const int woff = PRE ? 0 : kd * S + (half ? toffL[kd] : 0);
-                const bool mid = half && s == nmine;  // (kd == pm: the bottom chain's last step)
+                const bool mid = half && s == nmine && !apart;  // (kd == pm: the bottom chain's last step)
                 double* dst = PRE ? sm + (so[s] & 0xFFFF) + i : (mid ? corB : rb) + woff + i;
                 const double old = *dst;  // (every lane: an unconditional read, the unused ones ignored)
                 const double* w = rb + ks * S;
@@ -641,8 +650,13 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
         const double* w = rb + pm * S;
         const double* cb = corB + pm * S;
         double v4[4];
+        if (apart) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) v4[c] = w[jg + 8 * c] - cb[jg + 8 * c];
+            for (int c = 0; c < 4; ++c) v4[c] = w[jg + 8 * c];
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v4[c] = w[jg + 8 * c] - cb[jg + 8 * c];
+        }
 #pragma unroll
         for (int s = 0; s < SL; ++s) {
             if (s == pm) {
@@ -764,6 +778,7 @@ __device__ __forceinline__ void twisted_solve4(const TwoSided4<SL>& R, const KPa
     const int nb = p.nb, pm = p.pmeet, amax = p.amax, bmax = p.bmax, nbot = nb - 1 - pm;
     const int nst = nbot > pm ? nbot : pm;
     const int nmine = half ? nbot : pm, lim = half ? bmax : amax;
+    const int apart = __builtin_amdgcn_readfirstlane(PRE ? so[0] : middle_apart(p, toffL));
     const bool writer = q == 0, lowrank = i < lim;
     const int ir = lowrank ? i : 0;  // F / G row this thread sums (row 0 for the rest: reads stay in range)
     auto ld8 = [](const double* a, double (&v)[8]) __attribute__((always_inline)) {
@@ -782,7 +797,7 @@ __device__ __forceinline__ void twisted_solve4(const TwoSided4<SL>& R, const KPa
             if (s <= nmine) {
                 const int ks = half ? nb - s : s - 1, kd = half ? nb - 1 - s : s;
                 const int woff = PRE ? 0 : kd * S + (half ? toffL[kd] : 0);
-                const bool mid = half && kd == pm;
+                const bool mid = half && kd == pm && !apart;
                 double* dst = PRE ? sm + (so[s] & 0xFFFF) + i : (mid ? corB : rb) + woff + i;
                 const double old = (writer && lowrank && !mid) ? *dst : 0.0;
                 double v8[8], f8[8];
@@ -1448,7 +1463,11 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
         __syncthreads();
         PH(5)
         const double r_hi = RHO_EQ_OVER_RHO_INEQ * rho;
-        const double ri_lo = 1.0 / RHO_MIN, ri_mid = 1.0 / rho, ri_hi = 1.0 / r_hi;
+        double ri_lo = 1.0 / RHO_MIN, ri_mid = 1.0 / rho, ri_hi = 1.0 / r_hi;
+        // (through an empty asm: seen as reciprocals, the row update's select among them was
+        // folded into one division of the selected rho -- a full f64 division per row per
+        // iteration inside the loop)
+        asm volatile("" : "+v"(ri_mid), "+v"(ri_hi));
         while (iter < stop_at) {
             ++iter;
             int opq = 0;

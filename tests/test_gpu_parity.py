@@ -1411,3 +1411,50 @@ def test_long_horizon_factor_reuse_is_exact(monkeypatch):
         same = r1.iter == it
         du = np.array([np.abs(r1.x[k, b["u_block"]] - ro[k].x[b["u_block"]]).max() for k in range(len(ro))])
         assert np.all(du[same] < U_TOL), (step, du[same].max())
+
+
+@pytest.mark.gpu
+def test_long_horizon_middle_block_in_place(monkeypatch):
+    """solve_big.hip::middle_apart: when the middle block's rows the top chain updates [0, amax)
+    and the rows the bottom chain updates [toff_p, toff_p + bmax) are disjoint (cfg 5: rows 0-9
+    and 20-29), the bottom chain writes (old - x) - y into rb in place (x, y: the last DPP
+    level's two halves) and the middle step reads w_p alone; otherwise (MPCQP_MIDDLE_APART=0
+    forces it) the bottom chain's x + y goes to corB and the middle step forms w_p - corB --
+    the same update, rounded differently.  Both handles against the oracle doing the same
+    calls (a cold solve, then a warm-started one after an update of q): statuses equal,
+    iteration counts for >= 7/8 of the instances, and where they agree, the inputs within
+    U_TOL; the two handles' iteration counts agree with each other as well."""
+    b = mpc.make_batch(5, B=8, seed=23)
+    s = dict(warm_start=True, polish=False)
+    P, A = b["P"], b["A"]
+    handles = []
+    for apart in ("1", "0"):
+        monkeypatch.setenv("MPCQP_MIDDLE_APART", apart)
+        h = OSQPBatch()
+        h.setup(P, b["q"], A, b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
+        handles.append(h)
+    monkeypatch.delenv("MPCQP_MIDDLE_APART")
+    orc = []
+    for k in range(b["Px"].shape[0]):
+        o = pyoracle.OSQP()
+        Pk, Ak = P.copy(), A.copy()
+        Pk.data, Ak.data = b["Px"][k].copy(), b["Ax"][k].copy()
+        o.setup(Pk, b["q"][k], Ak, b["l"][k], b["u"][k], **s)
+        orc.append(o)
+    for step in range(2):
+        if step:
+            for h in handles:
+                h.update(q=b["q"] * 0.97)
+            for k, o in enumerate(orc):
+                o.update(q=b["q"][k] * 0.97)
+        ro = [o.solve() for o in orc]
+        it = np.array([r.info.iter for r in ro])
+        st = np.array([r.info.status_val for r in ro])
+        res = [h.solve() for h in handles]
+        assert np.mean(res[0].iter == res[1].iter) >= 7 / 8, (step, res[0].iter, res[1].iter)
+        for r in res:
+            assert np.array_equal(r.status_val, st), (step, r.status_val, st)
+            assert np.mean(r.iter == it) >= 7 / 8, (step, r.iter, it)
+            same = r.iter == it
+            du = np.array([np.abs(r.x[k, b["u_block"]] - ro[k].x[b["u_block"]]).max() for k in range(len(ro))])
+            assert np.all(du[same] < U_TOL), (step, du[same].max())
