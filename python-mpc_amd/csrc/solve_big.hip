@@ -492,9 +492,11 @@ __device__ __noinline__ bool factorize2_nl(const KP* gp, long b, double rho, dou
 template <int SL>
 struct TwoSided {
     double Inv[SL][4];
+    // frows: also copy the F / G rows into LDS (after a factorisation, which uses that region as
+    // scratch; a termination check leaves it alone, so a run start after one need not)
     __device__ __forceinline__ void load(int nb, int pm, int amax, int bmax, const double* __restrict__ Fg,
                                          const double* __restrict__ Hg, const double* __restrict__ Sg,
-                                         double* __restrict__ Fc, double* __restrict__ Gc) {
+                                         double* __restrict__ Fc, double* __restrict__ Gc, bool frows) {
         const int tid = threadIdx.x, half = __builtin_amdgcn_readfirstlane(tid >> 8), u = tid & 255, i = u >> 3,
                   jg = u & 7;
         const int nbot = nb - 1 - pm;
@@ -505,6 +507,7 @@ struct TwoSided {
 #pragma unroll
             for (int c = 0; c < 4; ++c) Inv[s][c] = have ? Sg[(long)k * SS + i * S + jg + 8 * c] : 0.0;
         }
+        if (!frows) return;
         for (int o = tid; o < pm * amax * S; o += TB) {  // row q = k amax + r of F_{k+1}
             const int q = o >> 5, j = o & (S - 1), k = q / amax, r = q - k * amax;
             Fc[q * FGS + j] = Fg[(long)(k + 1) * SS + r * S + j];
@@ -1419,7 +1422,7 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
         std::conditional_t<IF, TwoSidedQ<NS + 1>,
                            std::conditional_t<TTK == 512, TwoSided<NS + 1>,
                                               std::conditional_t<TTK == 256, TwoSided4<NS + 1>, TwoSidedW<NS>>>> RF;
-        if constexpr (IF) {
+        if constexpr (IF || TTK == 512) {
             RF.load(nb, p.pmeet, amax, p.bmax, Fg, Hg, Sg, Fc, Gc, frows);
             frows = false;
         } else {
