@@ -485,7 +485,7 @@ __device__ __noinline__ bool factorize2_nl(const KP* gp, long b, double rho, dou
 // The factor on chip for the two-sided sweep.  Thread t: half h = t / 256 (0 top,
 // 1 bottom), (i, jg) = (t % 256 / 8, t % 8): row i of a tile is summed by one 8-lane
 // DPP half-row, lane jg holding columns jg + 8c.
-//   top    Inv[s] = S_s^{-1} (s < p), M^{-1} (s = p)      (registers)
+//   top    Inv[s] = S_s^{-1} (s < p), M^{-1} (s = SL-1)   (registers)
 //   bottom Inv[s] = T_{nb-1-s}^{-1}                       (registers)
 //   F_k rows (k = 1..p) and G_k tail rows (k = p..nb-2)  (LDS; the backward sweep
 //   reads them transposed: H_k = F_{k+1}', T_k^{-1} E_k = G_{k-1}')
@@ -502,8 +502,10 @@ struct TwoSided {
         const int nbot = nb - 1 - pm;
 #pragma unroll
         for (int s = 0; s < SL; ++s) {
-            const bool have = half == 0 ? s <= pm : s < nbot;
-            const int k = half == 0 ? s : nb - 1 - s;
+            // top: S_s^{-1} in slot s < p, M^{-1} in the last slot (the middle step's operand at a
+            // fixed place, not picked by p at run time); bottom: T_{nb-1-s}^{-1} in slot s < nb-1-p
+            const bool have = half == 0 ? (s < pm || s == SL - 1) : s < nbot;
+            const int k = half == 0 ? (s == SL - 1 ? pm : s) : nb - 1 - s;
 #pragma unroll
             for (int c = 0; c < 4; ++c) Inv[s][c] = have ? Sg[(long)k * SS + i * S + jg + 8 * c] : 0.0;
         }
@@ -660,13 +662,8 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
 #pragma unroll
             for (int c = 0; c < 4; ++c) v4[c] = w[jg + 8 * c] - cb[jg + 8 * c];
         }
-#pragma unroll
-        for (int s = 0; s < SL; ++s) {
-            if (s == pm) {
-                const double t = reduce8(dot4c(R.Inv[s], v4));
-                if (writer) xt[pm * S + i] = t;
-            }
-        }
+        const double t = reduce8(dot4c(R.Inv[SL - 1], v4));  // (M^{-1}: TwoSided::load's last slot)
+        if (writer) xt[pm * S + i] = t;
     }
     __syncthreads();
     SPH(13)
