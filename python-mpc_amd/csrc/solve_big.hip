@@ -521,6 +521,9 @@ struct TwoSided {
     }
 };
 
+__device__ __forceinline__ double dot4f(const double (&a)[4], const double (&v)[4]) {  // one mul, three fma
+    return __builtin_fma(a[3], v[3], __builtin_fma(a[2], v[2], __builtin_fma(a[1], v[1], a[0] * v[0])));
+}
 __device__ __forceinline__ double dot4c(const double (&a)[4], const double (&v)[4]) {
     return (a[0] * v[0] + a[1] * v[1]) + (a[2] * v[2] + a[3] * v[3]);
 }
@@ -628,14 +631,16 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
                 // leaves lanes 0-3 summing the S^-1 row and lanes 4-7 the F row, so each later
                 // level moves one double instead of two; lane 0 stores t and lane 4 the update,
                 // in one store instruction
-                const bool up = j0 >= 4, sub = up && !mid;
+                int jo = j0;
+                asm volatile("" : "+v"(jo));  // (the half-row split as a compare, not a spilled mask)
+                const bool up = jo >= 4, sub = up && !mid;
                 // the store's address and its value as one fma (sg x + o: t, the update
                 // old - c, or the middle block's c) settled before the sums
                 __attribute__((address_space(3))) double* a =
                     (__attribute__((address_space(3))) double*)(up ? dst : xt + ks * S + i);
                 double sg = sub ? -1.0 : 1.0, o = sub ? old : 0.0;
                 asm volatile("" : "+v"(a), "+v"(sg), "+v"(o));
-                const double tp = dot4c(R.Inv[s - 1], v4), cp = dot4c(f4, v4);
+                const double tp = dot4f(R.Inv[s - 1], v4), cp = dot4f(f4, v4);
                 double x = up ? cp : tp;
                 x += dpp<0x141>(up ? tp : cp);
                 x += dpp<0xB1>(x);
