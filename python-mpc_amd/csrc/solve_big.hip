@@ -1424,12 +1424,6 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
         std::conditional_t<IF, TwoSidedQ<NS + 1>,
                            std::conditional_t<TTK == 512, TwoSided<NS + 1>,
                                               std::conditional_t<TTK == 256, TwoSided4<NS + 1>, TwoSidedW<NS>>>> RF;
-        if constexpr (IF || TTK == 512) {
-            RF.load(nb, p.pmeet, amax, p.bmax, Fg, Hg, Sg, Fc, Gc, frows);
-            frows = false;
-        } else {
-            RF.load(nb, p.pmeet, amax, p.bmax, Fg, Hg, Sg, Fc, Gc);
-        }
         int so[NS + 1], fo[NS + 1];  // (TTK == 512, NS < 10: twisted_solve's step offsets)
         // the interface form: toff[lane] in one VGPR (iface_solve::toff_of)
         int tvl = 0;
@@ -1443,12 +1437,16 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
         // gather lists as LDS-base offsets (GatherR): A' w for the rhs, A x~ for the rows
         extern __shared__ __attribute__((aligned(16))) double smb[];
         const unsigned oA = (unsigned)(L.Acsc - smb), oW = (unsigned)(L.w - smb), oXt = (unsigned)(L.xt - smb);
+        // the list strides from the kernel arguments through an empty asm per run (not a load of
+        // p.self's copy in front of the list loads; not hoisted out of the run loop either)
+        int stc = npad, str = m;
+        asm volatile("" : "+s"(stc), "+s"(str));
         GatherR<K> cg[CS];
 #pragma unroll
         for (int s = 0; s < CS; ++s) {
             const int pc = tid + s * TTK;
             cvar[s] = pc < npad ? p.pad_var[pc] : -1;
-            if (pc < npad) cg[s].load(p.gcol + pc, &p.self->npad, oA, oW);
+            if (pc < npad) cg[s].load(p.gcol + pc, stc, oA, oW);
             else cg[s].clear(nnzA, oA, oW);
         }
         GatherR<K> rg[RS];
@@ -1456,11 +1454,19 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
         for (int s = 0; s < RS; ++s) {
             const int i = tid + s * TTK;
             if (i < m) {
-                rg[s].load(p.grow + i, &p.self->m, oA, oXt);
+                rg[s].load(p.grow + i, str, oA, oXt);
                 L.w[i] = rho_of(L.ct[i], rho) * Z[i] - y[s];  // w = rho z_prev - y (rho may be new)
             } else {
                 rg[s].clear(nnzA, oA, oXt);
             }
+        }
+        // the factor last: global loads return in order, so the rhs phase waits for the lists
+        // alone and the factor's loads stay in flight under it (the sweep is their first use)
+        if constexpr (IF || TTK == 512) {
+            RF.load(nb, p.pmeet, amax, p.bmax, Fg, Hg, Sg, Fc, Gc, frows);
+            frows = false;
+        } else {
+            RF.load(nb, p.pmeet, amax, p.bmax, Fg, Hg, Sg, Fc, Gc);
         }
         int stop_at = p.max_iter;
         if (p.check_term) stop_at = min(stop_at, (iter / p.check_term + 1) * p.check_term);

@@ -1075,6 +1075,11 @@ struct GatherR {
 #pragma unroll
         for (int k = 0; k < K; ++k) e[k] = (unsigned)list[k * st] + o;
     }
+    __device__ __forceinline__ void load(const int* list, int st, unsigned oA, unsigned oV) {
+        const unsigned o = oA + (oV << 16);
+#pragma unroll
+        for (int k = 0; k < K; ++k) e[k] = (unsigned)list[k * st] + o;
+    }
     __device__ __forceinline__ void clear(int zero_pos, unsigned oA, unsigned oV) {
 #pragma unroll
         for (int k = 0; k < K; ++k) e[k] = (unsigned)zero_pos + oA + (oV << 16);
