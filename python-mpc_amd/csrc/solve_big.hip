@@ -524,6 +524,9 @@ struct TwoSided {
 __device__ __forceinline__ double dot4f(const double (&a)[4], const double (&v)[4]) {  // one mul, three fma
     return __builtin_fma(a[3], v[3], __builtin_fma(a[2], v[2], __builtin_fma(a[1], v[1], a[0] * v[0])));
 }
+__device__ __forceinline__ double dot4fn(const double (&a)[4], const double (&v)[4]) {  // -dot4f, exactly
+    return __builtin_fma(-a[3], v[3], __builtin_fma(-a[2], v[2], __builtin_fma(-a[1], v[1], -a[0] * v[0])));
+}
 __device__ __forceinline__ double dot4c(const double (&a)[4], const double (&v)[4]) {
     return (a[0] * v[0] + a[1] * v[1]) + (a[2] * v[2] + a[3] * v[3]);
 }
@@ -531,7 +534,7 @@ __device__ __forceinline__ double dot4c(const double (&a)[4], const double (&v)[
 // xt = K^{-1} rb.  The forward sweeps' low-rank updates go into rb in place (the
 // writer lane of a row reads the old value at the start of the step, off the critical
 // path), except the bottom chain's update of the middle block, which the top chain
-// updates too: it goes to corB[p][toff_p + a] (a < bmax), zero everywhere else (cleared
+// updates too: it goes (negated) to corB[p][toff_p + a] (a < bmax), zero everywhere else (cleared
 // once per solve, the same entries rewritten every iteration).  A step reads only its
 // block of rb and the F / G row (8 LDS reads per lane, 16 before), sums two 8-lane DPP
 // dot products side by side.  Both halves run the same instruction stream with per-half
@@ -634,22 +637,25 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
                 int jo = j0;
                 asm volatile("" : "+v"(jo));  // (the half-row split as a compare, not a spilled mask)
                 const bool up = jo >= 4, sub = up && !mid;
-                // the store's address and its value as one fma (sg x + o: t, the update
-                // old - c, or the middle block's c) settled before the sums
+                // the store's address and the value it adds to (o: the old value of an update,
+                // 0 for t and for the middle block's correction) settled before the sums.  The
+                // F row's products are summed negated (-c: the sign folded into the fma
+                // operands, exact), so every store is o + sum -- t, old - c, or -c into corB
+                // (the middle step adds it)
                 __attribute__((address_space(3))) double* a =
                     (__attribute__((address_space(3))) double*)(up ? dst : xt + ks * S + i);
-                double sg = sub ? -1.0 : 1.0, o = sub ? old : 0.0;
-                asm volatile("" : "+v"(a), "+v"(sg), "+v"(o));
-                const double tp = dot4f(R.Inv[s - 1], v4), cp = dot4f(f4, v4);
+                double o = sub ? old : 0.0;
+                asm volatile("" : "+v"(a), "+v"(o));
+                const double tp = dot4f(R.Inv[s - 1], v4), cp = dot4fn(f4, v4);
                 double x = up ? cp : tp;
                 x += dpp<0x141>(up ? tp : cp);
                 x += dpp<0xB1>(x);
-                // the last level's add folded into the store's fma: sg (x + y) + o as
-                // sg y + (sg x + o), the inner fma taken while y moves
-                double pre = __builtin_fma(sg, x, o);
+                // the last level's add folded into the store: o + (x + y) as (o + x) + y, the
+                // first add taken while y moves
+                double pre = o + x;
                 asm volatile("" : "+v"(pre));  // (kept out of the store's branch)
                 const double y = dpp<0x4E>(x);
-                if (writer || (j0 == 4 && lowrank)) *a = __builtin_fma(sg, y, pre);
+                if (writer || (j0 == 4 && lowrank)) *a = pre + y;
             }
             __syncthreads();
         }
@@ -663,9 +669,9 @@ __device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KPara
         if (apart) {
 #pragma unroll
             for (int c = 0; c < 4; ++c) v4[c] = w[jg + 8 * c];
-        } else {
+        } else {  // (corB holds -c: twisted_solve's forward step)
 #pragma unroll
-            for (int c = 0; c < 4; ++c) v4[c] = w[jg + 8 * c] - cb[jg + 8 * c];
+            for (int c = 0; c < 4; ++c) v4[c] = w[jg + 8 * c] + cb[jg + 8 * c];
         }
         const double t = reduce8(dot4c(R.Inv[SL - 1], v4));  // (M^{-1}: TwoSided::load's last slot)
         if (writer) xt[pm * S + i] = t;
