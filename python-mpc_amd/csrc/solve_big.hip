@@ -475,11 +475,17 @@ template <int TT, class KP>
 __device__ __noinline__ bool factorize2_nl(const KP* gp, long b, double rho, double* X2) {
     const KPc& p = kconst(gp);
     SL2 C = carve(p);
+    bool ok;
     if constexpr (TT >= 256)  // (the two-wave variant 14 keeps the unsplit form)
-        return factorize2s<TT>(p, C.L, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
-                               p.Si + b * (long)p.nb * SS);
-    return factorize2<TT>(p, C.L, X2, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
-                          p.Si + b * (long)p.nb * SS);
+        ok = factorize2s<TT>(p, C.L, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
+                             p.Si + b * (long)p.nb * SS);
+    else
+        ok = factorize2<TT>(p, C.L, X2, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
+                            p.Si + b * (long)p.nb * SS);
+    // the rho the workspace factor belongs to (scal[3]), beside it: a solve reuses the factor only
+    // when it is also the instance's current rho (scal[2]), whatever cleared or forgot ffresh
+    if (threadIdx.x == 0) p.scal[b * 4 + 3] = ok ? rho : -1.0;
+    return ok;
 }
 
 // The factor on chip for the two-sided sweep.  Thread t: half h = t / 256 (0 top,
@@ -1390,7 +1396,7 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
     // the workspace factor is the current one (KParams::ffresh: this instance's convexity check
     // at setup, or its previous solve, factored K at this rho and these row classes): start
     // without refactoring -- the single-QP path's setup() + solve() factored twice before
-    const bool fresh = p.reuse && p.ffresh[b] == 1;
+    const bool fresh = p.reuse && p.ffresh[b] == 1 && p.scal[b * 4 + 3] == rho;
     if (fresh && factor_only) return;
     bool can_check = false, need_factor = !fresh;
     bool frows = true;  // the F / G rows must be (re)loaded into LDS at the next run start
@@ -1591,8 +1597,10 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
     }
     finalize_nl<TTK>(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates, p.ostat, p.oiter);
     // the workspace now holds the factor of the final rho (the next solve's): fresh unless the
-    // last factorisation failed
-    if (tid == 0) p.ffresh[b] = status == MPCQP_NON_CVX_ ? 0 : 1;
+    // last factorisation failed, or a rho step at the last iteration (max_iter a multiple of the
+    // rho interval) left the refactorisation it asked for undone -- finalize_nl stores that new
+    // rho, while F / H / Si still hold the old one's factor (OSQP 0.6 refactors inside adapt_rho)
+    if (tid == 0) p.ffresh[b] = (status == MPCQP_NON_CVX_ || need_factor) ? 0 : 1;
 #ifdef MPCQP_PHASE_PROF
     if (prof) {
         __syncthreads();

@@ -1285,7 +1285,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 // the workspace factor is setup()'s (same data, rho and row classes: the same
                 // arithmetic, so the same tiles) -- used once: this solve's later factorisations,
                 // and the ones of later solves, are its own
-                if (iter == 0 && p.reuse && p.ffresh[b] == 1) {
+                if (iter == 0 && p.reuse && p.ffresh[b] == 1 && p.scal[b * 4 + 3] == rho) {
                     const double2* src = (const double2*)(p.Si + b * (long)p.nb * SS);
                     for (int e = tid; e < 2 * SS; e += T4) ((double2*)Sg)[e] = src[e];
                     ok = true;
@@ -1312,7 +1312,10 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 __syncthreads();
                 double2* dst = (double2*)(p.Si + b * (long)p.nb * SS);
                 for (int e = tid; e < 2 * SS; e += T4) dst[e] = ((const double2*)Sg)[e];
-                if (tid == 0) p.ffresh[b] = 1;
+                if (tid == 0) {
+                    p.ffresh[b] = 1;
+                    p.scal[b * 4 + 3] = rho;  // the factor's rho (the RU solve checks it against scal[2])
+                }
                 return;
             }
             __syncthreads();

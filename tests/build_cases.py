@@ -70,7 +70,7 @@ def run_batch(name, cfg, B, variant, settings):
     h.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **settings)
     r = h.solve()
     info = h.plan_info()
-    return {f"{name}_x": r.x, f"{name}_iter": r.iter, f"{name}_status_val": r.status_val,
+    return {f"{name}_x": r.x, f"{name}_y": r.y, f"{name}_iter": r.iter, f"{name}_status_val": r.status_val,
             f"{name}_variant": np.int32(info["variant"])}
 
 

@@ -9,7 +9,7 @@ import pytest
 import scipy.sparse as sparse
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for p in (os.path.join(ROOT, "python-mpc_amd"), os.path.join(ROOT, "oracle"), ROOT):
+for p in (os.path.join(ROOT, "python-mpc_amd"), os.path.join(ROOT, "oracle"), ROOT, os.path.join(ROOT, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)
 
@@ -18,6 +18,18 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a HIP device (MI355X); run via gpurun")
+
+
+def pytest_terminal_summary(terminalreporter):
+    """The agreement fractions every device-vs-oracle batch check observed (tests/parity.py)."""
+    import parity
+    if not parity.RECORDS:
+        return
+    terminalreporter.section("parity agreement (device vs oracle)")
+    for label, n, fs, fi, nd, du, note in parity.RECORDS:
+        terminalreporter.write_line(f"{label}: {n} instances, status {fs:.4f}, iterations {fi:.4f}, "
+                                    f"{nd} disagreeing (each held to the termination test), "
+                                    f"max |du| where equal {du:.2e}{note}")
 
 
 def load_golden(name):

@@ -17,56 +17,9 @@ import pytest
 
 import pyoracle
 from osqp_amd import OSQPBatch, mpc
+from parity import check_agreement, subset, termination_detail as _termination_holds
 
 pytestmark = pytest.mark.gpu  # (the checker itself is CPU-tested: test_fullsize_checker.py)
-
-EPS = 1e-3
-SLACK = 1e-9  # host recomputation of the residuals (fp64 sums in another order)
-
-
-def _csc_rows_cols(M):
-    cols = np.repeat(np.arange(M.shape[1]), np.diff(M.indptr))
-    return M.indices.astype(np.int64), cols
-
-
-def _matvec(rows, cols, vals, x, nrow):
-    """Batched y[b] = M_b x[b] for one CSC pattern with per-instance values (B, nnz):
-    the products grouped by row and summed with one reduceat over the batch."""
-    order = np.argsort(rows, kind="stable")
-    r = rows[order]
-    contrib = vals[:, order] * x[:, cols[order]]
-    starts = np.flatnonzero(np.r_[True, r[1:] != r[:-1]]) if r.size else np.zeros(0, np.int64)
-    out = np.zeros((x.shape[0], nrow))
-    if r.size:
-        out[:, r[starts]] = np.add.reduceat(contrib, starts, axis=1)
-    return out
-
-
-def _termination_holds(b, x, y):
-    P, A = b["P"], b["A"]
-    n, m = b["n"], b["m"]
-    pr, pc = _csc_rows_cols(P)
-    ar, ac = _csc_rows_cols(A)
-    Px = _matvec(pr, pc, b["Px"], x, n)
-    off = pr != pc  # full symmetric P from its upper triangle
-    Px += _matvec(pc[off], pr[off], b["Px"][:, off], x, n)
-    Ax = _matvec(ar, ac, b["Ax"], x, m)
-    Aty = _matvec(ac, ar, b["Ax"], y, n)
-    q = b["q"]
-    inf = lambda v: np.abs(v).max(axis=1)  # noqa: E731
-    r_dua = inf(Px + q + Aty)
-    tol_dua = EPS + EPS * np.maximum(np.maximum(inf(Px), inf(Aty)), inf(q))
-    lo = np.maximum(b["l"], -1e30)
-    up = np.minimum(b["u"], 1e30)
-    dist = inf(np.maximum(lo - Ax, 0.0) + np.maximum(Ax - up, 0.0))
-    tol_pri = (EPS + EPS * inf(Ax)) / (1.0 - EPS)
-    return r_dua <= tol_dua * (1 + 1e-9) + SLACK, dist <= tol_pri * (1 + 1e-9) + SLACK, r_dua / tol_dua, dist / tol_pri
-
-
-def termination_holds(b, x, y):
-    """(dual ok, primal ok) per instance; shared with the CPU test of this checker."""
-    ok_d, ok_p, _, _ = _termination_holds(b, x, y)
-    return ok_d, ok_p
 
 
 def test_cfg3_full_batch_meets_the_termination_test():
@@ -99,10 +52,8 @@ def test_cfg3_full_batch_meets_the_termination_test():
     idx = np.random.default_rng(1).choice(B, 256, replace=False)
     bo = pyoracle.solve_batch(b["P"], b["A"], b["Px"][idx], b["q"][idx], b["Ax"][idx], b["l"][idx], b["u"][idx],
                               nthreads=16, **s)
-    assert np.mean(bo.iter == r1.iter[idx]) >= 0.99
-    same = bo.iter == r1.iter[idx]
-    du = np.abs(r1.x[idx][:, b["u_block"]] - bo.x[:, b["u_block"]]).max(axis=1)
-    assert np.all(du[same] < 1e-4), du.max()
+    check_agreement("cfg3 B=65536, oracle sample 256", subset(b, idx), r1.x[idx], r1.y[idx], r1.status_val[idx],
+                    r1.iter[idx], bo)
 
 
 def _stage_shift(v, N, nxa, nu, groups):
@@ -156,7 +107,13 @@ def test_cfg5_full_batch_warm_meets_the_termination_test():
     idx = np.random.default_rng(2).choice(B, 128, replace=False)
     bo = pyoracle.solve_batch(b["P"], b["A"], b["Px"][idx], b["q"][idx], b["Ax"][idx], l[idx], u[idx],
                               nthreads=16, x0=xs[idx], y0=ys[idx], **s)
-    same = bo.iter == r2.iter[idx]
-    assert (bo.status_val == 1).all() and same.mean() >= 0.97, (bo.iter[~same], r2.iter[idx][~same])
-    du = np.abs(r2.x[idx][:, b["u_block"]] - bo.x[:, b["u_block"]]).max(axis=1)
-    assert np.all(du[same] < 1e-4), du.max()
+    assert (bo.status_val == 1).all()
+    # (warm-started long-horizon solves: the iteration counts may part by one check interval on
+    # a few instances -- the reduced KKT's rounding over hundreds of iterations, DESIGN.md §3;
+    # each such instance is held to the termination test and the eps bound instead)
+    def tight(d):  # the sampled instances' optimum: the oracle from the same warm start at eps 1e-9
+        j = idx[d]
+        return pyoracle.solve_batch(b["P"], b["A"], b["Px"][j], b["q"][j], b["Ax"][j], l[j], u[j], nthreads=16,
+                                    x0=xs[j], y0=ys[j], **dict(s, eps_abs=1e-9, eps_rel=1e-9, max_iter=200000)).x
+    check_agreement("cfg5 B=8192 warm, oracle sample 128", subset(b2, idx), r2.x[idx], r2.y[idx],
+                    r2.status_val[idx], r2.iter[idx], bo, min_match=0.97, tight=tight)

@@ -1,11 +1,11 @@
-"""CPU check of tests/test_fullsize.py's termination-test checker: the oracle's own
+"""CPU check of the termination-test checker (tests/parity.py, used by the GPU parity tests): the oracle's own
 "solved" results (OSQP 0.6 restatement) satisfy it on a small slack batch, and a perturbed
 solution fails it."""
 import numpy as np
 
 import pyoracle
 from osqp_amd import mpc
-from test_fullsize import termination_holds
+from parity import termination_holds
 
 
 def test_checker_accepts_oracle_solutions_and_rejects_perturbed_ones():

@@ -16,6 +16,7 @@ import pytest
 
 import pyoracle
 from osqp_amd import OSQP, OSQPBatch, mpc
+from parity import check_agreement
 
 pytestmark = pytest.mark.gpu
 
@@ -93,20 +94,27 @@ def test_reference_builder_qps(golden, name, nu):
     _cmp_single(g["P"], g["q"], g["A"], g["l"], g["u"], _settings(g), slice(n - N * nu, n))
 
 
-def _batch_parity(b, settings, nthreads=16, min_match=0.99, rg=None):
+def _batch_parity(b, settings, nthreads=16, min_match=1.0, rg=None, label=None, x0=None, y0=None):
+    """Device vs oracle over batch b: tests/parity.py::check_agreement (agreement fractions
+    recorded; every disagreeing instance held to OSQP's termination test and compared with
+    the optimum, the oracle at eps 1e-9)."""
+    ws = {} if x0 is None else dict(x0=x0, y0=y0)
     bo = pyoracle.solve_batch(b["P"], b["A"], b["Px"], b["q"], b["Ax"], b["l"], b["u"], nthreads=nthreads,
-                              **settings)
+                              **ws, **settings)
+
+    def tight(d):
+        w = {} if x0 is None else dict(x0=x0[d], y0=y0[d])
+        return pyoracle.solve_batch(b["P"], b["A"], b["Px"][d], b["q"][d], b["Ax"][d], b["l"][d], b["u"][d],
+                                    nthreads=nthreads, **w,
+                                    **dict(settings, eps_abs=1e-9, eps_rel=1e-9, max_iter=200000)).x
     if rg is None:
         bg = OSQPBatch()
         bg.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **settings)
         rg = bg.solve()
-    ok = np.isfinite(bo.x).all(axis=1)
-    du = np.abs(rg.x[:, b["u_block"]] - bo.x[:, b["u_block"]]).max(axis=1)
-    same_status = rg.status_val == bo.status_val
-    same_iter = rg.iter == bo.iter
-    assert same_status.mean() >= min_match, (rg.status_val[~same_status][:8], bo.status_val[~same_status][:8])
-    assert same_iter.mean() >= min_match
-    assert np.all(du[ok & same_iter] < U_TOL), du.max()
+    label = label or f"cfg{b.get('cfg', '?')} B={b['Px'].shape[0]}"
+    y = getattr(rg, "y", None)
+    du = check_agreement(label, b, rg.x, y, rg.status_val, rg.iter, bo, min_match=min_match,
+                         tight=tight if settings.get("eps_abs", 1e-3) > 1e-8 else None)
     return du, rg, bo
 
 
@@ -122,8 +130,11 @@ def test_cfg3_batch_sample():
 
 
 def test_cfg5_batch_sample():
+    # (cold long-horizon solves of ~400 iterations: a count may part by one check interval --
+    # the reduced KKT's rounding, DESIGN.md §3 -- on an instance; it is held to the termination
+    # test and the eps bound instead)
     b = mpc.make_batch(5, B=64)
-    du, rg, bo = _batch_parity(b, dict(polish=False, warm_start=False))
+    du, rg, bo = _batch_parity(b, dict(polish=False, warm_start=False), min_match=0.98)
 
 
 def test_invalid_bounds_raise():
@@ -306,10 +317,8 @@ def test_cfg5_warm_started_batch():
     bg.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
     bg.warm_start(x=xs, y=ys)
     rg = bg.solve()
-    same_iter = rg.iter == bo.iter
-    assert (rg.status_val == bo.status_val).mean() >= 0.99 and same_iter.mean() >= 0.95
-    du = np.abs(rg.x[:, b["u_block"]] - bo.x[:, b["u_block"]]).max(axis=1)
-    assert np.all(du[same_iter] < U_TOL), du.max()
+    # (warm-started long-horizon solves: see test_cfg5_batch_sample on the 0.95 bar)
+    _batch_parity(b, s, min_match=0.95, rg=rg, label="cfg5 B=64 warm", x0=xs, y0=ys)
     assert bo.iter.mean() < r0.iter.mean()
 
 
@@ -364,7 +373,7 @@ def test_alternative_kernel_variants(monkeypatch, variant, cfg, B):
     monkeypatch.setenv("MPCQP_VARIANT", str(variant))
     b = mpc.make_batch(cfg, B=B)
     settings = dict(warm_start=True) if cfg == 3 else dict(polish=False, warm_start=False)
-    _batch_parity(b, settings)
+    _batch_parity(b, settings, min_match=0.98 if cfg == 5 else 1.0)  # (cfg 5: test_cfg5_batch_sample)
 
 
 EXPERIMENTAL = [(14, 3, 256), (8, 2, 256), (16, 2, 256), (18, 3, 256), (15, 5, 64)]
@@ -384,8 +393,10 @@ def test_experimental_kernel_variants(tmp_path):
     got = build_cases.in_build("exp", specs, tmp_path / "exp.npz")
     for v, cfg, B in EXPERIMENTAL:
         assert int(got[f"v{v}_variant"]) == v
-        rg = SimpleNamespace(x=got[f"v{v}_x"], iter=got[f"v{v}_iter"], status_val=got[f"v{v}_status_val"])
-        _batch_parity(mpc.make_batch(cfg, B=B), sets[cfg], rg=rg)
+        rg = SimpleNamespace(x=got[f"v{v}_x"], y=got[f"v{v}_y"], iter=got[f"v{v}_iter"],
+                             status_val=got[f"v{v}_status_val"])
+        _batch_parity(mpc.make_batch(cfg, B=B), sets[cfg], rg=rg, min_match=0.98 if cfg == 5 else 1.0,
+                      label=f"exp variant {v}, cfg{cfg} B={B}")
 
 
 def test_dense_inverse_form(tmp_path):
@@ -401,8 +412,8 @@ def test_dense_inverse_form(tmp_path):
     specs = [("batch", k, 2, 1024, None, s) for k, s in sets.items()]
     got = build_cases.in_build("exp", specs, tmp_path / "dk.npz", extra_env={"MPCQP_DENSE_W4": "1"})
     for k, s in sets.items():
-        rg = SimpleNamespace(x=got[f"{k}_x"], iter=got[f"{k}_iter"], status_val=got[f"{k}_status_val"])
-        _batch_parity(mpc.make_batch(2, B=1024), s, rg=rg)
+        rg = SimpleNamespace(x=got[f"{k}_x"], y=got[f"{k}_y"], iter=got[f"{k}_iter"], status_val=got[f"{k}_status_val"])
+        _batch_parity(mpc.make_batch(2, B=1024), s, rg=rg, label=f"cfg2 B=1024 dense-inverse form ({k})")
 
 
 def test_long_horizon_interface_form(tmp_path):
@@ -416,8 +427,8 @@ def test_long_horizon_interface_form(tmp_path):
                                extra_env={"MPCQP_BIG_FORM": "iface"})
     assert int(got["if_variant"]) == 12
     b = mpc.make_batch(5, B=64)
-    rg = SimpleNamespace(x=got["if_x"], iter=got["if_iter"], status_val=got["if_status_val"])
-    _batch_parity(b, s, rg=rg)
+    rg = SimpleNamespace(x=got["if_x"], y=got["if_y"], iter=got["if_iter"], status_val=got["if_status_val"])
+    _batch_parity(b, s, rg=rg, min_match=0.98, label="cfg5 B=64 interface form")
     h = OSQPBatch()
     h.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
     r = h.solve()
@@ -1411,6 +1422,41 @@ def test_long_horizon_factor_reuse_is_exact(monkeypatch):
         same = r1.iter == it
         du = np.array([np.abs(r1.x[k, b["u_block"]] - ro[k].x[b["u_block"]]).max() for k in range(len(ro))])
         assert np.all(du[same] < U_TOL), (step, du[same].max())
+
+
+@pytest.mark.gpu
+def test_long_horizon_reuse_after_a_rho_step_at_max_iter(monkeypatch):
+    """a solve whose last iteration is a rho-adaptation step (max_iter a
+    multiple of the rho interval) stores the new rho while the workspace factor is still the
+    old rho's; the next solve must refactor (OSQP 0.6 refactors inside adapt_rho), not start
+    from that stale factor.  cfg-5 handles that reuse the factor and ones that never do
+    (MPCQP_FACTOR_REUSE=0) run max_iter = 100 / 200 / 300 cold, then two warm re-solves, and
+    agree bit for bit; the rho step at the last iteration is confirmed to have fired on some
+    instance (its rho-update count exceeds that of a max_iter - 1 run)."""
+    b = mpc.make_batch(5, B=8, seed=21)
+    P, A = b["P"], b["A"]
+    fired = 0
+    for mi in (100, 200, 300):
+        s = dict(warm_start=True, polish=False, max_iter=mi)
+        handles = []
+        for reuse in ("1", "0"):
+            monkeypatch.setenv("MPCQP_FACTOR_REUSE", reuse)
+            h = OSQPBatch()
+            h.setup(P, b["q"], A, b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
+            handles.append(h)
+        monkeypatch.setenv("MPCQP_FACTOR_REUSE", "0")
+        short = OSQPBatch()
+        short.setup(P, b["q"], A, b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **dict(s, max_iter=mi - 1))
+        monkeypatch.delenv("MPCQP_FACTOR_REUSE")
+        r1, r0, rs = handles[0].solve(), handles[1].solve(), short.solve()
+        late = (r0.rho_updates > rs.rho_updates) & (r0.iter == mi)
+        fired += int(late.sum())
+        for step in range(3):
+            assert np.array_equal(r1.iter, r0.iter) and np.array_equal(r1.status_val, r0.status_val), (mi, step)
+            assert np.array_equal(r1.x, r0.x) and np.array_equal(r1.y, r0.y), (mi, step)
+            if step < 2:
+                r1, r0 = handles[0].solve(), handles[1].solve()
+    assert fired > 0, "no instance adapted rho at its last iteration: the case is not exercised"
 
 
 @pytest.mark.gpu

@@ -10,6 +10,7 @@ QPs over 8 GPUs) is exercised at one rank's full shard: 32768 instances.
 import numpy as np
 import pytest
 
+from parity import check_agreement
 import pyoracle
 from osqp_amd import OSQPBatch, mpc
 
@@ -94,8 +95,6 @@ def test_cfg4_rank_shard_32768(monkeypatch):
     assert (st == 1).all()
     idx = np.random.default_rng(0).choice(B, 384, replace=False)
     bo = pyoracle.solve_batch(P, A, Px[idx], b["q"][idx], Ax[idx], b["l"][idx], b["u"][idx], nthreads=16, **s)
-    assert np.mean(bo.status_val == st[idx]) == 1.0
-    assert np.mean(bo.iter == it[idx]) >= 0.99
-    du = np.abs(o1[0].cpu().numpy()[idx][:, b["u_block"]] - bo.x[:, b["u_block"]]).max(axis=1)
-    same = bo.iter == it[idx]
-    assert np.all(du[same] < 1e-4), du.max()
+    bs = dict(b, P=P, A=A, Px=Px[idx], Ax=Ax[idx], q=b["q"][idx], l=b["l"][idx], u=b["u"][idx])
+    check_agreement("cfg4 rank shard 32768, oracle sample 384", bs, o1[0].cpu().numpy()[idx],
+                    o1[1].cpu().numpy()[idx], st[idx], it[idx], bo)
