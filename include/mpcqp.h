@@ -240,7 +240,8 @@ int mpcqp_debug_dispatch_order(mpcqp_handle *h, int32_t *out);
  * kernel -- 16-byte loads and stores, four or eight in flight per lane, 256-thread workgroups;
  * five forms (non-temporal; default policy; default policy with eight per lane; one pass of a
  * workgroup per 16 KiB, default policy or non-temporal) -- on `stream`
- * (hipStream_t, NULL: the null stream), timed by an event pair around each form's launches:
+ * (hipStream_t, NULL: the null stream of the current device; a non-NULL stream makes its own
+ * device the calling thread's current one), timed by an event pair around each form's launches:
  * *ms = the average per copy of the fastest form.  Blocks until done. */
 int mpcqp_debug_copy(const double *src, double *dst, int64_t n, int32_t reps, void *stream, double *ms);
 

@@ -1616,9 +1616,21 @@ int mpcqp_debug_copy(const double* src, double* dst, int64_t n, int32_t reps, vo
     if (!src || !dst || !ms || n <= 0 || n % 16384 || reps <= 0 || ((uintptr_t)src | (uintptr_t)dst) & 15)
         return fail(MPCQP_EINVAL, "mpcqp_debug_copy: n > 0, n %% 16384 == 0, reps > 0, 16-byte aligned buffers");
     hipStream_t st = (hipStream_t)stream;
-    hipEvent_t a, b;
-    HIPCHK(hipEventCreate(&a));
-    HIPCHK(hipEventCreate(&b));
+    if (st) {  // the events and kernels on the device the caller's stream belongs to
+        int dev = 0;
+        HIPCHK(hipStreamGetDevice(st, &dev));
+        HIPCHK(hipSetDevice(dev));
+    }
+    struct Events {  // destroyed on every return path (HIPCHK returns early)
+        hipEvent_t a = nullptr, b = nullptr;
+        ~Events() {
+            if (a) (void)hipEventDestroy(a);
+            if (b) (void)hipEventDestroy(b);
+        }
+    } ev;
+    HIPCHK(hipEventCreate(&ev.a));
+    HIPCHK(hipEventCreate(&ev.b));
+    hipEvent_t a = ev.a, b = ev.b;
     double best = 0.0;
     for (int form = 0; form < 5; ++form) {  // the fastest of the five forms (kernels.hip::launch_copy16)
         HIPCHK(launch_copy16(src, dst, n, st, form));  // (warm-up)
@@ -1632,8 +1644,6 @@ int mpcqp_debug_copy(const double* src, double* dst, int64_t n, int32_t reps, vo
         if (form == 0 || per < best) best = per;
     }
     *ms = best;
-    (void)hipEventDestroy(a);
-    (void)hipEventDestroy(b);
     return 0;
 }
 

@@ -209,12 +209,17 @@ def _csc_sorted(M):
 
 def canonical_data(P, A):
     """osqp-python's prepare_data: P -> triu CSC, A -> CSC, sorted int32 indices.  The upper
-    triangle is taken from the CSC arrays directly (the same entries, order and duplicates as
-    scipy.sparse.triu; a few tens of microseconds instead of a few hundred on the reference's
-    fresh-object-per-call pattern, Control/MPC/mpc_dynamics.py:392)."""
+    triangle is taken from the CSC arrays directly: the same entries and order as
+    scipy.sparse.triu (a few tens of microseconds instead of a few hundred on the reference's
+    fresh-object-per-call pattern, Control/MPC/mpc_dynamics.py:392).  Duplicate entries of P
+    are summed first, as triu's COO -> CSC conversion sums them; A keeps its duplicates, as
+    osqp-python passes A's stored entries to OSQP unchanged."""
     if P is None:
         raise ValueError("P must be provided")
     P = _csc_sorted(P)
+    if not P.has_canonical_format:  # duplicates (sorted indices are known by now)
+        P = P.copy()
+        P.sum_duplicates()
     A = _csc_sorted(A)
     n = P.shape[1]
     cols = np.repeat(np.arange(n, dtype=np.int64), np.diff(P.indptr))

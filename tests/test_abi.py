@@ -384,3 +384,21 @@ def test_canonical_data_matches_scipy():
         assert np.array_equal(Mk.indptr, M0.indptr) and np.array_equal(Mk.indices, M0.indices)
         assert np.array_equal(Vk, V[:, keep])
         assert np.array_equal(osqp_amd._kept_index(V)[keep], np.arange(int(keep.sum())))
+
+
+def test_canonical_data_sums_duplicate_P_entries_like_triu():
+    """canonical_data's fast upper triangle must match scipy.sparse.triu (what
+    osqp-python's prepare_data takes), which sums duplicate entries; a P with a duplicated
+    (0, 0) entry gave nnz 3 against triu's 2."""
+    import scipy.sparse as sp
+    from osqp_amd import canonical_data
+    P = sp.csc_matrix((np.array([1.0, 2.0, 0.5, 3.0]), np.array([0, 0, 0, 1]), np.array([0, 2, 4])), shape=(2, 2))
+    assert not P.has_canonical_format
+    A = sp.csc_matrix(np.eye(2))
+    Pc, _ = canonical_data(P, A)
+    ref = sp.triu(P, format="csc")
+    ref.sort_indices()
+    assert Pc.nnz == ref.nnz == 3  # (0, 0) once, (0, 1), (1, 1)
+    assert np.array_equal(Pc.indptr, ref.indptr) and np.array_equal(Pc.indices, ref.indices)
+    assert np.array_equal(Pc.data, ref.data)
+    assert Pc.toarray()[0, 0] == 3.0
