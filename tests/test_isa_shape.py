@@ -1,0 +1,58 @@
+"""The hot kernels' register allocation, pinned (CPU test).
+
+The fused cfg-2 kernel and the long-horizon kernel are held in shape by empty-asm register
+steering points (29 `asm volatile("")` in solve_big.hip / solve_wave.hip / solve_phases.h) and by
+code placement: DESIGN.md records that edits outside the ADMM loop move its register assignment
+by +-1 %, and spills or `v_readlane` reloads that appeared only on the GPU.  This test reads the
+code objects that ship in python-mpc_amd/osqp_amd/libmpcqp.so (tests/isa_shape.py) and fails when
+any of the recorded shapes moves:
+
+* VGPR / AGPR counts, spilled VGPRs, the scratch bytes per lane (12 B on cfg 2 and cfg 5: the
+  callee-saved SGPR-spill lanes of the out-of-line phases; 44 B with 5 spilled VGPRs on the
+  slack layouts' eliminated-column kernel), SGPR spills at most the recorded count;
+* the ADMM loop: its instruction count, its workgroup barriers, no scratch access, and its
+  `v_readlane` count (none in the four-wave loops);
+* k_solve_b's two-sided sweep steps: no `v_readlane` and no scratch access in them.
+
+An intended change to these kernels updates the numbers here (`python tests/isa_shape.py`
+prints them) together with the same-box A/B that justified it.
+"""
+import os
+
+import pytest
+
+import isa_shape
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "python-mpc_amd", "osqp_amd", "libmpcqp.so")
+
+PINNED = {
+    "cfg2": dict(vgpr_count=256, agpr_count=0, vgpr_spill_count=0, private_segment_fixed_size=12, sgpr_spill_max=185,
+                 loop=dict(instructions=197, barriers=4, readlane=0, scratch=0)),
+    "cfg3": dict(vgpr_count=256, agpr_count=0, vgpr_spill_count=5, private_segment_fixed_size=44, sgpr_spill_max=212,
+                 loop=dict(instructions=233, barriers=4, readlane=0, scratch=0)),
+    "cfg5": dict(vgpr_count=254, agpr_count=0, vgpr_spill_count=0, private_segment_fixed_size=12, sgpr_spill_max=236,
+                 loop=dict(instructions=1617, barriers=21, readlane=46, scratch=0),
+                 step_readlane=0, step_scratch=0),
+}
+
+
+@pytest.fixture(scope="module")
+def shapes():
+    if not isa_shape.tools_present():
+        pytest.skip("ROCm LLVM tools (llvm-objcopy, clang-offload-bundler, llvm-readelf, llvm-objdump) absent")
+    if not os.path.exists(LIB):
+        pytest.skip("libmpcqp.so not built")
+    return isa_shape.report(LIB, isa_shape.HOT)
+
+
+@pytest.mark.parametrize("key", sorted(PINNED))
+def test_hot_kernel_shape_is_pinned(shapes, key):
+    got, want = shapes[key], PINNED[key]
+    for f in ("vgpr_count", "agpr_count", "vgpr_spill_count", "private_segment_fixed_size"):
+        assert got[f] == want[f], (key, f, got[f], want[f], got["symbol"])
+    assert got["sgpr_spill_count"] <= want["sgpr_spill_max"], (key, got["sgpr_spill_count"])
+    assert got["loop"] == want["loop"], (key, got["loop"], want["loop"])
+    if "step_readlane" in want:
+        assert got["step_loops"] >= 8, got  # the forward / backward step runs of the sweep were found
+        assert got["step_readlane"] == want["step_readlane"] and got["step_scratch"] == want["step_scratch"], got
