@@ -250,13 +250,27 @@ def pmc_traffic(workload, batch, kernel):
     """HBM bytes per k_solve launch from rocprofv3 PMC passes committed under
     profiles/ (tools/gpu_profile.sh + tools/pmc_summary.py give traffic.json, copied to profiles/traffic_<workload>_b<B>.json:
     FETCH_SIZE and WRITE_SIZE from separate --pmc passes, FETCH_SIZE doubled per
-    the gfx950 note of MI355X_MICROARCH.md).  {} when not measured."""
+    the gfx950 note of MI355X_MICROARCH.md).  {} when not measured.  The record names the code it
+    was measured on (code_sha16: tools/codeobj.py's hash of every instantiation of the kernel in the
+    library); when that is not the loaded library's, the record is stale -- {"traffic_stale": True}."""
     path = os.path.join(ROOT, "profiles", f"traffic_{workload}_b{batch}.json")
     if not os.path.exists(path):
         return {}
     with open(path) as f:
         t = json.load(f)
-    return t if t.get("kernel") == kernel else {}  # measured on another kernel: not this one's traffic
+    if t.get("kernel") != kernel:
+        return {}  # measured on another kernel: not this one's traffic
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import codeobj
+        import osqp_amd
+        cur = codeobj.kernel_code_hash(osqp_amd.LIB_PATH, kernel)
+    except Exception as e:  # (tools absent: the record cannot be tied to this build)
+        return {"traffic_stale": True, "stale_reason": f"code hash unavailable: {e}", "source": t.get("source")}
+    if t.get("code_sha16") != cur:
+        return {"traffic_stale": True, "code_sha16": cur, "source": t.get("source"),
+                "stale_reason": f"measured on code {t.get('code_sha16')}, loaded {cur}"}
+    return t
 
 
 def copy_peak(dev_index, nbytes=2 << 30, reps=10):
@@ -795,6 +809,8 @@ def main(argv=None, solver_cls=None, device=None):
                                 "kernel_variant": info["variant"], "threads_per_qp": info["threads_per_qp"]}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic.get("bytes_per_launch"),
+                         "traffic_stale": bool(traffic.get("traffic_stale", False)),
+                         "traffic_code_sha16": traffic.get("code_sha16"),
                          # the achievable peak of a plain device copy on this
                          # GPU, beside the datasheet peak (diagnostic; `frac` uses the datasheet)
                          "peak_copy_measured": copy_gbs,

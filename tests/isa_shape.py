@@ -1,89 +1,13 @@
-"""Code-object shape of the production library's hot kernels (test helper, CPU only).
-
-Reads what actually ships: the gfx950 code objects bundled in libmpcqp.so's .hip_fatbin
-section (one clang offload bundle per translation unit), unbundled with clang-offload-bundler,
-their AMDGPU metadata printed by llvm-readelf --notes, their instructions by llvm-objdump.
-"""
+"""Code-object shape of the production library's hot kernels (test helper, CPU only): what
+actually ships, read by tools/codeobj.py from libmpcqp.so's bundled gfx950 code objects."""
 import os
 import re
 import subprocess
+import sys
 import tempfile
 
-LLVM = "/opt/rocm/lib/llvm/bin"
-MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
-TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
-FIELDS = ("vgpr_count", "agpr_count", "sgpr_count", "vgpr_spill_count", "sgpr_spill_count",
-          "private_segment_fixed_size", "group_segment_fixed_size")
-
-
-def tools_present():
-    return all(os.path.exists(os.path.join(LLVM, t)) for t in ("llvm-objcopy", "clang-offload-bundler",
-                                                                "llvm-readelf", "llvm-objdump"))
-
-
-def code_objects(lib, workdir):
-    """Paths of the gfx950 code objects inside `lib`."""
-    fat = os.path.join(workdir, "fat.bin")
-    subprocess.run([os.path.join(LLVM, "llvm-objcopy"), f"--dump-section=.hip_fatbin={fat}", lib, os.devnull],
-                   check=True, capture_output=True)
-    data = open(fat, "rb").read()
-    offs = [m.start() for m in re.finditer(re.escape(MAGIC), data)] + [len(data)]
-    out = []
-    for i in range(len(offs) - 1):
-        b = os.path.join(workdir, f"b{i}.bin")
-        co = os.path.join(workdir, f"co{i}.elf")
-        with open(b, "wb") as f:
-            f.write(data[offs[i]:offs[i + 1]])
-        subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={b}",
-                        f"--targets={TARGET}", f"--output={co}"], check=True, capture_output=True)
-        out.append(co)
-    return out
-
-
-def metadata(co):
-    """{kernel name: {field: int}} from the code object's AMDGPU metadata note."""
-    txt = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", co], check=True, capture_output=True,
-                         text=True).stdout
-    out = {}
-    for m in re.finditer(r"\n  - (\.\w+:.*?)(?=\n  - \.|\n  amdhsa\.target|\Z)", txt, re.S):
-        body = m.group(1)
-        nm = re.search(r"\.name:\s+(\S+)", body)
-        if not nm:
-            continue
-        d = {}
-        for f in FIELDS:
-            r = re.search(r"\." + f + r":\s+(\d+)", body)
-            d[f] = int(r.group(1)) if r else 0
-        out[nm.group(1)] = d
-    return out
-
-
-def symbol_range(co, name):
-    txt = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "-s", co], check=True, capture_output=True,
-                         text=True).stdout
-    for ln in txt.splitlines():
-        f = ln.split()
-        if len(f) >= 8 and f[-1] == name and f[3] == "FUNC":
-            a = int(f[1], 16)
-            return a, a + int(f[2])
-    raise KeyError(name)
-
-
-def instructions(co, name):
-    """(instructions, {label: index}) of kernel `name`."""
-    a, b = symbol_range(co, name)
-    txt = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", "--symbolize-operands", f"--start-address={a}",
-                          f"--stop-address={b}", co], check=True, capture_output=True, text=True).stdout
-    ins, labels = [], {}
-    for ln in txt.splitlines():
-        m = re.match(r"^[0-9a-f]+ <(L\d+)>:", ln)
-        if m:
-            labels[m.group(1)] = len(ins)
-            continue
-        if "//" in ln and ln.startswith("\t"):
-            ins.append(ln.split("//")[0].strip())
-    return ins, labels
-
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+from codeobj import LLVM, code_objects, instructions, metadata, tools_present  # noqa: E402,F401
 
 def loops(ins, labels):
     """Backward branches: (start, end) instruction index ranges, innermost first by length."""

@@ -402,3 +402,27 @@ def test_canonical_data_sums_duplicate_P_entries_like_triu():
     assert np.array_equal(Pc.indptr, ref.indptr) and np.array_equal(Pc.indices, ref.indices)
     assert np.array_equal(Pc.data, ref.data)
     assert Pc.toarray()[0, 0] == 3.0
+
+
+def test_traffic_record_is_tied_to_the_measured_code(tmp_path, monkeypatch):
+    """bench.py reports roofline.traffic only from a PMC record measured on the
+    loaded library's code (code_sha16, tools/codeobj.py); another build's record is stale."""
+    import json as _json
+    import bench
+    import osqp_amd
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import codeobj
+    if not os.path.exists(osqp_amd.LIB_PATH):
+        pytest.skip("libmpcqp.so not built")
+    cur = codeobj.kernel_code_hash(osqp_amd.LIB_PATH, "mpcqp::k_setup_solve_w4")
+    assert len(cur) == 16 and cur != codeobj.kernel_code_hash(osqp_amd.LIB_PATH, "mpcqp::k_solve_b")
+    (tmp_path / "profiles").mkdir()
+    rec = {"kernel": "mpcqp::k_setup_solve_w4", "bytes_per_launch": 123.0, "source": "test"}
+    f = tmp_path / "profiles" / "traffic_w_b8.json"
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    for sha, stale in ((None, True), ("0123456789abcdef", True), (cur, False)):
+        f.write_text(_json.dumps(dict(rec, code_sha16=sha)))
+        t = bench.pmc_traffic("w", 8, "mpcqp::k_setup_solve_w4")
+        assert bool(t.get("traffic_stale")) == stale, (sha, t)
+        assert (t.get("bytes_per_launch") == 123.0) == (not stale)
+    assert bench.pmc_traffic("w", 8, "mpcqp::k_solve_b") == {}  # a record of another kernel

@@ -41,6 +41,13 @@ def main():
     B = line["config"]["batch_per_gpu"]
     alg = line["roofline"]["bytes_per_solve"]
     res = {"kernel": kernel, "workload": line["config"]["workload"], "batch": B}
+    # the code the counters were collected on (bench.py::pmc_traffic compares it with the loaded
+    # library's): the package of the run (MPCQP_PKG, else this tree's), its production library
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import codeobj
+    pkg = os.environ.get("MPCQP_PKG", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                   "python-mpc_amd"))
+    res["code_sha16"] = codeobj.kernel_code_hash(os.path.join(pkg, "osqp_amd", "libmpcqp.so"), kernel)
     kt = rows(os.path.join(d, "kt", "*kernel_stats.csv"))
     for r in kt:
         if kernel.split("::")[-1] in r["Name"]:
