@@ -433,7 +433,8 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io, bool sync = true) {
     k.mode = solve_mode(k.variant);
     // k_solve_w2 sorts the next dispatch order in its last workgroup (MPCQP_ORDER_KERNEL=1: k_order)
     k.done = nullptr;
-    if ((k.variant == 10 || k.variant == 17) && k.order && !(getenv("MPCQP_ORDER_KERNEL") && getenv("MPCQP_ORDER_KERNEL")[0] == '1'))
+    if ((k.variant == 10 || k.variant == 17 || k.variant == 19) && k.order &&
+        !(getenv("MPCQP_ORDER_KERNEL") && getenv("MPCQP_ORDER_KERNEL")[0] == '1'))
         k.done = done;
     {  // resident solve workgroups: below this batch size the dispatch order is moot
         int ncu = 0;

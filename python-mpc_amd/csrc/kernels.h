@@ -165,6 +165,14 @@ hipError_t launch_polish(const KParams& p, long B, double* xo, double* yo, hipSt
 // one-wave-per-QP kernel (solve_wave.hip), variants 8 and 9
 hipError_t launch_solve_wave(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st,
                         KernelRef* ref = nullptr);
+// one 512-thread workgroup per QP, alone on its CU, the dense-inverse solve held in registers
+// (solve_heavy.hip, variant 19): the latency form for a batch's predicted-slowest instances
+bool heavy_fits(const KParams& p);
+size_t heavy_lds(const KParams& p);
+hipError_t launch_solve_heavy(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st,
+                              KernelRef* ref = nullptr);
+hipError_t launch_setup_solve_heavy(const KParams& p, long B, const double* Px, const double* Ax, const double* q,
+                                    const double* l, const double* u, double* xo, double* yo, hipStream_t st);
 // 512-thread long-horizon kernel (solve_big.hip), variants 11-13
 hipError_t launch_solve_big(const KParams& p, long B, double* xo, double* yo, int factor_only, hipStream_t st,
                         KernelRef* ref = nullptr);

@@ -675,6 +675,9 @@ size_t lds_kernel_bytes(const KParams& p) {
     if (p.variant == 16) return lds_dense_bytes(p);
 #endif
     if (p.variant == 10 || p.variant == 17) return lds_w2_bytes(p);
+#ifdef MPCQP_EXPERIMENTAL
+    if (p.variant == 19) return heavy_lds(p);
+#endif
     return (p.variant >= 11 && p.variant <= 15) ? lds_solve_bytes_big(p) : lds_solve_bytes(p);
 }
 
@@ -699,10 +702,10 @@ bool variant_fits(const KParams& p, int v) {
     const int cs = (p.npad + T - 1) / T, rs = (p.m + T - 1) / T;
     if (p.ne && v != 17) return false;  // eliminated variables: the four-wave kernel only
 #ifndef MPCQP_EXPERIMENTAL
-    // measured and not taken (DESIGN.md §5, §10): one-wave 8 / 9, two-wave two-sided 14,
-    // 256-thread twisted 15, dense inverse 16, eight-wave 18 -- only in the exp / diagnostic
-    // builds (MPCQP_BUILD=exp)
-    if (v == 8 || v == 9 || v == 14 || v == 15 || v == 16 || v == 18) return false;
+    // measured and not taken (DESIGN.md §5, §10, §11): one-wave 8 / 9, two-wave two-sided 14,
+    // 256-thread twisted 15, dense inverse 16, eight-wave 18, one-instance-per-CU dense 19 -- only
+    // in the exp / diagnostic builds (MPCQP_BUILD=exp)
+    if (v == 8 || v == 9 || v == 14 || v == 15 || v == 16 || v == 18 || v == 19) return false;
 #endif
     switch (v) {
         case 0: case 7: return p.nb == 4 && p.amax <= 8 && p.gk <= 6 && cs <= 1 && rs <= 1;
@@ -752,6 +755,7 @@ bool variant_fits(const KParams& p, int v) {
                    packed < 65536 && lds_solve_bytes(q2) <= 160 * 1024;
         }
 #ifdef MPCQP_EXPERIMENTAL
+        case 19: return heavy_fits(p);  // one 512-thread workgroup per QP (solve_heavy.hip)
         case 16:  // dense inverse: one variable per lane pair of a 256-thread workgroup, packed LDS addresses
             return p.n <= kDenseR && p.npad <= 128 && p.gk <= 6 && p.pk <= 4 && p.m <= 2 * 128 &&
                    lds_dense_bytes(p) < 65536;
@@ -761,7 +765,7 @@ bool variant_fits(const KParams& p, int v) {
 }
 
 int solve_variant(const KParams& p) {
-    static const int order[] = {17, 10, 0, 1, 2, 3, 11, 12, 13, 4, 5, 6};  // 8, 9, 14, 16, 18: MPCQP_VARIANT only
+    static const int order[] = {17, 10, 0, 1, 2, 3, 11, 12, 13, 4, 5, 6};  // 8, 9, 14, 16, 18, 19: MPCQP_VARIANT only
     for (int v : order)
         if (variant_fits(p, v)) return v;
     return -1;
@@ -777,13 +781,14 @@ int solve_threads(int variant) {
         case 16: return 256;
         case 17: return 256;
         case 18: return 512;
+        case 19: return 512;
         default: return T;
     }
 }
 
 int solve_mode(int variant) {  // what factorize stores for the variant (KParams::mode)
     switch (variant) {
-        case 0: case 8: case 9: case 10: case 17: case 18: return 2;
+        case 0: case 8: case 9: case 10: case 17: case 18: case 19: return 2;
         case 1: case 2: case 3: case 7: case 16: return 1;  // (16: no factor stored; dx aliases rb)
         case 11: case 12: case 13: case 14: case 15: return 3;  // two-sided factor (solve_big.hip)
         default: return 0;
@@ -803,6 +808,14 @@ static hipError_t launch_solve_only(const KParams& p, long B, double* xo, double
         case 6: return go<0, 32, 16, 8, 8, 1>(p, B, xo, yo, factor_only, st, lds, ref);
         case 7: return go<4, 8, 6, 1, 1, 2, false>(p, B, xo, yo, factor_only, st, lds, ref);
         case 8: case 9: case 10: case 17: case 18: return launch_solve_wave(p, B, xo, yo, factor_only, st, ref);
+#ifdef MPCQP_EXPERIMENTAL
+        case 19: {
+            if (!factor_only) return launch_solve_heavy(p, B, xo, yo, 0, st, ref);
+            KParams q = p;  // setup()'s convexity factorisation: the four-wave kernel's (the same factor)
+            q.variant = 17;
+            return launch_solve_wave(q, B, xo, yo, factor_only, st, ref);
+        }
+#endif
 #ifdef MPCQP_EXPERIMENTAL
         case 16: return launch_solve_dense(p, B, xo, yo, factor_only, st, ref);
 #endif

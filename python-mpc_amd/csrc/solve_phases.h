@@ -569,9 +569,13 @@ __device__ __forceinline__ bool factorize_w2(const KP& p, SLds& L, const double 
 // k assembles D_k and pre-pivots it (block 0: the whole inverse), all four at once --
 // then the same k = 1..3 chain (F_k, the corner, the G blocks, wave 0's corner pivots).
 // The critical path of stage 1 is one block's pivots instead of two.  Same outputs.
-template <bool ROT = false, class KP>
+// TT = 512 (solve_heavy.hip, the one-instance-per-CU kernel): waves 0-3 run stage 1 and the
+// chain exactly as with 256 threads, waves 4-7 join the F / G products (the same sums per
+// output element: the factor is bit-identical to the 256-thread one).
+template <bool ROT = false, int TT = 256, class KP>
 __device__ __forceinline__ bool factorize_w4(const KP& p, SLds& L, const double rho, double* __restrict__ Hg,
                                              double* __restrict__ Sg, double* __restrict__ Fo) {
+    static_assert(TT == 256 || TT == 512, "four or eight waves");
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int amax = p.amax, as = amax * S;
     const long gstride = (long)amax * S;
@@ -593,12 +597,14 @@ __device__ __forceinline__ bool factorize_w4(const KP& p, SLds& L, const double 
 #else
 #define FPH(k)
 #endif
-    assemble_block<false, true>(p, L, rho, w, Sg + (long)w * SS, Ek(w), lane, 64, wave_sync);
-    wave_sync();
+    const bool sw = TT == 256 || w < 4;  // a stage-1 wave (wave w: block w)
     // an eliminated column's pivot K_jj is a pivot of the full KKT factorisation too: a
     // non-positive (or NaN) one makes the instance non-convex, as OSQP's LDL' of the
     // quasi-definite matrix would find, even though the reduced blocks may still factor
     bool oke = true;
+    if (sw) {
+    assemble_block<false, true>(p, L, rho, w, Sg + (long)w * SS, Ek(w), lane, 64, wave_sync);
+    wave_sync();
     if (p.ne && lane < S) {
         // eliminated columns (plan.h Plan::eown): the owner lane of block column w S + lane
         // forms K_jj, K_pj of its column j, folds the Schur complement -K_pj^2 / K_jj into its
@@ -622,9 +628,13 @@ __device__ __forceinline__ bool factorize_w4(const KP& p, SLds& L, const double 
         }
         wave_sync();
     }
+    }
     FPH(8)
-    bool okw = gj_seg<1, false, ROT>(Sg + (long)w * SS, bufw, w ? amax : 0, p.bsize[w], nullptr);
-    okw = okw && __builtin_amdgcn_ballot_w64(!oke) == 0;
+    bool okw = true;
+    if (sw) {
+        okw = gj_seg<1, false, ROT>(Sg + (long)w * SS, bufw, w ? amax : 0, p.bsize[w], nullptr);
+        okw = okw && __builtin_amdgcn_ballot_w64(!oke) == 0;
+    }
     FPH(10)
     __syncthreads();
     FPH(11)
@@ -634,7 +644,7 @@ __device__ __forceinline__ bool factorize_w4(const KP& p, SLds& L, const double 
         const double* E = Ek(k);
         double* F = Fk(k);
         const int l0 = p.toff[k - 1], bmax = p.bmax;
-        for (int o = tid; o < as; o += 256) {
+        for (int o = tid; o < as; o += TT) {
             const int r = o >> 5, j = o & (S - 1);
             double sacc = 0.0;
 #pragma unroll 4
@@ -663,7 +673,7 @@ __device__ __forceinline__ bool factorize_w4(const KP& p, SLds& L, const double 
                 const bool adj = j == k - 2;
                 const double* Gp = adj ? Fk(k - 1) : G20;
                 const double sg = adj ? 1.0 : -1.0;
-                for (int o = tid - 64; o < as; o += 192) {
+                for (int o = tid - 64; o < as; o += TT - 64) {
                     const int r = o >> 5, c = o & (S - 1);
                     double sacc = 0.0;
 #pragma unroll

@@ -2430,6 +2430,12 @@ static int setup_solve_fits(const KParams& p) {
 
 hipError_t launch_setup_solve(const KParams& p, long B, const double* Px, const double* Ax, const double* q,
                               const double* l, const double* u, double* xo, double* yo, hipStream_t st) {
+#ifdef MPCQP_EXPERIMENTAL
+    if (p.variant == 19) {
+        hipError_t e = launch_setup_solve_heavy(p, B, Px, Ax, q, l, u, xo, yo, st);
+        return (e != hipSuccess || !p.polish) ? e : launch_polish(p, B, xo, yo, st);
+    }
+#endif
     if (!setup_solve_fits(p)) {
         hipError_t e = launch_setup(p, B, Px, Ax, q, l, u, st);
         return e != hipSuccess ? e : launch_solve(p, B, xo, yo, 0, st);

@@ -376,15 +376,16 @@ def test_alternative_kernel_variants(monkeypatch, variant, cfg, B):
     _batch_parity(b, settings, min_match=0.98 if cfg == 5 else 1.0)  # (cfg 5: test_cfg5_batch_sample)
 
 
-EXPERIMENTAL = [(14, 3, 256), (8, 2, 256), (16, 2, 256), (18, 3, 256), (15, 5, 64)]
+EXPERIMENTAL = [(14, 3, 256), (8, 2, 256), (16, 2, 256), (18, 3, 256), (15, 5, 64), (19, 2, 1024)]
 
 
 def test_experimental_kernel_variants(tmp_path):
-    """The variants measured and not taken (DESIGN.md §5) are built only into the exp
+    """The variants measured and not taken (DESIGN.md §5, §11) are built only into the exp
     library (python-mpc_amd/csrc/Makefile, MPCQP_EXPERIMENTAL): the two-wave two-sided
     kernel on the slack layout (14), the one-wave kernel (8) and the dense-inverse kernel
     (16) on cfg 2, the eight-wave kernel (18) on the slack layout, the 256-thread twisted
-    long-horizon kernel (15) on cfg 5.  They stay exact against
+    long-horizon kernel (15) on cfg 5, the one-instance-per-CU latency kernel (19,
+    solve_heavy.hip: 512 threads, M = K^-1 in registers) on the whole cfg-2 batch.  They stay exact against
     the oracle, solved in a child process under MPCQP_BUILD=exp; and the production
     library refuses them (MPCQP_VARIANT=v does not fit)."""
     import build_cases

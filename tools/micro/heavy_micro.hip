@@ -37,13 +37,16 @@ __host__ __device__ inline int padc(int c) {
     return 32 * k + c;
 }
 
+// PROD: 0 no product phase, 1 product without the 8-lane sums, 2 full; ph: per-phase cycles (wave 0)
+template <int PROD>
 __global__ __launch_bounds__(TT, 1) void k_iter(const double* Mg, const int* colg, const int* rowg, int nit,
-                                                 long long* cyc, double* out) {
+                                                 long long* cyc, double* out, long long* ph) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double* Av = sm;                 // 512 A values (+ zero slot at 511)
     double* w = Av + 512;            // MR
     double* rb = w + MR;             // NP
     double* xt = rb + NP;            // NP
+    double* rbs = xt + NP;           // 8 x 18: b by segment (PROD 3), banks spread
     const int tid = threadIdx.x, lane = tid & 63;
     for (int e = tid; e < 512; e += TT) Av[e] = e == 511 ? 0.0 : 0.001 * (e % 37) - 0.01;
     for (int i = tid; i < MR; i += TT) w[i] = 0.01 * (i % 7);
@@ -65,7 +68,7 @@ __global__ __launch_bounds__(TT, 1) void k_iter(const double* Mg, const int* col
     double X = 0.0, Z = 0.0, y = 0.0;
     const double sigma = 1e-6, alpha = 1.6, q = 0.01 * (tid & 7), rv = 0.1, rvi = 10.0, lo = -1.0, up = 1.0;
     __syncthreads();
-    long long t0 = clock64();
+    long long t0 = clock64(), tp = t0, pa = 0, pb = 0, pc = 0;
     for (int it = 0; it < nit; ++it) {
         // rhs (columns): x update from x~, b = sigma x - q + A' w
         if (tid < NP) {
@@ -78,14 +81,19 @@ __global__ __launch_bounds__(TT, 1) void k_iter(const double* Mg, const int* col
 #pragma unroll
             for (int k = 0; k < K; ++k) v += av[k] * wv[k];
             rb[tid] = v;
+            if (PROD == 3) {
+                const int blk = tid >> 5, c = tid & 31, h = c >= SEGW;
+                if (c < 2 * SEGW) rbs[18 * (2 * blk + h) + c - SEGW * h] = v;
+            }
         }
         __syncthreads();
+        { const long long t = clock64(); pa += t - tp; tp = t; }
         // x~ = M b: 2 rows x 14 columns per lane, 8-lane sums
-        if (tid < 8 * NRP) {
+        if (PROD > 0 && tid < 8 * NRP) {
             double bv[SEGW];
 #pragma unroll
             for (int c = 0; c < SEGW; c += 2) {
-                const double2 t = *(const double2*)(rb + c0 + c);
+                const double2 t = PROD == 3 ? *(const double2*)(rbs + 18 * sg + c) : *(const double2*)(rb + c0 + c);
                 bv[c] = t.x;
                 bv[c + 1] = t.y;
             }
@@ -97,11 +105,12 @@ __global__ __launch_bounds__(TT, 1) void k_iter(const double* Mg, const int* col
                 a2 += Mr[1][c] * bv[c];
                 a3 += Mr[1][c + 1] * bv[c + 1];
             }
-            const double s0 = reduce8(a0 + a1), s1 = reduce8(a2 + a3);
+            const double s0 = PROD >= 2 ? reduce8(a0 + a1) : a0 + a1, s1 = PROD >= 2 ? reduce8(a2 + a3) : a2 + a3;
             if (sg == 0) xt[r0] = s0;
             if (sg == 1) xt[r1] = s1;
         }
         __syncthreads();
+        { const long long t = clock64(); pb += t - tp; tp = t; }
         // rows: z~ = A x~, relax, project, y, w
         if (tid < MR) {
             double xv[K], av[K];
@@ -117,9 +126,10 @@ __global__ __launch_bounds__(TT, 1) void k_iter(const double* Mg, const int* col
             w[tid] = rv * zn - y;
         }
         __syncthreads();
+        { const long long t = clock64(); pc += t - tp; tp = t; }
     }
     const long long t1 = clock64();
-    if (tid == 0) cyc[blockIdx.x] = t1 - t0;
+    if (tid == 0) { cyc[blockIdx.x] = t1 - t0; ph[3 * blockIdx.x] = pa; ph[3 * blockIdx.x + 1] = pb; ph[3 * blockIdx.x + 2] = pc; }
     if (tid < MR) out[blockIdx.x * 1024 + tid] = Z + X;
 }
 
@@ -238,17 +248,26 @@ int main() {
     CK(hipMemcpy(dc, colg.data(), 4 * K * NP, hipMemcpyHostToDevice));
     CK(hipMemcpy(dr, rowg.data(), 4 * K * MR, hipMemcpyHostToDevice));
     const size_t lds = 100000;
-    CK(hipFuncSetAttribute((const void*)k_iter, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     CK(hipFuncSetAttribute((const void*)k_sweep, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     std::vector<long long> cyc(G);
-    for (int rep = 0; rep < 2; ++rep) {
-        hipLaunchKernelGGL(k_iter, dim3(G), dim3(TT), lds, 0, dM, dc, dr, NIT, dcyc, dout);
-        CK(hipDeviceSynchronize());
-        CK(hipMemcpy(cyc.data(), dcyc, 8 * G, hipMemcpyDeviceToHost));
-        long long mx = 0, mn = cyc[0];
-        for (auto c : cyc) { mx = std::max(mx, c); mn = std::min(mn, c); }
-        printf("iteration: %.0f .. %.0f cycles (one WG per CU, %d WGs)\n", (double)mn / NIT, (double)mx / NIT, G);
-    }
+    long long* dph;
+    CK(hipMalloc(&dph, 8 * 3 * G));
+    std::vector<long long> ph(3 * G);
+    auto run = [&](auto kern, const char* what) -> int {
+        CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        for (int rep = 0; rep < 2; ++rep) {
+            hipLaunchKernelGGL(kern, dim3(G), dim3(TT), lds, 0, dM, dc, dr, NIT, dcyc, dout, dph);
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(cyc.data(), dcyc, 8 * G, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(ph.data(), dph, 8 * 3 * G, hipMemcpyDeviceToHost));
+            long long mx = 0, mn = cyc[0];
+            for (auto c : cyc) { mx = std::max(mx, c); mn = std::min(mn, c); }
+            printf("%s: iteration %.0f .. %.0f cycles; wave 0 phases rhs %.0f product %.0f rows %.0f\n", what,
+                   (double)mn / NIT, (double)mx / NIT, (double)ph[0] / NIT, (double)ph[1] / NIT, (double)ph[2] / NIT);
+        }
+        return 0;
+    };
+    if (run(k_iter<3>, "full, bank-spread b") || run(k_iter<2>, "full") || run(k_iter<1>, "no 8-lane sums") || run(k_iter<0>, "no product")) return 1;
     for (int rep = 0; rep < 2; ++rep) {
         hipLaunchKernelGGL(k_sweep, dim3(G), dim3(TT), lds, 0, dK, dMo, dcyc, 4);
         CK(hipDeviceSynchronize());
