@@ -208,8 +208,8 @@ void *mpcqp_get_stream(const mpcqp_handle *h);
  * own stream(s) and on the caller stream the last *_device call used. */
 int mpcqp_synchronize(mpcqp_handle *h);
 /* hipEvent-bracketed time of the last solve: milliseconds, or -1 when unavailable.
- * The host-pointer mpcqp_solve_batch always records it; the *_device entry points
- * only while mpcqp_timing is on (no event packet between their kernels otherwise). */
+ * Recorded only while mpcqp_timing is on, by the host-pointer mpcqp_solve_batch and the
+ * *_device entry points alike (no event packet between the kernels otherwise). */
 double mpcqp_last_kernel_ms(mpcqp_handle *h);
 
 /* Kernel timing for bench.py's roofline: while enabled, every *_device solve

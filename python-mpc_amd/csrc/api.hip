@@ -1216,12 +1216,15 @@ int mpcqp_solve_batch(mpcqp_handle* h, double* x, double* y, int32_t* status, in
     // every shard's kernels are enqueued before any result is copied back: a copy into the
     // caller's (pageable) memory blocks the host until its shard is done, so copying inside
     // the launch loop would start shard d+1 only after shard d had finished
+    // an event pair around the solve launch only while timing is on (mpcqp_timing): two event
+    // packets cost a one-QP solve() ~5.5 us of its ~150 (cfg 2, same-box A/B, profiles/r6/lat_events_ab.txt)
+    const bool evs = h->collect;
     for (auto& s : h->shards) {
         HIPCHK(hipSetDevice(s.dev));
         if (int e = stream_enter(s, s.stream)) return e;
-        HIPCHK(hipEventRecord(s.ev0, s.stream));
+        if (evs) HIPCHK(hipEventRecord(s.ev0, s.stream));
         HIPCHK(launch_solve(s.kp, s.B, s.out_x, s.out_y, 0, s.stream));
-        HIPCHK(hipEventRecord(s.ev1, s.stream));
+        if (evs) HIPCHK(hipEventRecord(s.ev1, s.stream));
         HIPCHK(launch_order(s.kp, s.B, s.stream));
         if (int e = stream_leave(s, s.stream)) return e;
     }
@@ -1287,7 +1290,7 @@ int mpcqp_solve_batch(mpcqp_handle* h, double* x, double* y, int32_t* status, in
     h->staged = all_staged;
     float ms = 0.f;
     h->last_ms = -1.0;
-    if (h->shards.size() == 1 && hipEventElapsedTime(&ms, h->shards[0].ev0, h->shards[0].ev1) == hipSuccess) {
+    if (evs && h->shards.size() == 1 && hipEventElapsedTime(&ms, h->shards[0].ev0, h->shards[0].ev1) == hipSuccess) {
         h->last_ms = ms;
         h->last_pair = {h->shards[0].ev0, h->shards[0].ev1};
     }
