@@ -81,6 +81,10 @@ def parse(argv=None):
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--separate-setup", action="store_true",
                     help="setup() and solve() as two kernels (default: mpcqp_setup_solve_device, fused where possible)")
+    ap.add_argument("--one-shot", action=argparse.BooleanOptionalAction, default=True,
+                    help="mpcqp_set_one_shot (default on): the fused kernel keeps no workspace state for later "
+                         "calls -- the reference's fresh OSQP() + setup() + solve() per call "
+                         "(mpc_kinematics.py:194-198); outputs bit-identical to --no-one-shot's persisting kernel")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no HIP events in the timed region (roofline kernel_ms from the untimed pass)")
     ap.add_argument("--no-dispatch-ab", action="store_true",
@@ -246,14 +250,15 @@ def solve_kernel_name(info, fused):
             16: "mpcqp::k_solve_d"}.get(v, "mpcqp::k_solve")
 
 
-def pmc_traffic(workload, batch, kernel):
+def pmc_traffic(workload, batch, kernel, one_shot=False):
     """HBM bytes per k_solve launch from rocprofv3 PMC passes committed under
     profiles/ (tools/gpu_profile.sh + tools/pmc_summary.py give traffic.json, copied to profiles/traffic_<workload>_b<B>.json:
     FETCH_SIZE and WRITE_SIZE from separate --pmc passes, FETCH_SIZE doubled per
     the gfx950 note of MI355X_MICROARCH.md).  {} when not measured.  The record names the code it
     was measured on (code_sha16: tools/codeobj.py's hash of every instantiation of the kernel in the
-    library); when that is not the loaded library's, the record is stale -- {"traffic_stale": True}."""
-    path = os.path.join(ROOT, "profiles", f"traffic_{workload}_b{batch}.json")
+    library); when that is not the loaded library's, the record is stale -- {"traffic_stale": True}.
+    one_shot: the one-shot form's record (traffic_<workload>_b<B>_oneshot.json)."""
+    path = os.path.join(ROOT, "profiles", f"traffic_{workload}_b{batch}{'_oneshot' if one_shot else ''}.json")
     if not os.path.exists(path):
         return {}
     with open(path) as f:
@@ -556,6 +561,8 @@ def main(argv=None, solver_cls=None, device=None):
     dsync()
     solver = Solver(P, A, B, device=local, **settings)
     warm = args.config == 5
+    one_shot = bool(args.one_shot and not warm and not args.separate_setup and hasattr(solver, "one_shot")
+                    and solver.one_shot(True))
     xs = ys = None
     if warm:
         # SURVEY.md §8d D2, cfg 5 ("warm-started ADMM"): solve once cold, shift the solution
@@ -653,6 +660,8 @@ def main(argv=None, solver_cls=None, device=None):
         os.environ["MPCQP_DISPATCH"] = "identity"
         ident = Solver(P, A, B, device=local, **settings)
         del os.environ["MPCQP_DISPATCH"]
+        if one_shot:
+            ident.one_shot(True)
         for t in range(1 + args.warmup):
             step(t, ident)
         ident.synchronize()
@@ -726,7 +735,7 @@ def main(argv=None, solver_cls=None, device=None):
     flop_iter = 2 * (3 * info["nb"] * S * S + 2 * nnzA) + 12 * (n + m)
     fp64_tflops = flop_iter * float(iters_last.astype(np.float64).sum()) / (solve_ms * 1e-3) / 1e12
 
-    traffic = pmc_traffic(spec["name"], B, solve_kernel_name(info, fused=fused))
+    traffic = pmc_traffic(spec["name"], B, solve_kernel_name(info, fused=fused), one_shot)
     copy_gbs = copy_peak(local) if (on_gpu and rank == 0 and not args.no_cpu) else None
 
     cpu = None
@@ -794,10 +803,12 @@ def main(argv=None, solver_cls=None, device=None):
                        "eps_abs": 1e-3, "eps_rel": 1e-3,
                        "step": ("setup()+warm_start(base solution shifted one stage)+solve()" if warm else
                                 "setup()+solve()" + ("" if args.separate_setup else
-                                                     f" (mpcqp_setup_solve_device: one call; kernel {kname})"))
+                                                     f" (mpcqp_setup_solve_device: one call; kernel {kname}"
+                                                     + (", one-shot: no workspace state kept)" if one_shot else ")")))
                                + " per instance, inputs resident in HBM; a distinct batch per step (" +
                                ("initial states drawn afresh)" if args.independent else
                                 f"initial states jittered +-{args.jitter:.0%} of the D2 ranges)"),
+                       "one_shot": one_shot,
                        "parallelism": f"batch-shard x{world}",
                        "dispatch": "longest previous solve first (kernels.hip::k_order), predicted from the "
                                    "previous step's different batch",

@@ -128,9 +128,20 @@ struct mpcqp_handle {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_setup, ev_solve;
     std::pair<hipEvent_t, hipEvent_t> last_pair{nullptr, nullptr};  // events of the last device solve
     bool staged = false;  // every shard's hstage holds the last mpcqp_solve_batch's results
+    bool one_shot = false;    // mpcqp_set_one_shot: setup_solve_device persists no workspace state
+    bool state_gone = false;  // the last setup was one-shot: calls that read the workspace refuse
 };
 
 namespace {
+
+// calls that read what a setup leaves in the workspace (the scaled data, the iterates, the
+// certificates) after a one-shot setup + solve, which left none of it
+int need_state(const mpcqp_handle* h, const char* what) {
+    if (h && h->state_gone)
+        return fail(MPCQP_EINVAL, "%s: the last setup was one-shot (mpcqp_set_one_shot): the workspace keeps no "
+                    "state; call a setup first", what);
+    return 0;
+}
 
 template <class T>
 size_t carve(size_t& off, size_t count) {
@@ -1016,6 +1027,7 @@ int mpcqp_setup_batch(int32_t n, int32_t m, const int32_t* Pp, const int32_t* Pi
 }
 
 int mpcqp_update_batch(mpcqp_handle* h, const double* q, const double* l, const double* u) {
+    if (int e = need_state(h, "mpcqp_update_batch")) return e;
     if (!h) return fail(MPCQP_EINVAL, "NULL handle");
     h->staged = false;  // (device work: the staged results of the last solve are stale)
     if (l && u)
@@ -1077,6 +1089,7 @@ int mpcqp_update_batch(mpcqp_handle* h, const double* q, const double* l, const 
 
 int mpcqp_update_matrices_batch(mpcqp_handle* h, const double* Px, const int32_t* Px_idx, int32_t nPx,
                                 const double* Ax, const int32_t* Ax_idx, int32_t nAx) {
+    if (int e = need_state(h, "mpcqp_update_matrices_batch")) return e;
     if (!h) return fail(MPCQP_EINVAL, "NULL handle");
     h->staged = false;  // (device work: the staged results of the last solve are stale)
     if (!Px && !Ax) return fail(MPCQP_EINVAL, "no matrix values given");
@@ -1194,6 +1207,7 @@ int mpcqp_update_settings(mpcqp_handle* h, const mpcqp_settings* s, int32_t set_
 }
 
 int mpcqp_warm_start_batch(mpcqp_handle* h, const double* x, const double* y) {
+    if (int e = need_state(h, "mpcqp_warm_start_batch")) return e;
     if (!h) return fail(MPCQP_EINVAL, "NULL handle");
     h->staged = false;  // (device work: the staged results of the last solve are stale)
     const long n = h->n, m = h->m;
@@ -1211,6 +1225,7 @@ int mpcqp_warm_start_batch(mpcqp_handle* h, const double* x, const double* y) {
 }
 
 int mpcqp_solve_batch(mpcqp_handle* h, double* x, double* y, int32_t* status, int32_t* iters) {
+    if (int e = need_state(h, "mpcqp_solve_batch")) return e;
     if (!h) return fail(MPCQP_EINVAL, "NULL handle");
     const long n = h->n, m = h->m;
     // every shard's kernels are enqueued before any result is copied back: a copy into the
@@ -1342,6 +1357,7 @@ int mpcqp_get_polish_status(mpcqp_handle* h, int32_t* status_polish) {
 }
 
 int mpcqp_get_certificates(mpcqp_handle* h, double* prim_inf_cert, double* dual_inf_cert) {
+    if (int e = need_state(h, "mpcqp_get_certificates")) return e;
     if (!h) return fail(MPCQP_EINVAL, "NULL handle");
     if (h->staged) {
         for (auto& s : h->shards) {
@@ -1399,10 +1415,12 @@ int mpcqp_setup_device(mpcqp_handle* h, const double* dPx, const double* dAx, co
     HIPCHK(launch_setup(s.kp, s.B, dPx, dAx, dq, dl, du, st));
     if (h->collect_setup)
         if (int e = ev_end(h->collect_setup, h->ev_setup, st)) return e;
+    h->state_gone = false;
     return stream_leave(s, st);
 }
 
 int mpcqp_update_device(mpcqp_handle* h, const double* dq, const double* dl, const double* du, void* stream) {
+    if (int e = need_state(h, "mpcqp_update_device")) return e;
     if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "device entry points need a single-device handle");
     h->staged = false;  // (device work: the staged results of the last solve are stale)
     Shard& s = h->shards[0];
@@ -1414,6 +1432,7 @@ int mpcqp_update_device(mpcqp_handle* h, const double* dq, const double* dl, con
 }
 
 int mpcqp_warm_start_device(mpcqp_handle* h, const double* dx, const double* dy, void* stream) {
+    if (int e = need_state(h, "mpcqp_warm_start_device")) return e;
     if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "device entry points need a single-device handle");
     h->staged = false;  // (device work: the staged results of the last solve are stale)
     Shard& s = h->shards[0];
@@ -1427,6 +1446,7 @@ int mpcqp_warm_start_device(mpcqp_handle* h, const double* dx, const double* dy,
 }
 
 int mpcqp_solve_device(mpcqp_handle* h, double* dx, double* dy, int32_t* dstatus, int32_t* diters, void* stream) {
+    if (int e = need_state(h, "mpcqp_solve_device")) return e;
     if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "device entry points need a single-device handle");
     h->staged = false;  // (device work: the staged results of the last solve are stale)
     Shard& s = h->shards[0];
@@ -1466,7 +1486,9 @@ int mpcqp_setup_solve_device(mpcqp_handle* h, const double* dPx, const double* d
     KParams k = s.kp;
     k.ostat = dstatus;
     k.oiter = diters;
-    HIPCHK(launch_setup_solve(k, s.B, dPx, dAx, dq, dl, du, dx, dy, st));
+    const bool one = h->one_shot && one_shot_form(k) > 0;
+    HIPCHK(launch_setup_solve(k, s.B, dPx, dAx, dq, dl, du, dx, dy, st, one));
+    h->state_gone = one;
     if (h->collect) {
         if (int e = ev_end(h->collect, h->ev_solve, st)) return e;
         h->last_pair = h->ev_solve.back();
@@ -1478,6 +1500,16 @@ int mpcqp_setup_solve_device(mpcqp_handle* h, const double* dPx, const double* d
 
 void* mpcqp_get_stream(const mpcqp_handle* h) {
     return (h && !h->shards.empty()) ? (void*)h->shards[0].stream : nullptr;
+}
+
+int mpcqp_set_one_shot(mpcqp_handle* h, int32_t on) {
+    if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "device entry points need a single-device handle");
+    h->one_shot = on != 0;
+    return 0;
+}
+
+int mpcqp_one_shot_applies(const mpcqp_handle* h) {
+    return (h && h->shards.size() == 1) ? one_shot_form(h->shards[0].kp) : 0;
 }
 
 int mpcqp_set_shared_matrices(mpcqp_handle* h, int32_t shared) {

@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include "device_common.h"
+#include "solve_phases.h"
 #include "wave_util.h"
 
 namespace mpcqp {
@@ -30,7 +31,11 @@ __host__ __device__ inline size_t lds_setup_r_bytes(int nnzP, int nnzA, int npad
     return sizeof(double) * ((size_t)nnzP + 1 + nnzA + 1 + npad + m + (tt > 512 ? tt / 64 : 8)) + 16;
 }
 
-template <int TT, int K, int KP, int RS, int AS, int PS, bool KEEP = false>
+// ONE (the one-shot fused setup + solve, mpcqp_set_one_shot): the scaled problem is left in LDS
+// where the solve kernel's carve keeps it (solve_phases.h::carve: A, P, bounds, row classes,
+// q, x = z = 0) instead of in the workspace -- no later call reads it there; D, E, c and the
+// status slots are written as always
+template <int TT, int K, int KP, int RS, int AS, int PS, bool KEEP = false, bool ONE = false>
 __device__ __forceinline__ void setup_r_body(const KParams& p, const long b, const double* __restrict__ Px_in,
                                              const double* __restrict__ Ax_in, const double* __restrict__ q_in,
                                              const double* __restrict__ l_in, const double* __restrict__ u_in,
@@ -165,9 +170,13 @@ __device__ __forceinline__ void setup_r_body(const KParams& p, const long b, con
     // bounds: clip to +-OSQP_INFTY (python wrapper), validate, scale, classify
     bool bad = false;
     const double rho = cmin(cmax(p.rho0, RHO_MIN), RHO_MAX);
+    double lo1[RS], up1[RS];   // (ONE: staged for the solve's LDS carve)
+    signed char ct1[RS];
 #pragma unroll
     for (int s = 0; s < RS; ++s) {
         const int i = tid + s * TT;
+        lo1[s] = up1[s] = 0.0;
+        ct1[s] = 0;
         if (i < m) {
             double li = cmax(l_in[b * m + i], -OSQP_INFTY);
             double ui = cmin(u_in[b * m + i], OSQP_INFTY);
@@ -178,10 +187,16 @@ __device__ __forceinline__ void setup_r_body(const KParams& p, const long b, con
             if (li < -OSQP_INFTY * MIN_SCALING && ui > OSQP_INFTY * MIN_SCALING) t = -1;
             else if (ui - li < RHO_TOL) t = 1;
             else t = 0;
-            p.l[b * m + i] = li;
-            p.u[b * m + i] = ui;
+            if constexpr (ONE) {
+                lo1[s] = li;
+                up1[s] = ui;
+                ct1[s] = t;
+            } else {
+                p.l[b * m + i] = li;
+                p.u[b * m + i] = ui;
+            }
             p.E[b * m + i] = Ev[s];
-            if (!KEEP) {
+            if (!KEEP && !ONE) {
                 p.ct[b * m + i] = t;
                 p.z[b * m + i] = 0.0;
                 p.y[b * m + i] = 0.0;
@@ -189,12 +204,52 @@ __device__ __forceinline__ void setup_r_body(const KParams& p, const long b, con
         }
     }
     bad = block_any<TT>(bad, flag);
-    for (int v = tid; v < nnzP; v += TT) p.Px[b * nnzP + v] = Pv[v];
-    for (int e = tid; e < nnzA; e += TT) p.Ax[b * nnzA + e] = Ac[e];
+    if constexpr (ONE) {
+        // the scaled data into the solve's carve: every value is read into registers first
+        // (the two layouts overlap), then written after a barrier
+        static_assert(!KEEP, "a matrix update keeps the workspace");
+        double av1[AS], pv1[PS];
+#pragma unroll
+        for (int s = 0; s < AS; ++s) av1[s] = tid + s * TT < nnzA ? Ac[tid + s * TT] : 0.0;
+#pragma unroll
+        for (int s = 0; s < PS; ++s) pv1[s] = tid + s * TT < nnzP ? Pv[tid + s * TT] : 0.0;
+        __syncthreads();
+        SL2 C = carve(p);
+#pragma unroll
+        for (int s = 0; s < AS; ++s)
+            if (tid + s * TT < nnzA) C.L.Acsc[tid + s * TT] = av1[s];
+#pragma unroll
+        for (int s = 0; s < PS; ++s)
+            if (tid + s * TT < nnzP) C.L.Pv[tid + s * TT] = pv1[s];
+        const int mp = (m + 63) & ~63;  // (solve_mpad: padded rows inert, l = u = 0)
+#pragma unroll
+        for (int s = 0; s < RS; ++s) {
+            const int i = tid + s * TT;
+            if (i < mp) {
+                C.L.lo[i] = lo1[s];
+                C.L.up[i] = up1[s];
+                C.L.ct[i] = ct1[s];
+                C.Z[i] = 0.0;
+            }
+        }
+        for (int i = tid + RS * TT; i < mp; i += TT) {  // (rows past RS * TT: padding only)
+            C.L.lo[i] = 0.0;
+            C.L.up[i] = 0.0;
+            C.L.ct[i] = 0;
+            C.Z[i] = 0.0;
+        }
+        if (pc < npad) {
+            C.L.qv[pc] = qv;
+            C.X[pc] = 0.0;
+        }
+    } else {
+        for (int v = tid; v < nnzP; v += TT) p.Px[b * nnzP + v] = Pv[v];
+        for (int e = tid; e < nnzA; e += TT) p.Ax[b * nnzA + e] = Ac[e];
+    }
     if (pc < npad) {
-        p.q[b * npad + pc] = qv;
+        if (!ONE) p.q[b * npad + pc] = qv;
         p.D[b * npad + pc] = Dv;
-        if (!KEEP) p.x[b * npad + pc] = 0.0;
+        if (!KEEP && !ONE) p.x[b * npad + pc] = 0.0;
     }
     if (tid == 0) {
         p.scal[b * 4 + 0] = c;

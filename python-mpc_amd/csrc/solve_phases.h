@@ -1483,8 +1483,11 @@ __device__ __noinline__ void objective_nl(const KParams* gp, double cinv) {
     objective_ph<TT>(gp, cinv);
 }
 
-// store_solution + info (y is in ys)
-template <int TT>
+// store_solution + info (y is in ys).  ONE (the one-shot fused setup + solve, mpcqp_set_one_shot):
+// no later call reads the workspace, so the warm-start iterates x, z, y and the infeasibility
+// certificates are not stored -- the outputs, the status / iteration count (the next dispatch
+// order) and the info are
+template <int TT, bool ONE = false>
 __device__ __forceinline__ void finalize_ph(const KParams* gp, long b, double* __restrict__ xo,
                                          double* __restrict__ yo, double cinv, double rho, int status,
                                          int info_iter, int rho_updates, int* ostat, int* oiter) {
@@ -1532,17 +1535,19 @@ __device__ __forceinline__ void finalize_ph(const KParams* gp, long b, double* _
         const double xv = c.X[pc];
         if (j >= 0) {
             if (xo) xo[b * n + j] = has_sol ? (p.scaling ? Dg[pc] * xv : xv) : __builtin_nan("");
-            p.dxc[b * n + j] = dinf ? c.L.dx[pc] * (1.0 / nrm[1]) : c.L.dx[pc];
+            if (!ONE) p.dxc[b * n + j] = dinf ? c.L.dx[pc] * (1.0 / nrm[1]) : c.L.dx[pc];
         }
-        p.x[b * npad + pc] = has_sol ? xv : 0.0;
+        if (!ONE) p.x[b * npad + pc] = has_sol ? xv : 0.0;
     }
 #pragma unroll 1
     for (int i = tid; i < m; i += TT) {
         const double yv = c.L.ys[i];
         if (yo) yo[b * m + i] = has_sol ? (p.scaling ? (Eg[i] * yv) * cinv : yv) : __builtin_nan("");
-        p.dyc[b * m + i] = pinf ? c.dY[i] * (1.0 / nrm[0]) : c.dY[i];
-        p.y[b * m + i] = has_sol ? yv : 0.0;
-        p.z[b * m + i] = has_sol ? c.Z[i] : 0.0;
+        if (!ONE) {
+            p.dyc[b * m + i] = pinf ? c.dY[i] * (1.0 / nrm[0]) : c.dY[i];
+            p.y[b * m + i] = has_sol ? yv : 0.0;
+            p.z[b * m + i] = has_sol ? c.Z[i] : 0.0;
+        }
     }
     if (tid == 0) {
         p.status[b] = status;
@@ -1557,11 +1562,11 @@ __device__ __forceinline__ void finalize_ph(const KParams* gp, long b, double* _
         p.scal[b * 4 + 2] = rho;
     }
 }
-template <int TT>
+template <int TT, bool ONE = false>
 __device__ __noinline__ void finalize_nl(const KParams* gp, long b, double* __restrict__ xo,
                                          double* __restrict__ yo, double cinv, double rho, int status,
                                          int info_iter, int rho_updates, int* ostat, int* oiter) {
-    finalize_ph<TT>(gp, b, xo, yo, cinv, rho, status, info_iter, rho_updates, ostat, oiter);
+    finalize_ph<TT, ONE>(gp, b, xo, yo, cinv, rho, status, info_iter, rho_updates, ostat, oiter);
 }
 
 template <int TT>
@@ -1584,6 +1589,14 @@ __device__ __forceinline__ bool factorize_ph(const KParams* gp, long b, double r
 template <int TT, bool ROT = false>
 __device__ __noinline__ bool factorize_nl(const KParams* gp, long b, double rho, double* sdst = nullptr) {
     return factorize_ph<TT, ROT>(gp, b, rho, sdst);
+}
+// the same with the G blocks to `hdst` (the one-shot fused kernel: an LDS region, no workspace
+// round trip) instead of the instance's H tiles
+template <int TT, bool ROT = false>
+__device__ __noinline__ bool factorize_g_nl(const KParams* gp, long b, double rho, double* sdst, double* hdst) {
+    KPc& p = kconst(gp);
+    SL2 c = carve(p);
+    return factorize<TT, KPc, false, ROT>(p, c.L, rho, p.F + b * (long)p.nb * SS, hdst, sdst);
 }
 
 

@@ -1170,7 +1170,13 @@ __device__ __forceinline__ void form_dense_rows(__attribute__((address_space(1))
 // factorisation of a solve takes setup()'s convexity factor when it is current (KParams::ffresh:
 // the factor-only launch leaves the S_k^{-1} tiles in the instance's Si region, the G blocks in H
 // and the eliminated columns' ec / ed in F); the factor-only launch (factor_only) persists them
-template <int K, int KPK, int QR, bool EL = false, int KC = K, bool DK = false, bool RU = false>
+// ONE (the one-shot fused kernel, mpcqp_set_one_shot; cold start): the setup left the scaled
+// problem in this carve (setup_r.h ONE) and finalize stores no warm-start state -- no workspace
+// round trip for data no later call reads; GL (where the LDS budget of two workgroups per CU
+// allows it, one_shot_form): the G blocks go to an LDS region after the S_k^{-1} tiles instead
+// of the instance's H tiles, and a refactorisation keeps y there instead of in the workspace
+template <int K, int KPK, int QR, bool EL = false, int KC = K, bool DK = false, bool RU = false, bool ONE = false,
+          bool GL = false>
 __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restrict__ xo, double* __restrict__ yo,
                                               int factor_only = 0) {
     static_assert(!(DK && EL), "the dense inverse covers plans without eliminated columns");
@@ -1184,7 +1190,9 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
     const int n = p.n, m = p.m, npad = p.npad, nnzP = p.nnzP, nnzA = p.nnzA;
     SL2 C = carve(p);
     SLds& L = C.L;
-    const double* Hg = p.H + b * (long)p.nb * SS;
+    // GL: the G blocks (amax x S per pair) go to LDS after the S_k^{-1} tiles
+    const double* Hg = GL ? C.L.Acsc + 2 * ((lds_base_bytes(p) + 15) / 16) + (long)NB * SS
+                           : p.H + b * (long)p.nb * SS;
     double* const Sg = C.L.Acsc + 2 * ((lds_base_bytes(p) + 15) / 16);  // S_k^{-1} tiles in LDS (lds_w2_bytes)
 
     if (p.err[b]) {
@@ -1211,22 +1219,27 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
     };
     double rho = p.scal[b * 4 + 2];
     const double sigma = p.sigma, alpha = p.alpha;
-    const bool warm = p.warm_start != 0;
-    for (int e = tid; e < nnzA; e += T4) L.Acsc[e] = p.Ax[b * nnzA + e];
-    if (tid == 0) L.Acsc[nnzA] = 0.0;
-    for (int v = tid; v < nnzP; v += T4) L.Pv[v] = p.Px[b * nnzP + v];
-    if (tid == 0) L.Pv[nnzP] = 0.0;
+    const bool warm = !ONE && p.warm_start != 0;
     const int mp = solve_mpad(m);
-    for (int i = tid; i < mp; i += T4) {
-        const bool in = i < m;
-        L.lo[i] = in ? p.l[b * m + i] : 0.0;
-        L.up[i] = in ? p.u[b * m + i] : 0.0;
-        L.ct[i] = in ? p.ct[b * m + i] : 0;
-        C.Z[i] = (in && warm) ? p.z[b * m + i] : 0.0;
-    }
-    for (int pc = tid; pc < npad; pc += T4) {
-        L.qv[pc] = p.q[b * npad + pc];
-        C.X[pc] = warm ? p.x[b * npad + pc] : 0.0;
+    if constexpr (!ONE) {
+        for (int e = tid; e < nnzA; e += T4) L.Acsc[e] = p.Ax[b * nnzA + e];
+        if (tid == 0) L.Acsc[nnzA] = 0.0;
+        for (int v = tid; v < nnzP; v += T4) L.Pv[v] = p.Px[b * nnzP + v];
+        if (tid == 0) L.Pv[nnzP] = 0.0;
+        for (int i = tid; i < mp; i += T4) {
+            const bool in = i < m;
+            L.lo[i] = in ? p.l[b * m + i] : 0.0;
+            L.up[i] = in ? p.u[b * m + i] : 0.0;
+            L.ct[i] = in ? p.ct[b * m + i] : 0;
+            C.Z[i] = (in && warm) ? p.z[b * m + i] : 0.0;
+        }
+        for (int pc = tid; pc < npad; pc += T4) {
+            L.qv[pc] = p.q[b * npad + pc];
+            C.X[pc] = warm ? p.x[b * npad + pc] : 0.0;
+        }
+    } else {
+        if (tid == 0) L.Acsc[nnzA] = 0.0;
+        if (tid == 0) L.Pv[nnzP] = 0.0;
     }
     if (tid < 8) L.cor[tid] = 0.0;        // c_0 = 0 (block 0 has no correction)
     if (tid < 8) L.cor[32 + tid] = 0.0;   // the upper half's zero correction row (phase B)
@@ -1273,8 +1286,13 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
         if (need_factor) {
             need_factor = false;
             if (iter > 0) {
-                const auto yp = opaque_gptr(p.y + b * m);
-                for (int i = tid; i < m; i += T4) yp[i] = L.ys[i];
+                if constexpr (GL) {  // (y kept on chip, after the G blocks)
+                    double* const ysv = Sg + (long)NB * SS + (long)(NB * (NB - 1) / 2) * p.amax * S;
+                    for (int i = tid; i < m; i += T4) ysv[i] = L.ys[i];
+                } else {
+                    const auto yp = opaque_gptr(p.y + b * m);
+                    for (int i = tid; i < m; i += T4) yp[i] = L.ys[i];
+                }
                 __syncthreads();  // every ys read is done before factorize_w4's E tiles overwrite it
             }
             // the slack layouts' (EL) factorisation with rotated tile rows: cfg 3
@@ -1294,6 +1312,8 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 }
                 __syncthreads();
                 if (tid == 0) p.ffresh[b] = 0;
+            } else if constexpr (GL) {
+                ok = factorize_g_nl<T4, EL>(p.self, b, rho, Sg, Sg + (long)NB * SS);
             } else {
                 ok = factorize_nl<T4, EL>(p.self, b, rho, Sg);
             }
@@ -1320,7 +1340,10 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
             }
             __syncthreads();
             const bool have_y = iter > 0 || warm;
-            {
+            if constexpr (GL) {
+                const double* const ysv = Sg + (long)NB * SS + (long)(NB * (NB - 1) / 2) * p.amax * S;
+                for (int i = tid; i < mp; i += T4) L.ys[i] = (have_y && i < m) ? ysv[i] : 0.0;
+            } else {
                 const auto yp = opaque_gptr(p.y + b * m);
                 for (int i = tid; i < mp; i += T4) L.ys[i] = (have_y && i < m) ? yp[i] : 0.0;
             }
@@ -1845,7 +1868,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
         status = check_termination_nl<T4>(p.self, b, cval, cinv, 1);
         if (status == MPCQP_UNSOLVED_) status = MPCQP_MAX_ITER_REACHED_;
     }
-    finalize_nl<T4>(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates, p.ostat, p.oiter);
+    finalize_nl<T4, ONE>(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates, p.ostat, p.oiter);
 #ifdef MPCQP_PHASE_PROF
     if (prof) {
         __syncthreads();
@@ -1875,8 +1898,10 @@ __global__ __launch_bounds__(T4, 2) void k_solve_w4(KParams p, double* __restric
     order_epilogue<T4>(p, (int*)sm);
 }
 
-// setup (setup_r.h with 256 threads: one column and one row per thread) + solve
-template <int K, int KPK, int QR, int SK, int SAS, bool EL = false, int KC = K, bool DK = false>
+// setup (setup_r.h with 256 threads: one column and one row per thread) + solve; ONE: the
+// one-shot form (solve_w4_body)
+template <int K, int KPK, int QR, int SK, int SAS, bool EL = false, int KC = K, bool DK = false, bool ONE = false,
+          bool GL = false>
 __global__ __launch_bounds__(T4, 2) void k_setup_solve_w4(KParams p, const double* __restrict__ Px_in,
                                                           const double* __restrict__ Ax_in,
                                                           const double* __restrict__ q_in,
@@ -1884,9 +1909,9 @@ __global__ __launch_bounds__(T4, 2) void k_setup_solve_w4(KParams p, const doubl
                                                           const double* __restrict__ u_in, double* __restrict__ xo,
                                                           double* __restrict__ yo) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    setup_r_body<T4, SK, 4, 1, SAS, 1>(p, instance_of(p), Px_in, Ax_in, q_in, l_in, u_in, sm);
+    setup_r_body<T4, SK, 4, 1, SAS, 1, false, ONE>(p, instance_of(p), Px_in, Ax_in, q_in, l_in, u_in, sm);
     __syncthreads();
-    solve_w4_body<K, KPK, QR, EL, KC, DK>(p, xo, yo);
+    solve_w4_body<K, KPK, QR, EL, KC, DK, false, ONE, GL>(p, xo, yo);
     order_epilogue<T4>(p, (int*)sm);
 }
 
@@ -2428,8 +2453,39 @@ static int setup_solve_fits(const KParams& p) {
            p.nnzP <= 2 * T2;
 }
 
+int one_shot_form(const KParams& p, size_t* lds) {
+    if (p.variant != 17 || p.polish || !setup_solve_fits(p)) return 0;
+    const size_t base = std::max(lds_w2_bytes(p), lds_setup_r_bytes(p.nnzP, p.nnzA, p.npad, p.m));
+    // (form 2: the G blocks and the y of a refactorisation, which the factorisation's E tiles
+    // overwrite in the carve, after the S_k^{-1} tiles)
+    const size_t g = sizeof(double) * ((size_t)(p.nb * (p.nb - 1) / 2) * p.amax * S + (size_t)p.m);
+    const int form = base + g <= 80 * 1024 ? 2 : 1;  // (two workgroups per CU, as the persisting kernel)
+    if (lds) *lds = form == 2 ? base + g : base;
+    return form;
+}
+
 hipError_t launch_setup_solve(const KParams& p, long B, const double* Px, const double* Ax, const double* q,
-                              const double* l, const double* u, double* xo, double* yo, hipStream_t st) {
+                              const double* l, const double* u, double* xo, double* yo, hipStream_t st,
+                              bool one_shot) {
+    size_t lds1 = 0;
+    const int form = one_shot ? one_shot_form(p, &lds1) : 0;
+    if (form) {
+        decltype(&k_setup_solve_w4<6, 4, 5, 6, 2>) k4;
+        if (form == 2)
+            k4 = p.ne ? k_setup_solve_w4<6, 4, 8, 8, 3, true, 8, false, true, true>
+                      : (p.amax <= 5 ? k_setup_solve_w4<6, 4, 5, 6, 2, false, 6, false, true, true>
+                                     : k_setup_solve_w4<6, 4, 8, 6, 2, false, 6, false, true, true>);
+        else
+            k4 = p.ne ? k_setup_solve_w4<6, 4, 8, 8, 3, true, 8, false, true>
+                      : (p.amax <= 5 ? k_setup_solve_w4<6, 4, 5, 6, 2, false, 6, false, true>
+                                     : k_setup_solve_w4<6, 4, 8, 6, 2, false, 6, false, true>);
+        hipError_t e = lists_fit(p, 6, p.ne ? 8 : 6, 4, p.ne || p.amax > 5 ? 8 : 5);
+        if (e != hipSuccess) return e;
+        e = hipFuncSetAttribute((const void*)k4, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k4, dim3((unsigned)B), dim3(T4), lds1, st, p, Px, Ax, q, l, u, xo, yo);
+        return hipGetLastError();
+    }
 #ifdef MPCQP_EXPERIMENTAL
     if (p.variant == 19) {
         hipError_t e = launch_setup_solve_heavy(p, B, Px, Ax, q, l, u, xo, yo, st);

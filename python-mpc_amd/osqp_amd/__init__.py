@@ -137,6 +137,8 @@ def lib():
     L.mpcqp_solve_device.argtypes = [vp, vp, vp, vp, vp, vp]
     L.mpcqp_synchronize.argtypes = [vp]
     L.mpcqp_set_shared_matrices.argtypes = [vp, C.c_int32]
+    L.mpcqp_set_one_shot.argtypes = [vp, C.c_int32]
+    L.mpcqp_one_shot_applies.argtypes = [vp]
     L.mpcqp_get_stream.argtypes = [vp]
     L.mpcqp_get_stream.restype = vp
     L.mpcqp_last_kernel_ms.argtypes = [vp]
@@ -620,6 +622,15 @@ class DeviceBatch:
         _check(lib().mpcqp_setup_solve_device(self._h.ptr, self._ptr(Px), self._ptr(Ax), self._ptr(q), self._ptr(l),
                                               self._ptr(u), self._ptr(x), self._ptr(y), self._ptr(status),
                                               self._ptr(iters), stream), "setup_solve_device")
+
+    def one_shot(self, on=True):
+        """mpcqp_set_one_shot: setup_solve keeps no workspace state (the scaled problem, the G
+        blocks, the warm-start iterates, the certificates) for later calls -- the Control/MPC
+        pattern of a fresh setup() + solve() per call.  Returns the form that applies to this
+        handle's kernel: 0 none (not the fused four-wave kernel), 1 the G blocks in the workspace,
+        2 the G blocks on chip (mpcqp_one_shot_applies)."""
+        _check(lib().mpcqp_set_one_shot(self._h.ptr, int(on)), "set_one_shot")
+        return int(lib().mpcqp_one_shot_applies(self._h.ptr))
 
     def synchronize(self):
         _check(lib().mpcqp_synchronize(self._h.ptr), "synchronize")

@@ -295,9 +295,11 @@ def test_null_handle_is_einval():
         lambda: L.mpcqp_get_info_batch(null, None, None, None, None, None),
         lambda: L.mpcqp_get_certificates(null, None, None),
         lambda: L.mpcqp_synchronize(null),
+        lambda: L.mpcqp_set_one_shot(null, 1),
     ]
     for c in calls:
         assert c() == 1  # MPCQP_EINVAL (include/mpcqp.h)
+    assert L.mpcqp_one_shot_applies(null) == 0
     with pytest.raises(ValueError, match="not initialized"):
         osqp_amd.OSQP().update_settings(eps_abs=1e-4)
     with pytest.raises(ValueError, match="not initialized"):
