@@ -402,6 +402,7 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io, bool sync = true) {
     k.ffresh = (int*)(base + carve<int>(off, B));  // zero from the memset above
     k.reuse = !(getenv("MPCQP_FACTOR_REUSE") && getenv("MPCQP_FACTOR_REUSE")[0] == '0');
     k.apart = !(getenv("MPCQP_MIDDLE_APART") && getenv("MPCQP_MIDDLE_APART")[0] == '0');
+    k.lchain = !(getenv("MPCQP_LDS_CHAIN") && getenv("MPCQP_LDS_CHAIN")[0] == '0');
     {  // dispatch order (kernels.hip::k_order), identity until the first solve
         int* ord = (int*)(base + carve<int>(off, B));
         HIPCHK(launch_iota(ord, B, s.stream));

@@ -83,6 +83,9 @@ struct KParams {
     // setup calls: P and A values shared by every instance (Px[nnzP], Ax[nnzA] instead of
     // B copies; LTI MPC -- mpcqp_set_shared_matrices)
     int mat_shared;
+    // k_solve_b's factorisation chain runs on LDS copies of its tiles (solve_big.hip::
+    // factorize2s_lds_chain; MPCQP_LDS_CHAIN=0: the workspace form, A/B)
+    int lchain;
 };
 constexpr long kOrderFuseMax = 16384;  // larger batches sort in k_order (1024 threads)
 

@@ -246,7 +246,8 @@ __device__ __forceinline__ bool factorize2(const KP& p, SLds& L, double* __restr
 // pivot.  buf: 2 S doubles of LDS.
 __device__ __forceinline__ bool gj_rows(double* __restrict__ T, double* __restrict__ buf, const unsigned piv,
                                         const unsigned done, const double* __restrict__ dl, const int o1, const int n1,
-                                        const double* __restrict__ dl2, const int o2, const int n2) {
+                                        const double* __restrict__ dl2, const int o2, const int n2,
+                                        double* __restrict__ T2 = nullptr) {
     const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
     double v[16];
 #pragma unroll
@@ -310,7 +311,173 @@ __device__ __forceinline__ bool gj_rows(double* __restrict__ T, double* __restri
     }
 #pragma unroll
     for (int jj = 0; jj < 16; jj += 2) *(double2*)(T + i * S + 16 * h + jj) = make_double2(sc * v[jj], sc * v[jj + 1]);
+    if (T2)  // (a second copy: the LDS chain's workspace write-back)
+#pragma unroll
+        for (int jj = 0; jj < 16; jj += 2)
+            *(double2*)(T2 + i * S + 16 * h + jj) = make_double2(sc * v[jj], sc * v[jj + 1]);
     return minpiv > 0.0;
+}
+
+// A barrier that orders LDS only: the chain's workspace stores (the write-back of S_k^{-1},
+// F_k, G_k) are read by nothing before the factorisation's closing __syncthreads, so no barrier
+// of the chain waits for them to land
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// factorize2s's chain with its operands in LDS (round 6).  In the workspace form every step
+// waited on HBM / L2 round trips: the product read S_{k-1}^{-1} back from the workspace tile
+// the previous step's pivots had just stored, the corner pivots loaded their tile from the
+// workspace, and every __syncthreads after a workspace store waited for it to land.  Here
+//   * the tile a step pivots (stage 1's S_k in the workspace) and the E_k coupling block of
+//     the next step (amax x bmax of E_k, row stride 16) are loaded while the products run;
+//   * the corner pivots run on the LDS tile and store the result twice: LDS (the next step's
+//     S_{k-1}^{-1}) and the workspace (the solve's factor; never read back here);
+//   * the barriers order LDS only (lds_barrier).
+// Same sums in the same order on the same values: the factor is bit-identical to the
+// workspace form's.  Xl: two tiles per chain (prev / current), two E blocks per chain.
+template <int TT, class KP>
+__device__ __forceinline__ bool factorize2s_lds_chain(const KP& p, SLds& L, double* __restrict__ Fg,
+                                                      double* __restrict__ Hg, double* __restrict__ Sg,
+                                                      double* __restrict__ Xl, const int ntop, const int nbot,
+                                                      const int nst, bool okw) {
+    constexpr int NW = TT / 64, HT = TT / 2;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, half = tid / HT, u = tid % HT;
+    const int nb = p.nb, amax = p.amax, bmax = p.bmax, pm = p.pmeet;
+    double* const Fl = L.SP;
+    double* const Gl = L.SP + 16 * S;
+    double* const dlt = L.SP + 32 * S;
+    double* const dlb = dlt + 256;
+    double* const bufw = dlb + 256 + w * 2 * S;
+    double* const tT = Xl;             // top tiles [2][SS]
+    double* const tB = Xl + 2 * SS;    // bottom tiles [2][SS]
+    double* const eT = Xl + 4 * SS;    // top E blocks [2][256]
+    double* const eB = eT + 512;       // bottom E blocks [2][256]
+    auto rows = [&](int a, int n) -> unsigned { return n <= 0 ? 0u : (((n >= 32 ? ~0u : ((1u << n) - 1u))) << a); };
+    // the chains' blocks at step s (-1: none)
+    auto top_k = [&](int s) { return s == nst + 1 ? (pm > 0 ? pm : -1) : (s <= ntop ? s : -1); };
+    auto bot_k = [&](int s) { return s == nst + 1 ? (pm < nb - 1 ? pm : -1) : (s <= nbot ? nb - 1 - s : -1); };
+    // E block of step s: element i of the half's 256 (row i / 16, column i % 16)
+    constexpr int NE = 256 / HT;
+    auto e_load = [&](int s, int i) -> double {
+        const int r = i >> 4, c = i & 15;
+        if (half == 0) {
+            const int kt = top_k(s);
+            if (kt < 0 || r >= amax || c >= bmax) return 0.0;
+            return Fg[(long)kt * SS + r * S + p.toff[kt - 1] + c];
+        }
+        const int kb = bot_k(s);
+        if (kb < 0 || r >= amax || c >= bmax) return 0.0;
+        return Fg[(long)(kb + 1) * SS + r * S + p.toff[kb] + c];
+    };
+    // chain start: the end blocks' inverses (stage 1) as the first steps' S_{k-1}^{-1} / T_{k+1}^{-1},
+    // and the first step's E blocks
+    {
+        const double* src = half == 0 ? Sg : Sg + (long)(nb - 1) * SS;
+        double* dst = half == 0 ? tT : tB;
+        for (int e = 2 * u; e < SS; e += 2 * HT) *(double2*)(dst + e) = *(const double2*)(src + e);
+#pragma unroll
+        for (int q = 0; q < NE; ++q) (half == 0 ? eT : eB)[u + q * HT] = e_load(1, u + q * HT);
+    }
+    lds_barrier();
+    int pT = 0, pB = 0, qe = 0;  // prev tile of each chain, current E block
+#pragma unroll 1
+    for (int s = 1; s <= nst + 1; ++s) {
+        const bool mid = s == nst + 1;
+        const int kt = mid ? pm : s, kb = mid ? pm : nb - 1 - s;
+        const bool top = mid ? pm > 0 : s <= ntop;
+        const bool bot = mid ? pm < nb - 1 : s <= nbot;
+        // this step's tile (stage 1's S_k in the workspace): the top half loads the top (or
+        // middle) block, the bottom half the bottom one -- in flight under the products
+        const bool ldt = half == 0 ? (top || mid) : (bot && !mid);
+        const double* tsrc = Sg + (long)(half == 0 ? kt : kb) * SS;
+        double2 tv[SS / (2 * HT)];
+#pragma unroll
+        for (int q = 0; q < SS / (2 * HT); ++q)
+            tv[q] = ldt ? *(const double2*)(tsrc + 2 * u + q * 2 * HT) : make_double2(0.0, 0.0);
+        double en[NE];  // the next step's E block
+#pragma unroll
+        for (int q = 0; q < NE; ++q) en[q] = s <= nst ? e_load(s + 1, u + q * HT) : 0.0;
+        const double* Et = eT + qe * 256;
+        const double* Eb = eB + qe * 256;
+        // products: F_kt (top half's threads), G_kb (bottom half's)
+        if (half == 0 && top) {
+            const double* Sp = tT + pT * SS;
+            const int l0 = p.toff[kt - 1];
+            for (int o = u; o < amax * S; o += HT) {
+                const int r = o >> 5, j = o & (S - 1);
+                double sacc = 0.0;
+                for (int l = 0; l < bmax; ++l) sacc += Et[r * 16 + l] * Sp[(l0 + l) * S + j];
+                Fl[o] = sacc;
+            }
+        }
+        if (half == 1 && bot) {
+            const double* Tn = tB + pB * SS;
+            for (int o = u; o < bmax * S; o += HT) {
+                const int a = o >> 5, j = o & (S - 1);
+                double sacc = 0.0;
+                for (int r = 0; r < amax; ++r) sacc += Eb[r * 16 + a] * Tn[r * S + j];
+                Gl[o] = sacc;
+            }
+        }
+        {
+            double* td = (half == 0 ? tT + (pT ^ 1) * SS : tB + (pB ^ 1) * SS);
+            if (ldt)
+#pragma unroll
+                for (int q = 0; q < SS / (2 * HT); ++q) *(double2*)(td + 2 * u + q * 2 * HT) = tv[q];
+#pragma unroll
+            for (int q = 0; q < NE; ++q) (half == 0 ? eT : eB)[(qe ^ 1) * 256 + u + q * HT] = en[q];
+        }
+        lds_barrier();
+        // corners: -F E' (amax x amax), -G E_{kb+1} (bmax x bmax); F -> Fg[kt], G -> Hg[kb]
+        if (half == 0 && top) {
+            if (u < amax * amax) {
+                const int r = u / amax, c = u - r * amax;
+                double sacc = 0.0;
+                for (int l = 0; l < bmax; ++l) sacc += Fl[r * S + p.toff[kt - 1] + l] * Et[c * 16 + l];
+                dlt[r * 16 + c] = -sacc;
+            }
+            for (int o = u; o < amax * S; o += HT) Fg[(long)kt * SS + o] = Fl[o];
+        }
+        if (half == 1 && bot) {
+            if (u < bmax * bmax) {
+                const int a = u / bmax, c = u - a * bmax;
+                double sacc = 0.0;
+                for (int r = 0; r < amax; ++r) sacc += Gl[a * S + r] * Eb[r * 16 + c];
+                dlb[a * 16 + c] = -sacc;
+            }
+            for (int o = u; o < bmax * S; o += HT) Hg[(long)kb * SS + o] = Gl[o];
+        }
+        lds_barrier();
+        // corner pivots on the LDS tiles: wave 0 the top (or middle) block, wave NW/2 the bottom one
+        if (mid) {
+            if (w == 0) {
+                const unsigned ct = top ? rows(0, amax) : 0u;
+                const unsigned cb = bot ? rows(p.toff[pm], bmax) : 0u;
+                const unsigned all = rows(0, p.bsize[pm]);
+                okw = gj_rows(tT + (pT ^ 1) * SS, bufw, (ct | cb) & all, all & ~(ct | cb), dlt, 0, top ? amax : 0,
+                              dlb, bot ? p.toff[pm] : 0, bot ? bmax : 0, Sg + (long)pm * SS) && okw;
+            }
+        } else {
+            if (w == 0 && top) {
+                const unsigned c = rows(0, amax), all = rows(0, p.bsize[kt]);
+                okw = gj_rows(tT + (pT ^ 1) * SS, bufw, c & all, all & ~c, dlt, 0, amax, nullptr, 0, 0,
+                              Sg + (long)kt * SS) && okw;
+            }
+            if (w == NW / 2 && bot) {
+                const unsigned c = rows(p.toff[kb], bmax), all = rows(0, p.bsize[kb]);
+                okw = gj_rows(tB + (pB ^ 1) * SS, bufw, c & all, all & ~c, nullptr, 0, 0, dlb, p.toff[kb], bmax,
+                              Sg + (long)kb * SS) && okw;
+            }
+        }
+        lds_barrier();
+        if (top) pT ^= 1;
+        if (bot && !mid) pB ^= 1;
+        qe ^= 1;
+    }
+    return okw;
 }
 
 // The two-sided factorisation split like factorize_g (round 4): the Gauss-Jordan pivots that
@@ -331,9 +498,11 @@ __device__ __forceinline__ bool gj_rows(double* __restrict__ T, double* __restri
 // eight waves at once.  Same outputs as factorize2 (Sg: S_k^{-1} / M^{-1} / T_k^{-1}; Fg rows
 // < amax: F_k, k = 1..p; Hg rows < bmax: G_k, k = p..nb-2); the inverses agree at rounding
 // level (the pivot order differs).  Scratch: the LDS tiles of SLds (SP, DK, EK).
+// Xl (or null): the LDS chain (factorize2s_lds_chain) -- 4 S x S + 1024 doubles of scratch.
 template <int TT, class KP>
 __device__ __forceinline__ bool factorize2s(const KP& p, SLds& L, double rho, double* __restrict__ Fg,
-                                            double* __restrict__ Hg, double* __restrict__ Sg) {
+                                            double* __restrict__ Hg, double* __restrict__ Sg,
+                                            double* __restrict__ Xl = nullptr) {
     constexpr int NW = TT / 64, HT = TT / 2;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, half = tid / HT, u = tid % HT;
     const int nb = p.nb, amax = p.amax, bmax = p.bmax, pm = p.pmeet;
@@ -381,6 +550,9 @@ __device__ __forceinline__ bool factorize2s(const KP& p, SLds& L, double rho, do
     FPH(10)
     const int ntop = pm - 1 > 0 ? pm - 1 : 0, nbot = nb - 2 - pm > 0 ? nb - 2 - pm : 0;
     const int nst = ntop > nbot ? ntop : nbot;
+    if (Xl) {
+        okw = factorize2s_lds_chain<TT>(p, L, Fg, Hg, Sg, Xl, ntop, nbot, nst, okw);
+    } else {
     // step s: top block kt = s (s <= ntop), bottom block kb = nb - 1 - s (s <= nbot); s = nst + 1:
     // the middle block (both links)
 #pragma unroll 1
@@ -461,6 +633,7 @@ __device__ __forceinline__ bool factorize2s(const KP& p, SLds& L, double rho, do
         __syncthreads();
         FPH(11)
     }
+    }
 #undef FPH
     if (lane == 0) okf[w] = okw ? 1.0 : 0.0;
     __syncthreads();
@@ -471,6 +644,14 @@ __device__ __forceinline__ bool factorize2s(const KP& p, SLds& L, double rho, do
     return ok;
 }
 
+// the LDS chain's scratch (factorize2s_lds_chain) fits in the F / G region X2 (big_fg_len)
+template <class KP>
+__host__ __device__ inline int big_fg_len(const KP& p);
+template <class KP>
+__device__ __forceinline__ bool lds_chain_fits(const KP& p) {
+    return p.lchain && p.amax <= 16 && p.bmax <= 16 && big_fg_len(p) >= 4 * SS + 1024;
+}
+
 template <int TT, class KP>
 __device__ __noinline__ bool factorize2_nl(const KP* gp, long b, double rho, double* X2) {
     const KPc& p = kconst(gp);
@@ -478,7 +659,7 @@ __device__ __noinline__ bool factorize2_nl(const KP* gp, long b, double rho, dou
     bool ok;
     if constexpr (TT >= 256)  // (the two-wave variant 14 keeps the unsplit form)
         ok = factorize2s<TT>(p, C.L, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
-                             p.Si + b * (long)p.nb * SS);
+                             p.Si + b * (long)p.nb * SS, lds_chain_fits(p) ? X2 : nullptr);
     else
         ok = factorize2<TT>(p, C.L, X2, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
                             p.Si + b * (long)p.nb * SS);
@@ -746,7 +927,8 @@ __device__ void wave_twisted_solve(const TwoSidedW<NS>& R, const KParams& p, con
 
 // doubles of the F / G region: F_k rows (k = 1..p), G_k tail rows (k = p..nb-2), and
 // at least the four scratch tiles factorize2 needs
-__host__ __device__ inline int big_fg_len(const KParams& p) {
+template <class KP>
+__host__ __device__ inline int big_fg_len(const KP& p) {
     const int fg = (p.pmeet * p.amax + (p.nb - 1 - p.pmeet) * p.bmax) * FGS;
     return fg > 4 * SS ? fg : 4 * SS;
 }

@@ -1426,6 +1426,34 @@ def test_long_horizon_factor_reuse_is_exact(monkeypatch):
 
 
 @pytest.mark.gpu
+def test_long_horizon_lds_chain_is_exact(monkeypatch):
+    """The long-horizon factorisation's chain on LDS copies of its tiles (round 6,
+    solve_big.hip::factorize2s_lds_chain) against the workspace form (MPCQP_LDS_CHAIN=0): the
+    same sums on the same values, so cfg-5 handles of either form agree bit for bit through a
+    cold solve (setup()'s convexity factor reused), update(q) and update_settings(rho) (a
+    refactorisation at the new rho) -- and every instance is solved."""
+    b = mpc.make_batch(5, B=16, seed=23)
+    s = dict(warm_start=True, polish=False)
+    handles = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("MPCQP_LDS_CHAIN", on)
+        h = OSQPBatch()
+        h.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], **s)
+        handles.append(h)
+    monkeypatch.delenv("MPCQP_LDS_CHAIN")
+    for step, kw in enumerate([dict(), dict(q=b["q"] * 1.01), dict(rho=0.3)]):
+        for h in handles:
+            if "rho" in kw:
+                h.update_settings(**kw)
+            elif kw:
+                h.update(**kw)
+        r1, r0 = handles[0].solve(), handles[1].solve()
+        assert np.array_equal(r1.iter, r0.iter) and np.array_equal(r1.status_val, r0.status_val), step
+        assert np.array_equal(r1.x, r0.x) and np.array_equal(r1.y, r0.y), step
+        assert (r1.status_val == 1).all(), step
+
+
+@pytest.mark.gpu
 def test_long_horizon_reuse_after_a_rho_step_at_max_iter(monkeypatch):
     """a solve whose last iteration is a rho-adaptation step (max_iter a
     multiple of the rho interval) stores the new rho while the workspace factor is still the

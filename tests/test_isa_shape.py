@@ -7,8 +7,8 @@ by +-1 %, and spills or `v_readlane` reloads that appeared only on the GPU.  Thi
 code objects that ship in python-mpc_amd/osqp_amd/libmpcqp.so (tests/isa_shape.py) and fails when
 any of the recorded shapes moves:
 
-* VGPR / AGPR counts, spilled VGPRs, the scratch bytes per lane (12 B on cfg 2 and cfg 5: the
-  callee-saved SGPR-spill lanes of the out-of-line phases; 44 B with 5 spilled VGPRs on the
+* VGPR / AGPR counts, spilled VGPRs, the scratch bytes per lane (12 B on cfg 2, 48 B on cfg 5:
+  the callee-saved spill lanes of the out-of-line phases; 44 B with 5 spilled VGPRs on the
   slack layouts' eliminated-column kernel), SGPR spills at most the recorded count;
 * the ADMM loop: its instruction count, its workgroup barriers, no scratch access, and its
   `v_readlane` count (none in the four-wave loops);
@@ -31,7 +31,10 @@ PINNED = {
                  loop=dict(instructions=197, barriers=4, readlane=0, scratch=0)),
     "cfg3": dict(vgpr_count=256, agpr_count=0, vgpr_spill_count=5, private_segment_fixed_size=44, sgpr_spill_max=212,
                  loop=dict(instructions=233, barriers=4, readlane=0, scratch=0)),
-    "cfg5": dict(vgpr_count=254, agpr_count=0, vgpr_spill_count=0, private_segment_fixed_size=12, sgpr_spill_max=236,
+    # cfg 5: 48 B of scratch since the LDS factorisation chain (round 6): factorize2_nl, called
+    # once per factorisation, saves more callee-saved registers; the loop is unchanged and the
+    # same-box A/B is 254.7 k against 251.6 k solves/s (profiles/r6/lchain_ab.txt)
+    "cfg5": dict(vgpr_count=254, agpr_count=0, vgpr_spill_count=0, private_segment_fixed_size=48, sgpr_spill_max=238,
                  loop=dict(instructions=1617, barriers=21, readlane=46, scratch=0),
                  step_readlane=0, step_scratch=0),
 }

@@ -1,0 +1,47 @@
+"""Diagnostic: outputs of a cfg-5 batch (cold setup + solve, then a warm-started solve) for a
+bit-for-bit A/B of two builds or two settings of the long-horizon factorisation.
+  MPCQP_PKG=<pkg dir> python3 tools/lchain_check.py out.npz [B]
+  python3 tools/lchain_check.py --compare a.npz b.npz"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if sys.argv[1] == "--compare":
+    a, b = np.load(sys.argv[2]), np.load(sys.argv[3])
+    for k in a.files:
+        same = np.array_equal(a[k].view(np.int64) if a[k].dtype == np.float64 else a[k],
+                              b[k].view(np.int64) if b[k].dtype == np.float64 else b[k])
+        print(k, "bit-identical" if same else f"DIFFER max {np.nanmax(np.abs(a[k] - b[k]))}")
+    sys.exit(0)
+sys.path.insert(0, os.environ.get("MPCQP_PKG", os.path.join(ROOT, "python-mpc_amd")))
+import torch  # noqa: E402
+from osqp_amd import DeviceBatch, mpc, _drop_common_zeros  # noqa: E402
+
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 512
+b = mpc.make_batch(5, B=B, seed=77)
+P, Px = _drop_common_zeros(b["P"], b["Px"])
+A, Ax = _drop_common_zeros(b["A"], b["Ax"])
+s = {k: v for k, v in b["settings"].items() if k != "verbose"}
+dev = torch.device("cuda", 0)
+t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+dPx, dAx, dq, dl, du = (t(a) for a in (Px, Ax, b["q"], b["l"], b["u"]))
+torch.cuda.synchronize()
+h = DeviceBatch(P, A, B, device=0, **s)
+out = {}
+for tag in ("cold", "warm"):
+    x = torch.empty((B, b["n"]), dtype=torch.float64, device=dev)
+    y = torch.empty((B, b["m"]), dtype=torch.float64, device=dev)
+    st = torch.empty(B, dtype=torch.int32, device=dev)
+    it = torch.empty(B, dtype=torch.int32, device=dev)
+    if tag == "cold":
+        h.setup(dPx, dAx, dq, dl, du)
+    else:
+        h.update(q=dq * 1.01)
+    h.solve(x, y, st, it)
+    h.synchronize()
+    out.update({f"{tag}_x": x.cpu().numpy(), f"{tag}_y": y.cpu().numpy(), f"{tag}_st": st.cpu().numpy(),
+                f"{tag}_it": it.cpu().numpy()})
+np.savez(sys.argv[1], **out)
+print("saved", sys.argv[1], "solved", float((out["cold_st"] == 1).mean()), "iters", out["cold_it"].mean())
