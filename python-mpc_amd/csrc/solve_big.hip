@@ -273,14 +273,17 @@ __device__ __forceinline__ bool gj_rows(double* __restrict__ T, double* __restri
     double minpiv = 1.0, sc = 1.0, iv = 1.0;
     bool pivd = ((done >> i) & 1u) != 0;  // row i already pivoted
     int slot = 0;  // the publish buffer alternates between the pivots taken
-#pragma unroll 1
+    // unrolled over the 32 columns with a uniform skip of the rows not in `piv`: the pivot
+    // column is a register index known at compile time (the rolled loop's scalar switch
+    // picks, pick16 / put16, cost a multi-way branch twice per pivot)
+#pragma unroll
     for (int p = 0; p < S; ++p) {
         if (!((piv >> p) & 1u)) continue;  // (uniform)
-        const int pj = __builtin_amdgcn_readfirstlane(p & 15), ph = p >> 4;
+        const int pj = p & 15, ph = p >> 4;
         double* rb = buf + slot * S;
         slot ^= 1;
         if (h == ph) {
-            const double vp = sc * pick16(v, pj);
+            const double vp = sc * v[pj];
             rb[i] = pivd ? -vp : vp;  // row p = +-column p
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -306,7 +309,7 @@ __device__ __forceinline__ bool gj_rows(double* __restrict__ T, double* __restri
         for (int jj = 0; jj < 16; ++jj) v[jj] = __builtin_fma(-cd, rowv[jj], v[jj]);
         sc = self ? d : sc;
         iv = self ? pv : iv;
-        if (h == ph) put16(v, pj, self ? 1.0 : -cd);
+        if (h == ph) v[pj] = self ? 1.0 : -cd;
         pivd = pivd || self;
     }
 #pragma unroll
@@ -540,18 +543,21 @@ __device__ __forceinline__ bool factorize2s(const KP& p, SLds& L, double rho, do
         gsync();
         assemble_targets<false, false, true>(p, L, rho, k, D, E, lane, 64);
         gsync();
+        FPH(8)
         unsigned cut = 0;
         if (k > 0 && k <= pm) cut |= rows(0, amax);              // the link to block k-1
         if (k < nb - 1 && k >= pm) cut |= rows(p.toff[k], bmax);  // the link to block k+1
         const unsigned all = rows(0, p.bsize[k]);
         okw = gj_rows(D, bufw, all & ~cut, 0u, nullptr, 0, 0, nullptr, 0, 0) && okw;
+        FPH(10)
     }
     __syncthreads();
-    FPH(10)
+    FPH(11)
     const int ntop = pm - 1 > 0 ? pm - 1 : 0, nbot = nb - 2 - pm > 0 ? nb - 2 - pm : 0;
     const int nst = ntop > nbot ? ntop : nbot;
     if (Xl) {
         okw = factorize2s_lds_chain<TT>(p, L, Fg, Hg, Sg, Xl, ntop, nbot, nst, okw);
+        FPH(9)
     } else {
     // step s: top block kt = s (s <= ntop), bottom block kb = nb - 1 - s (s <= nbot); s = nst + 1:
     // the middle block (both links)

@@ -31,11 +31,12 @@ PINNED = {
                  loop=dict(instructions=197, barriers=4, readlane=0, scratch=0)),
     "cfg3": dict(vgpr_count=256, agpr_count=0, vgpr_spill_count=5, private_segment_fixed_size=44, sgpr_spill_max=212,
                  loop=dict(instructions=233, barriers=4, readlane=0, scratch=0)),
-    # cfg 5: 48 B of scratch since the LDS factorisation chain (round 6): factorize2_nl, called
-    # once per factorisation, saves more callee-saved registers; the loop is unchanged and the
-    # same-box A/B is 254.7 k against 251.6 k solves/s (profiles/r6/lchain_ab.txt)
-    "cfg5": dict(vgpr_count=254, agpr_count=0, vgpr_spill_count=0, private_segment_fixed_size=48, sgpr_spill_max=238,
-                 loop=dict(instructions=1617, barriers=21, readlane=46, scratch=0),
+    # cfg 5, round 6: the LDS factorisation chain and the unrolled Gauss-Jordan rows moved the
+    # callee-saved spill lanes of factorize2_nl (12 -> 44 B, once per factorisation) and the
+    # loop's register assignment (1617 -> 1606 instructions, 46 -> 39 v_readlane); same-box
+    # A/Bs 251.6 k -> 254.7 k -> 266.7 k solves/s (profiles/r6/lchain_ab.txt, gj_unroll_ab.txt)
+    "cfg5": dict(vgpr_count=254, agpr_count=0, vgpr_spill_count=0, private_segment_fixed_size=44, sgpr_spill_max=238,
+                 loop=dict(instructions=1606, barriers=21, readlane=39, scratch=0),
                  step_readlane=0, step_scratch=0),
 }
 

@@ -51,6 +51,15 @@ def main():
     pt = s.phase_times().astype(np.float64)
     it = dit.cpu().numpy().astype(np.float64)
     names = ["factor", "rhs", "bt_solve", "update", "checks", "tail"]
+    if B == 1:  # the oracle's rho-update count: factorisations = 1 + updates (the first one may be setup()'s)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle
+        o = pyoracle.OSQP()
+        Pk, Ak = P.copy(), A.copy()
+        Pk.data, Ak.data = Px[0].copy(), Ax[0].copy()
+        o.setup(Pk, b["q"][0], Ak, b["l"][0], b["u"][0], **settings)
+        r = o.solve()
+        print(f"oracle: iters {r.info.iter}, rho updates {r.info.rho_updates}")
     print(f"config {args.config} B={B} plan={s.plan_info()} kernel_ms={kt['solve_ms']:.3f}")
     slow = int(np.argmax(pt[:, 7]))
     if pt[:, 15].any():  # absolute start stamps (two-wave kernel): residency rounds and the critical instance
