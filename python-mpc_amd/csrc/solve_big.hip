@@ -349,6 +349,12 @@ __device__ __forceinline__ bool factorize2s_lds_chain(const KP& p, SLds& L, doub
     constexpr int NW = TT / 64, HT = TT / 2;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, half = tid / HT, u = tid % HT;
     const int nb = p.nb, amax = p.amax, bmax = p.bmax, pm = p.pmeet;
+#if defined(MPCQP_PHASE_PROF) && defined(MPCQP_CHAIN_STAMPS)
+    long long tc = clock64();  // (diagnostic: wave 0's products / corners / pivots, slots 8 / 10 / 11)
+#define CPH(k) if (tid == 0) { const long long t_ = clock64(); L.pacc[k] += t_ - tc; tc = t_; }
+#else
+#define CPH(k)
+#endif
     double* const Fl = L.SP;
     double* const Gl = L.SP + 16 * S;
     double* const dlt = L.SP + 32 * S;
@@ -434,6 +440,7 @@ __device__ __forceinline__ bool factorize2s_lds_chain(const KP& p, SLds& L, doub
             for (int q = 0; q < NE; ++q) (half == 0 ? eT : eB)[(qe ^ 1) * 256 + u + q * HT] = en[q];
         }
         lds_barrier();
+        CPH(8)
         // corners: -F E' (amax x amax), -G E_{kb+1} (bmax x bmax); F -> Fg[kt], G -> Hg[kb]
         if (half == 0 && top) {
             if (u < amax * amax) {
@@ -454,7 +461,8 @@ __device__ __forceinline__ bool factorize2s_lds_chain(const KP& p, SLds& L, doub
             for (int o = u; o < bmax * S; o += HT) Hg[(long)kb * SS + o] = Gl[o];
         }
         lds_barrier();
-        // corner pivots on the LDS tiles: wave 0 the top (or middle) block, wave NW/2 the bottom one
+        CPH(10)
+        // corner pivots on the LDS tiles: wave 0 the top (or middle) block, wave NW/2 + 1 the bottom one
         if (mid) {
             if (w == 0) {
                 const unsigned ct = top ? rows(0, amax) : 0u;
@@ -469,17 +477,21 @@ __device__ __forceinline__ bool factorize2s_lds_chain(const KP& p, SLds& L, doub
                 okw = gj_rows(tT + (pT ^ 1) * SS, bufw, c & all, all & ~c, dlt, 0, amax, nullptr, 0, 0,
                               Sg + (long)kt * SS) && okw;
             }
-            if (w == NW / 2 && bot) {
+            // (wave NW/2 + 1: the top chain's wave 0 and wave NW/2 share a SIMD -- the two
+            // pivot chains would interleave on one VALU)
+            if (w == NW / 2 + 1 && bot) {
                 const unsigned c = rows(p.toff[kb], bmax), all = rows(0, p.bsize[kb]);
                 okw = gj_rows(tB + (pB ^ 1) * SS, bufw, c & all, all & ~c, nullptr, 0, 0, dlb, p.toff[kb], bmax,
                               Sg + (long)kb * SS) && okw;
             }
         }
         lds_barrier();
+        CPH(11)
         if (top) pT ^= 1;
         if (bot && !mid) pB ^= 1;
         qe ^= 1;
     }
+    #undef CPH
     return okw;
 }
 
@@ -543,16 +555,22 @@ __device__ __forceinline__ bool factorize2s(const KP& p, SLds& L, double rho, do
         gsync();
         assemble_targets<false, false, true>(p, L, rho, k, D, E, lane, 64);
         gsync();
+#ifndef MPCQP_CHAIN_STAMPS
         FPH(8)
+#endif
         unsigned cut = 0;
         if (k > 0 && k <= pm) cut |= rows(0, amax);              // the link to block k-1
         if (k < nb - 1 && k >= pm) cut |= rows(p.toff[k], bmax);  // the link to block k+1
         const unsigned all = rows(0, p.bsize[k]);
         okw = gj_rows(D, bufw, all & ~cut, 0u, nullptr, 0, 0, nullptr, 0, 0) && okw;
+#ifndef MPCQP_CHAIN_STAMPS
         FPH(10)
+#endif
     }
     __syncthreads();
+#ifndef MPCQP_CHAIN_STAMPS
     FPH(11)
+#endif
     const int ntop = pm - 1 > 0 ? pm - 1 : 0, nbot = nb - 2 - pm > 0 ? nb - 2 - pm : 0;
     const int nst = ntop > nbot ? ntop : nbot;
     if (Xl) {
@@ -650,6 +668,15 @@ __device__ __forceinline__ bool factorize2s(const KP& p, SLds& L, double rho, do
     return ok;
 }
 
+// LDS after the common carve (solve.hip::lds_solve_bytes): the F rows
+// (derived from the LDS carve by pointer arithmetic only, so the compiler keeps
+// LDS instructions for it -- an integer round trip would make it a flat pointer)
+__device__ __forceinline__ double* big_fc(const SLds& L) {
+    char* c = (char*)(L.flag + 16);
+    c += (16u - ((unsigned)(unsigned long)c & 15u)) & 15u;
+    return A16((double*)c);
+}
+
 // the LDS chain's scratch (factorize2s_lds_chain) fits in the F / G region X2 (big_fg_len)
 template <class KP>
 __host__ __device__ inline int big_fg_len(const KP& p);
@@ -664,8 +691,11 @@ __device__ __noinline__ bool factorize2_nl(const KP* gp, long b, double rho, dou
     SL2 C = carve(p);
     bool ok;
     if constexpr (TT >= 256)  // (the two-wave variant 14 keeps the unsplit form)
+        // (the F / G region from the carve, not the X2 argument: an LDS-typed pointer, so the
+        // chain's tile and E accesses are ds_ instructions -- flat ones wait on the vector-memory
+        // counter too, i.e. for the chain's own workspace loads and write-back stores)
         ok = factorize2s<TT>(p, C.L, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
-                             p.Si + b * (long)p.nb * SS, lds_chain_fits(p) ? X2 : nullptr);
+                             p.Si + b * (long)p.nb * SS, lds_chain_fits(p) ? big_fc(C.L) : nullptr);
     else
         ok = factorize2<TT>(p, C.L, X2, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
                             p.Si + b * (long)p.nb * SS);
@@ -939,14 +969,6 @@ __host__ __device__ inline int big_fg_len(const KP& p) {
     return fg > 4 * SS ? fg : 4 * SS;
 }
 
-// LDS after the common carve (solve.hip::lds_solve_bytes): the F rows
-// (derived from the LDS carve by pointer arithmetic only, so the compiler keeps
-// LDS instructions for it -- an integer round trip would make it a flat pointer)
-__device__ __forceinline__ double* big_fc(const SLds& L) {
-    char* c = (char*)(L.flag + 16);
-    c += (16u - ((unsigned)(unsigned long)c & 15u)) & 15u;
-    return A16((double*)c);
-}
 
 // TTK = 512: TwoSided / twisted_solve (nb up to 24); TTK = 128: TwoSidedW / wave_twisted_solve (nb <= 8).
 // NS: the most steps one chain takes, max(p, nb-1-p).

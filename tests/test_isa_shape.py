@@ -7,7 +7,7 @@ by +-1 %, and spills or `v_readlane` reloads that appeared only on the GPU.  Thi
 code objects that ship in python-mpc_amd/osqp_amd/libmpcqp.so (tests/isa_shape.py) and fails when
 any of the recorded shapes moves:
 
-* VGPR / AGPR counts, spilled VGPRs, the scratch bytes per lane (12 B on cfg 2, 48 B on cfg 5:
+* VGPR / AGPR counts, spilled VGPRs, the scratch bytes per lane (12 B on cfg 2, 20 B on cfg 5:
   the callee-saved spill lanes of the out-of-line phases; 44 B with 5 spilled VGPRs on the
   slack layouts' eliminated-column kernel), SGPR spills at most the recorded count;
 * the ADMM loop: its instruction count, its workgroup barriers, no scratch access, and its
@@ -32,10 +32,10 @@ PINNED = {
     "cfg3": dict(vgpr_count=256, agpr_count=0, vgpr_spill_count=5, private_segment_fixed_size=44, sgpr_spill_max=212,
                  loop=dict(instructions=233, barriers=4, readlane=0, scratch=0)),
     # cfg 5, round 6: the LDS factorisation chain and the unrolled Gauss-Jordan rows moved the
-    # callee-saved spill lanes of factorize2_nl (12 -> 44 B, once per factorisation) and the
+    # callee-saved spill lanes of factorize2_nl (12 -> 20 B, once per factorisation) and the
     # loop's register assignment (1617 -> 1606 instructions, 46 -> 39 v_readlane); same-box
     # A/Bs 251.6 k -> 254.7 k -> 266.7 k solves/s (profiles/r6/lchain_ab.txt, gj_unroll_ab.txt)
-    "cfg5": dict(vgpr_count=254, agpr_count=0, vgpr_spill_count=0, private_segment_fixed_size=44, sgpr_spill_max=238,
+    "cfg5": dict(vgpr_count=254, agpr_count=0, vgpr_spill_count=0, private_segment_fixed_size=20, sgpr_spill_max=238,
                  loop=dict(instructions=1606, barriers=21, readlane=39, scratch=0),
                  step_readlane=0, step_scratch=0),
 }
