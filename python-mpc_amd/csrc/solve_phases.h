@@ -1590,13 +1590,30 @@ template <int TT, bool ROT = false>
 __device__ __noinline__ bool factorize_nl(const KParams* gp, long b, double rho, double* sdst = nullptr) {
     return factorize_ph<TT, ROT>(gp, b, rho, sdst);
 }
-// the same with the G blocks to `hdst` (the one-shot fused kernel: an LDS region, no workspace
-// round trip) instead of the instance's H tiles
+// The four-wave kernels' S_k^{-1} tiles in LDS (lds_w2_bytes: after the carve), formed from the
+// carve itself: a pointer the compiler sees derived from the LDS array keeps ds_ instructions,
+// where one passed in as an argument may become flat accesses -- which wait on the vector-memory
+// counter too, i.e. for the factorisation's own workspace stores
+template <class KP>
+__device__ __forceinline__ double* w4_tiles(const KP& p, const SL2& c) {
+    return c.L.Acsc + 2 * ((lds_base_bytes(p) + 15) / 16);
+}
+// factorize_nl into the LDS tiles (w4_tiles)
 template <int TT, bool ROT = false>
-__device__ __noinline__ bool factorize_g_nl(const KParams* gp, long b, double rho, double* sdst, double* hdst) {
+__device__ __noinline__ bool factorize_lds_nl(const KParams* gp, long b, double rho) {
     KPc& p = kconst(gp);
     SL2 c = carve(p);
-    return factorize<TT, KPc, false, ROT>(p, c.L, rho, p.F + b * (long)p.nb * SS, hdst, sdst);
+    return factorize<TT, KPc, false, ROT>(p, c.L, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
+                                          w4_tiles(p, c));
+}
+// the same with the G blocks to the LDS region after the tiles (the one-shot fused kernel's GL
+// form, one_shot_form 2: no workspace round trip) instead of the instance's H tiles
+template <int TT, bool ROT = false>
+__device__ __noinline__ bool factorize_g_nl(const KParams* gp, long b, double rho) {
+    KPc& p = kconst(gp);
+    SL2 c = carve(p);
+    double* const sg = w4_tiles(p, c);
+    return factorize<TT, KPc, false, ROT>(p, c.L, rho, p.F + b * (long)p.nb * SS, sg + (long)p.nb * SS, sg);
 }
 
 

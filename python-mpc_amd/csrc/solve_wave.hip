@@ -1307,13 +1307,19 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                     const double2* src = (const double2*)(p.Si + b * (long)p.nb * SS);
                     for (int e = tid; e < 2 * SS; e += T4) ((double2*)Sg)[e] = src[e];
                     ok = true;
+                } else if constexpr (EL) {
+                    ok = factorize_lds_nl<T4, EL>(p.self, b, rho);
                 } else {
                     ok = factorize_nl<T4, EL>(p.self, b, rho, Sg);
                 }
                 __syncthreads();
                 if (tid == 0) p.ffresh[b] = 0;
             } else if constexpr (GL) {
-                ok = factorize_g_nl<T4, EL>(p.self, b, rho, Sg, Sg + (long)NB * SS);
+                ok = factorize_g_nl<T4, EL>(p.self, b, rho);
+            } else if constexpr (EL) {
+                // (the tiles from the carve: an LDS-typed pointer, ds_ accesses -- cfg 3's
+                // factorisation was compiled with flat ones)
+                ok = factorize_lds_nl<T4, EL>(p.self, b, rho);
             } else {
                 ok = factorize_nl<T4, EL>(p.self, b, rho, Sg);
             }

@@ -7,7 +7,7 @@ o=gpurun_out/$1; mkdir -p $o
 PREV=$GRAFT_REPO_ROOT/ab/prev/python-mpc_amd
 timeout -k 10 120 python3 tools/lchain_check.py $o/new.npz > $o/check.log 2>&1 || exit 1
 MPCQP_PKG=$PREV timeout -k 10 120 python3 tools/lchain_check.py $o/prev.npz >> $o/check.log 2>&1 || exit 1
-python3 tools/lchain_check.py --compare $o/new.npz $o/prev.npz >> $o/check.log 2>&1
+python3 tools/lchain_check.py --compare $o/new.npz $o/prev.npz >> $o/check.log 2>&1; rm -f $o/new.npz $o/prev.npz
 for r in 1 2 3; do
   timeout -k 10 150 python3 bench.py --config 5 --no-cpu --no-pcie --no-latency --no-dispatch-ab --steps 5 --warmup 1 > $o/c5_new.$r.json 2>>$o/bench.err || exit 1
   MPCQP_PKG=$PREV timeout -k 10 150 python3 bench.py --config 5 --no-cpu --no-pcie --no-latency --no-dispatch-ab --steps 5 --warmup 1 > $o/c5_prev.$r.json 2>>$o/bench.err || exit 1

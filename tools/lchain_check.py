@@ -1,6 +1,6 @@
-"""Diagnostic: outputs of a cfg-5 batch (cold setup + solve, then a warm-started solve) for a
-bit-for-bit A/B of two builds or two settings of the long-horizon factorisation.
-  MPCQP_PKG=<pkg dir> python3 tools/lchain_check.py out.npz [B]
+"""Diagnostic: outputs of a batch (cold setup + solve, then a warm-started solve; on cfg 2 / 3
+also the one-shot fused setup + solve) for a bit-for-bit A/B of two builds or two settings.
+  MPCQP_PKG=<pkg dir> python3 tools/lchain_check.py out.npz [B] [cfg, default 5]
   python3 tools/lchain_check.py --compare a.npz b.npz"""
 import os
 import sys
@@ -20,7 +20,8 @@ import torch  # noqa: E402
 from osqp_amd import DeviceBatch, mpc, _drop_common_zeros  # noqa: E402
 
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 512
-b = mpc.make_batch(5, B=B, seed=77)
+cfg = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+b = mpc.make_batch(cfg, B=B, seed=77)
 P, Px = _drop_common_zeros(b["P"], b["Px"])
 A, Ax = _drop_common_zeros(b["A"], b["Ax"])
 s = {k: v for k, v in b["settings"].items() if k != "verbose"}
@@ -30,6 +31,14 @@ dPx, dAx, dq, dl, du = (t(a) for a in (Px, Ax, b["q"], b["l"], b["u"]))
 torch.cuda.synchronize()
 h = DeviceBatch(P, A, B, device=0, **s)
 out = {}
+if cfg != 5 and hasattr(h, "one_shot"):  # the fused setup + solve, one-shot form, too
+    h1 = DeviceBatch(P, A, B, device=0, **s)
+    h1.one_shot(True)
+    o = [torch.empty((B, b["n"]), dtype=torch.float64, device=dev), torch.empty((B, b["m"]), dtype=torch.float64, device=dev),
+         torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev)]
+    h1.setup_solve(dPx, dAx, dq, dl, du, *o)
+    h1.synchronize()
+    out.update({f"one_{k}": v.cpu().numpy() for k, v in zip(("x", "y", "st", "it"), o)})
 for tag in ("cold", "warm"):
     x = torch.empty((B, b["n"]), dtype=torch.float64, device=dev)
     y = torch.empty((B, b["m"]), dtype=torch.float64, device=dev)
