@@ -204,14 +204,15 @@ int mpcqp_set_shared_matrices(mpcqp_handle *h, int32_t shared);
 /* One-shot mode of mpcqp_setup_solve_device (the Control/MPC call pattern: a fresh OSQP()
  * + setup() + solve() every call, mpc_kinematics.py:194-198, so nothing reads the workspace
  * later): while on, the fused setup + solve kernel leaves the scaled problem on chip for the
- * solve instead of in the workspace, stores no warm-start iterates or certificates and, where
- * two workgroups per CU still fit (cfg 2), keeps the factorisation's G blocks on chip too --
+ * solve instead of in the workspace, stores no warm-start iterates or certificates and keeps the
+ * factorisation's G blocks on chip too where the plan leaves room (cfg 2, cfg 3) --
  * the outputs (x, y, status, iters) and the info are the same, bit for bit.  After such a call
  * the calls that read the workspace (update / warm_start / solve, the host batch calls, matrix
  * updates, certificates) fail with MPCQP_EINVAL until a setup.  mpcqp_one_shot_applies: 0 the
  * handle's kernel has no one-shot form (not the fused four-wave kernel, or polish: the call runs
- * as usual), 1 the form with the G blocks in the workspace, 2 with the G blocks on chip.  The
- * osqp API never turns it on. */
+ * as usual), 1 the form with the G blocks in the workspace, 2 with the G blocks in an LDS region
+ * of their own, 3 with the G blocks written straight into the solve's LDS copy.  The osqp API
+ * never turns it on. */
 int mpcqp_set_one_shot(mpcqp_handle *h, int32_t on);
 int mpcqp_one_shot_applies(const mpcqp_handle *h);
 /* The handle's own hipStream_t (the one a NULL `stream` selects; first shard), so that a

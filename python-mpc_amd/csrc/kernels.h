@@ -151,8 +151,9 @@ hipError_t launch_setup_solve(const KParams& p, long B, const double* Px, const 
                               const double* l, const double* u, double* xo, double* yo, hipStream_t st,
                               bool one_shot = false);
 // the one-shot fused kernel's form for the plan (solve_wave.hip): 0 none (not the fused four-wave
-// kernel, or polish), 1 the G blocks in the workspace, 2 the G blocks in LDS (two workgroups per
-// CU still fit); *lds = its dynamic LDS bytes
+// kernel, or polish), 1 the G blocks in the workspace, 2 the G blocks in an LDS region of their
+// own (two workgroups per CU still fit), 3 the G blocks straight into the solve's LDS copy
+// (factorize_w4_gl); *lds = its dynamic LDS bytes
 int one_shot_form(const KParams& p, size_t* lds = nullptr);
 // What a solve launch runs: the variant's kernel, workgroup size and dynamic LDS.  The
 // launch_solve_* functions given a non-null ref only fill it in (no launch).

@@ -695,6 +695,105 @@ __device__ __forceinline__ bool factorize_w4(const KP& p, SLds& L, const double 
     return okf[0] > 0.5 && okf[1] > 0.5 && okf[2] > 0.5 && okf[3] > 0.5;
 }
 
+// factorize_w4's form for the one-shot kernel on plans whose G blocks have no LDS region of
+// their own (one_shot_form 3, the slack layouts): the G blocks go straight into the solve's
+// copy gl (pair q at q 8 S, rows < amax; rows amax..7 and pair NP are zero from the kernel's
+// start), and F_k, G_20 are read back from there instead of the scratch tiles Fk / G20
+// (G_{k,k-1} = -F_k: a sum over negated operands is the negated sum, exactly, so every
+// stored value is the workspace form's bit for bit).  Scratch: E_0..E_3 and the wave buffers
+// at the start of the carve's V span (w, rb, xt, ys, dY: dead across a factorisation, y parked
+// by the caller; one_shot_form checks that they end before gl), the corner correction in red.
+template <bool ROT = false, class KP>
+__device__ __forceinline__ bool factorize_w4_gl(const KP& p, SLds& L, const double rho, double* __restrict__ Sg,
+                                                double* __restrict__ Fo) {
+    constexpr int TT = 256;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int amax = p.amax, as = amax * S;
+    constexpr long gstride = 8 * S;
+    double* const V = L.SP;
+    double* const Gl = L.gl;
+    double* const dl = L.red;                          // amax x amax, row stride 16
+    double* const bufw = V + 4 * as + w * 2 * S;       // the wave's Gauss-Jordan publish buffers
+    double* const okf = V + 4 * as + 8 * S;
+    auto Ek = [&](int k) __attribute__((always_inline)) { return V + k * as; };
+    auto wave_sync = []() __attribute__((always_inline)) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    bool oke = true;
+    assemble_block<false, true>(p, L, rho, w, Sg + (long)w * SS, Ek(w), lane, 64, wave_sync);
+    wave_sync();
+    if (p.ne && lane < S) {  // (factorize_w4's eliminated columns, unchanged)
+        const int pe = p.eown[w * S + lane];
+        if (pe >= 0) {
+            const int e = pe - p.nb * S, ne2 = 2 * p.ne;
+            const int2* __restrict__ et = (const int2*)p.etterm;
+            double kjj = p.sigma, kpj = 0.0;
+            for (int j = 0; j < p.eterm_max; ++j) {
+                const int2 a = et[(long)j * ne2 + 2 * e], c = et[(long)j * ne2 + 2 * e + 1];
+                kjj += a.y < 0 ? L.Pv[a.x] : rho_of(L.ct[a.y], rho) * L.Acsc[a.x & 0xFFFF] * L.Acsc[(unsigned)a.x >> 16];
+                kpj += c.y < 0 ? L.Pv[c.x] : rho_of(L.ct[c.y], rho) * L.Acsc[c.x & 0xFFFF] * L.Acsc[(unsigned)c.x >> 16];
+            }
+            const double ed = 1.0 / kjj, ec = kpj * ed;
+            oke = kjj > 0.0 && ed < __builtin_huge_val();
+            Sg[(long)w * SS + lane * S + lane] -= kpj * ec;
+            Fo[2 * e] = ec;
+            Fo[2 * e + 1] = ed;
+        }
+        wave_sync();
+    }
+    bool okw = gj_seg<1, false, ROT>(Sg + (long)w * SS, bufw, w ? amax : 0, p.bsize[w], nullptr);
+    okw = okw && __builtin_amdgcn_ballot_w64(!oke) == 0;
+    __syncthreads();
+#pragma unroll 1
+    for (int k = 1; k < 4; ++k) {
+        const double* Sp = Sg + (long)(k - 1) * SS;
+        const double* E = Ek(k);
+        double* const Gk = Gl + (long)(k * (k - 1) / 2 + k - 1) * gstride;  // G_{k,k-1} = -F_k
+        const int l0 = p.toff[k - 1], bmax = p.bmax;
+        for (int o = tid; o < as; o += TT) {
+            const int r = o >> 5, j = o & (S - 1);
+            double sacc = 0.0;
+#pragma unroll 4
+            for (int l = l0; l < l0 + bmax; ++l) sacc += E[r * S + l] * Sp[l * S + j];
+            Gk[o] = -sacc;
+        }
+        __syncthreads();
+        if (w == 0) {
+            // the corner S_k = D_k - F_k E_k': -F_k E_k' = sum over G_{k,k-1} E_k'
+            if (lane < amax * amax) {
+                const int r = lane / amax, c = lane - r * amax;
+                double sacc = 0.0;
+#pragma unroll 4
+                for (int l = l0; l < l0 + bmax; ++l) sacc += Gk[r * S + l] * E[c * S + l];
+                dl[r * 16 + c] = sacc;
+            }
+            wave_sync();
+            okw = gj_seg<2, false, ROT>(Sg + (long)k * SS, bufw, amax, p.bsize[k], dl) && okw;
+        } else {
+            // G_kj = -F_k G_{k-1,j} (j < k-1): G_{k,k-1} G_{k-1,j} for j < k-2, and
+            // G_{k,k-1} G_{k-1,k-2} = F_k F_{k-1} for j = k-2
+#pragma unroll 1
+            for (int j = 0; j < k - 1; ++j) {
+                const double* Gp = Gl + (long)((k - 1) * (k - 2) / 2 + j) * gstride;
+                for (int o = tid - 64; o < as; o += TT - 64) {
+                    const int r = o >> 5, c = o & (S - 1);
+                    double sacc = 0.0;
+#pragma unroll
+                    for (int l = 0; l < 8; ++l)
+                        if (l < amax) sacc += Gk[r * S + l] * Gp[l * S + c];
+                    Gl[(long)(k * (k - 1) / 2 + j) * gstride + o] = sacc;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (lane == 0) okf[w] = okw ? 1.0 : 0.0;
+    __syncthreads();
+    return okf[0] > 0.5 && okf[1] > 0.5 && okf[2] > 0.5 && okf[3] > 0.5;
+}
+
 __host__ __device__ inline double* w8_gpair(double* Fg, double* Hg, int amax, int q);  // (below)
 
 // The eight-wave kernel's factorisation (solve_wave.hip::k_solve_w8, variant 18: mode 2,
@@ -1605,6 +1704,14 @@ __device__ __noinline__ bool factorize_lds_nl(const KParams* gp, long b, double 
     SL2 c = carve(p);
     return factorize<TT, KPc, false, ROT>(p, c.L, rho, p.F + b * (long)p.nb * SS, p.H + b * (long)p.nb * SS,
                                           w4_tiles(p, c));
+}
+// the one-shot form 3: the G blocks straight into the solve's gl copy (factorize_w4_gl)
+template <int TT, bool ROT = false>
+__device__ __noinline__ bool factorize_gl_nl(const KParams* gp, long b, double rho) {
+    static_assert(TT == 256, "the four-wave kernel");
+    KPc& p = kconst(gp);
+    SL2 c = carve(p);
+    return factorize_w4_gl<ROT>(p, c.L, rho, w4_tiles(p, c), p.F + b * (long)p.nb * SS);
 }
 // the same with the G blocks to the LDS region after the tiles (the one-shot fused kernel's GL
 // form, one_shot_form 2: no workspace round trip) instead of the instance's H tiles

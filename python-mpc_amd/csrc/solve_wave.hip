@@ -1172,11 +1172,12 @@ __device__ __forceinline__ void form_dense_rows(__attribute__((address_space(1))
 // and the eliminated columns' ec / ed in F); the factor-only launch (factor_only) persists them
 // ONE (the one-shot fused kernel, mpcqp_set_one_shot; cold start): the setup left the scaled
 // problem in this carve (setup_r.h ONE) and finalize stores no warm-start state -- no workspace
-// round trip for data no later call reads; GL (where the LDS budget of two workgroups per CU
-// allows it, one_shot_form): the G blocks go to an LDS region after the S_k^{-1} tiles instead
-// of the instance's H tiles, and a refactorisation keeps y there instead of in the workspace
+// round trip for data no later call reads; GL 1 (where the LDS budget of two workgroups per CU
+// allows it, one_shot_form 2): the G blocks go to an LDS region after the S_k^{-1} tiles instead
+// of the instance's H tiles, and a refactorisation keeps y there instead of in the workspace;
+// GL 2 (one_shot_form 3): the G blocks go straight into gl (factorize_w4_gl)
 template <int K, int KPK, int QR, bool EL = false, int KC = K, bool DK = false, bool RU = false, bool ONE = false,
-          bool GL = false>
+          int GL = 0>
 __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restrict__ xo, double* __restrict__ yo,
                                               int factor_only = 0) {
     static_assert(!(DK && EL), "the dense inverse covers plans without eliminated columns");
@@ -1190,8 +1191,9 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
     const int n = p.n, m = p.m, npad = p.npad, nnzP = p.nnzP, nnzA = p.nnzA;
     SL2 C = carve(p);
     SLds& L = C.L;
-    // GL: the G blocks (amax x S per pair) go to LDS after the S_k^{-1} tiles
-    const double* Hg = GL ? C.L.Acsc + 2 * ((lds_base_bytes(p) + 15) / 16) + (long)NB * SS
+    // GL 1: the G blocks (amax x S per pair) go to LDS after the S_k^{-1} tiles; GL 2: straight
+    // into gl (factorize_w4_gl), no copy
+    const double* Hg = GL == 1 ? C.L.Acsc + 2 * ((lds_base_bytes(p) + 15) / 16) + (long)NB * SS
                            : p.H + b * (long)p.nb * SS;
     double* const Sg = C.L.Acsc + 2 * ((lds_base_bytes(p) + 15) / 16);  // S_k^{-1} tiles in LDS (lds_w2_bytes)
 
@@ -1240,6 +1242,8 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
     } else {
         if (tid == 0) L.Acsc[nnzA] = 0.0;
         if (tid == 0) L.Pv[nnzP] = 0.0;
+        if constexpr (GL == 2)  // (factorize_w4_gl writes rows < amax of the pairs; the rest stays zero)
+            for (int o = tid; o < (NP + 1) * 8 * S; o += T4) L.gl[o] = 0.0;
     }
     if (tid < 8) L.cor[tid] = 0.0;        // c_0 = 0 (block 0 has no correction)
     if (tid < 8) L.cor[32 + tid] = 0.0;   // the upper half's zero correction row (phase B)
@@ -1286,7 +1290,7 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
         if (need_factor) {
             need_factor = false;
             if (iter > 0) {
-                if constexpr (GL) {  // (y kept on chip, after the G blocks)
+                if constexpr (GL == 1) {  // (y kept on chip, after the G blocks)
                     double* const ysv = Sg + (long)NB * SS + (long)(NB * (NB - 1) / 2) * p.amax * S;
                     for (int i = tid; i < m; i += T4) ysv[i] = L.ys[i];
                 } else {
@@ -1314,8 +1318,10 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 }
                 __syncthreads();
                 if (tid == 0) p.ffresh[b] = 0;
-            } else if constexpr (GL) {
+            } else if constexpr (GL == 1) {
                 ok = factorize_g_nl<T4, EL>(p.self, b, rho);
+            } else if constexpr (GL == 2) {
+                ok = factorize_gl_nl<T4, EL>(p.self, b, rho);
             } else if constexpr (EL) {
                 // (the tiles from the carve: an LDS-typed pointer, ds_ accesses -- cfg 3's
                 // factorisation was compiled with flat ones)
@@ -1346,16 +1352,18 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
             }
             __syncthreads();
             const bool have_y = iter > 0 || warm;
-            if constexpr (GL) {
+            if constexpr (GL == 1) {
                 const double* const ysv = Sg + (long)NB * SS + (long)(NB * (NB - 1) / 2) * p.amax * S;
                 for (int i = tid; i < mp; i += T4) L.ys[i] = (have_y && i < m) ? ysv[i] : 0.0;
             } else {
                 const auto yp = opaque_gptr(p.y + b * m);
                 for (int i = tid; i < mp; i += T4) L.ys[i] = (have_y && i < m) ? yp[i] : 0.0;
             }
-            for (int o = tid; o < (NP + 1) * 8 * S; o += T4) {
-                const int q = o >> 8, t = (o >> 5) & 7;
-                L.gl[o] = (q < NP && t < p.amax) ? Hg[(long)q * p.amax * S + (o & 255)] : 0.0;
+            if constexpr (GL != 2) {
+                for (int o = tid; o < (NP + 1) * 8 * S; o += T4) {
+                    const int q = o >> 8, t = (o >> 5) & 7;
+                    L.gl[o] = (q < NP && t < p.amax) ? Hg[(long)q * p.amax * S + (o & 255)] : 0.0;
+                }
             }
             chs.load(p.gcol + (h ? KH : 0) * npad + pc, npad, abase, wbase);
             if constexpr (EL) {
@@ -1907,7 +1915,7 @@ __global__ __launch_bounds__(T4, 2) void k_solve_w4(KParams p, double* __restric
 // setup (setup_r.h with 256 threads: one column and one row per thread) + solve; ONE: the
 // one-shot form (solve_w4_body)
 template <int K, int KPK, int QR, int SK, int SAS, bool EL = false, int KC = K, bool DK = false, bool ONE = false,
-          bool GL = false>
+          int GL = 0>
 __global__ __launch_bounds__(T4, 2) void k_setup_solve_w4(KParams p, const double* __restrict__ Px_in,
                                                           const double* __restrict__ Ax_in,
                                                           const double* __restrict__ q_in,
@@ -2465,7 +2473,10 @@ int one_shot_form(const KParams& p, size_t* lds) {
     // (form 2: the G blocks and the y of a refactorisation, which the factorisation's E tiles
     // overwrite in the carve, after the S_k^{-1} tiles)
     const size_t g = sizeof(double) * ((size_t)(p.nb * (p.nb - 1) / 2) * p.amax * S + (size_t)p.m);
-    const int form = base + g <= 80 * 1024 ? 2 : 1;  // (two workgroups per CU, as the persisting kernel)
+    // form 3 (GL 2): the G blocks straight into the solve's gl copy, with factorize_w4_gl's
+    // scratch (the E tiles and wave buffers) in the carve's V span before gl
+    const long vspan = 3L * solve_mpad(p.m) + 2L * p.npad;
+    const int form = base + g <= 80 * 1024 ? 2 : (p.amax <= 8 && 4L * p.amax * S + 8 * S + 8 <= vspan ? 3 : 1);
     if (lds) *lds = form == 2 ? base + g : base;
     return form;
 }
@@ -2478,9 +2489,13 @@ hipError_t launch_setup_solve(const KParams& p, long B, const double* Px, const 
     if (form) {
         decltype(&k_setup_solve_w4<6, 4, 5, 6, 2>) k4;
         if (form == 2)
-            k4 = p.ne ? k_setup_solve_w4<6, 4, 8, 8, 3, true, 8, false, true, true>
-                      : (p.amax <= 5 ? k_setup_solve_w4<6, 4, 5, 6, 2, false, 6, false, true, true>
-                                     : k_setup_solve_w4<6, 4, 8, 6, 2, false, 6, false, true, true>);
+            k4 = p.ne ? k_setup_solve_w4<6, 4, 8, 8, 3, true, 8, false, true, 1>
+                      : (p.amax <= 5 ? k_setup_solve_w4<6, 4, 5, 6, 2, false, 6, false, true, 1>
+                                     : k_setup_solve_w4<6, 4, 8, 6, 2, false, 6, false, true, 1>);
+        else if (form == 3)
+            k4 = p.ne ? k_setup_solve_w4<6, 4, 8, 8, 3, true, 8, false, true, 2>
+                      : (p.amax <= 5 ? k_setup_solve_w4<6, 4, 5, 6, 2, false, 6, false, true, 2>
+                                     : k_setup_solve_w4<6, 4, 8, 6, 2, false, 6, false, true, 2>);
         else
             k4 = p.ne ? k_setup_solve_w4<6, 4, 8, 8, 3, true, 8, false, true>
                       : (p.amax <= 5 ? k_setup_solve_w4<6, 4, 5, 6, 2, false, 6, false, true>

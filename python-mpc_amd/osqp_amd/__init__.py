@@ -628,7 +628,8 @@ class DeviceBatch:
         blocks, the warm-start iterates, the certificates) for later calls -- the Control/MPC
         pattern of a fresh setup() + solve() per call.  Returns the form that applies to this
         handle's kernel: 0 none (not the fused four-wave kernel), 1 the G blocks in the workspace,
-        2 the G blocks on chip (mpcqp_one_shot_applies)."""
+        2 in an LDS region of their own, 3 straight into the solve's LDS copy
+        (mpcqp_one_shot_applies)."""
         _check(lib().mpcqp_set_one_shot(self._h.ptr, int(on)), "set_one_shot")
         return int(lib().mpcqp_one_shot_applies(self._h.ptr))
 

@@ -73,9 +73,9 @@ def report(lib, kernels):
 
 HOT = {
     # configs[1] (the headline): the fused setup + solve four-wave kernel
-    "cfg2": ("_ZN5mpcqp16k_setup_solve_w4ILi6ELi4ELi5ELi6ELi2ELb0ELi6ELb0ELb0ELb0EE", "w4"),
+    "cfg2": ("_ZN5mpcqp16k_setup_solve_w4ILi6ELi4ELi5ELi6ELi2ELb0ELi6ELb0ELb0ELi0EE", "w4"),
     # configs[2] / [3]: the slack layouts' eliminated-column instantiation
-    "cfg3": ("_ZN5mpcqp16k_setup_solve_w4ILi6ELi4ELi8ELi8ELi3ELb1ELi8ELb0ELb0ELb0EE", "w4"),
+    "cfg3": ("_ZN5mpcqp16k_setup_solve_w4ILi6ELi4ELi8ELi8ELi3ELb1ELi8ELb0ELb0ELi0EE", "w4"),
     # configs[4]: the long-horizon two-sided kernel, variant 12
     "cfg5": ("_ZN5mpcqp9k_solve_bILi512ELi9ELi8ELi2ELi2ELb0EE", "big"),
 }
