@@ -35,7 +35,8 @@ __host__ __device__ inline size_t lds_setup_r_bytes(int nnzP, int nnzA, int npad
 // where the solve kernel's carve keeps it (solve_phases.h::carve: A, P, bounds, row classes,
 // q, x = z = 0) instead of in the workspace -- no later call reads it there; D, E, c and the
 // status slots are written as always
-template <int TT, int K, int KP, int RS, int AS, int PS, bool KEEP = false, bool ONE = false>
+// EDL (with ONE; one_shot_form 2): E and D too go to the carve (solve_phases.h::edl_E / edl_D)
+template <int TT, int K, int KP, int RS, int AS, int PS, bool KEEP = false, bool ONE = false, bool EDL = false>
 __device__ __forceinline__ void setup_r_body(const KParams& p, const long b, const double* __restrict__ Px_in,
                                              const double* __restrict__ Ax_in, const double* __restrict__ q_in,
                                              const double* __restrict__ l_in, const double* __restrict__ u_in,
@@ -195,7 +196,7 @@ __device__ __forceinline__ void setup_r_body(const KParams& p, const long b, con
                 p.l[b * m + i] = li;
                 p.u[b * m + i] = ui;
             }
-            p.E[b * m + i] = Ev[s];
+            if (!EDL) p.E[b * m + i] = Ev[s];
             if (!KEEP && !ONE) {
                 p.ct[b * m + i] = t;
                 p.z[b * m + i] = 0.0;
@@ -242,13 +243,20 @@ __device__ __forceinline__ void setup_r_body(const KParams& p, const long b, con
             C.L.qv[pc] = qv;
             C.X[pc] = 0.0;
         }
+        if constexpr (EDL) {
+            double* const ed = edl_E(p, C);
+#pragma unroll
+            for (int s = 0; s < RS; ++s)
+                if (tid + s * TT < m) ed[tid + s * TT] = Ev[s];
+            if (pc < npad) edl_D(p, C)[pc] = Dv;
+        }
     } else {
         for (int v = tid; v < nnzP; v += TT) p.Px[b * nnzP + v] = Pv[v];
         for (int e = tid; e < nnzA; e += TT) p.Ax[b * nnzA + e] = Ac[e];
     }
     if (pc < npad) {
         if (!ONE) p.q[b * npad + pc] = qv;
-        p.D[b * npad + pc] = Dv;
+        if (!EDL) p.D[b * npad + pc] = Dv;
         if (!KEEP && !ONE) p.x[b * npad + pc] = 0.0;
     }
     if (tid == 0) {

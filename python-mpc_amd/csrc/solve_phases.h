@@ -1317,6 +1317,18 @@ __device__ __forceinline__ SL2 carve(const KP& p) {
     return c;
 }
 
+// EDL (the one-shot fused kernel's form 2, one_shot_form): the setup leaves E and D in the carve's
+// V span after gl (free in the four-wave kernel: its V is sized for 3 S x S of scratch) instead of
+// in the workspace; the checks and finalize read them there
+template <class KP>
+__device__ __forceinline__ double* edl_E(const KP& p, const SL2& c) {
+    return A16(c.L.gl + solve_glen(p.nb, p.amax, p.mode));
+}
+template <class KP>
+__device__ __forceinline__ double* edl_D(const KP& p, const SL2& c) {
+    return A16(edl_E(p, c) + al2(p.m));
+}
+
 // LDS scalar slots (in res[14..15] and flag[1..]): shared outcome of the out-of-line phases
 struct Shared {
     double* res;  // [0..13] Res, [14] obj, [15] new rho
@@ -1362,13 +1374,13 @@ __device__ __forceinline__ double psym_dot(const KP& p, const double* Pv, const 
 
 // update_info: residuals and the norms of their tolerances (OSQP compute_pri_res /
 // compute_dua_res / compute_pri_tol / compute_dua_tol, scaled and unscaled)
-template <int TT>
+template <int TT, bool EDL = false>
 __device__ __forceinline__ void update_info_ph(const KParams* gp, long b, double cinv) {
     KPc& p = kconst(gp);
     SL2 c = carve(p);
     const int tid = threadIdx.x, m = p.m, npad = p.npad;
-    const double* Eg = p.E + b * m;
-    const double* Dg = p.D + b * npad;
+    const double* Eg = EDL ? edl_E(p, c) : p.E + b * m;
+    const double* Dg = EDL ? edl_D(p, c) : p.D + b * npad;
     double v[14];
 #pragma unroll
     for (int k = 0; k < 14; ++k) v[k] = 0.0;
@@ -1419,18 +1431,18 @@ __device__ __forceinline__ void update_info_ph(const KParams* gp, long b, double
     }
     __syncthreads();
 }
-template <int TT>
+template <int TT, bool EDL = false>
 __device__ __noinline__ void update_info_nl(const KParams* gp, long b, double cinv) {
-    update_info_ph<TT>(gp, b, cinv);
+    update_info_ph<TT, EDL>(gp, b, cinv);
 }
 
 // is_primal_infeasible (delta_y in dY, projected in place as OSQP does)
-template <int TT, class KP>
+template <int TT, bool EDL = false, class KP>
 __device__ bool primal_infeasible(const KP& p, SL2& c, long b, double eps) {
     const int tid = threadIdx.x, m = p.m, npad = p.npad;
     const bool unscale = p.scaling && !p.scaled_term;
-    const double* Eg = p.E + b * m;
-    const double* Dg = p.D + b * npad;
+    const double* Eg = EDL ? edl_E(p, c) : p.E + b * m;
+    const double* Dg = EDL ? edl_D(p, c) : p.D + b * npad;
     double nd[1] = {0.0};
 #pragma unroll 1
     for (int i = tid; i < m; i += TT) {
@@ -1461,12 +1473,12 @@ __device__ bool primal_infeasible(const KP& p, SL2& c, long b, double eps) {
 }
 
 // is_dual_infeasible (delta_x in dx)
-template <int TT, class KP>
+template <int TT, bool EDL = false, class KP>
 __device__ bool dual_infeasible(const KP& p, SL2& c, long b, double cs_, double eps) {
     const int tid = threadIdx.x, m = p.m, npad = p.npad;
     const bool unscale = p.scaling && !p.scaled_term;
-    const double* Eg = p.E + b * m;
-    const double* Dg = p.D + b * npad;
+    const double* Eg = EDL ? edl_E(p, c) : p.E + b * m;
+    const double* Dg = EDL ? edl_D(p, c) : p.D + b * npad;
     const double cs = unscale ? cs_ : 1.0;
     double v[1] = {0.0}, sum[1] = {0.0};
 #pragma unroll 1
@@ -1504,7 +1516,7 @@ __device__ bool dual_infeasible(const KP& p, SL2& c, long b, double cs_, double 
 }
 
 // check_termination on the Res in LDS; status / obj / certificate flags in LDS.
-template <int TT>
+template <int TT, bool EDL = false>
 __device__ __forceinline__ int check_termination_ph(const KParams* gp, long b, double cval, double cinv,
                                                  int approximate) {
     KPc& p = kconst(gp);
@@ -1527,12 +1539,12 @@ __device__ __forceinline__ int check_termination_ph(const KParams* gp, long b, d
         else {
             const double ep = eps_abs + eps_rel * cmax(R.nz, R.nax);
             if (R.pri < ep) prim_ok = true;
-            else prim_inf = primal_infeasible<TT>(p, c, b, eps_pinf);
+            else prim_inf = primal_infeasible<TT, EDL>(p, c, b, eps_pinf);
         }
         double mx = cmax(cmax(R.nq, R.naty), R.npx);
         if (unscale) mx *= cinv;
         if (R.dua < eps_abs + eps_rel * mx) dual_ok = true;
-        else dual_inf = dual_infeasible<TT>(p, c, b, cval, eps_dinf);
+        else dual_inf = dual_infeasible<TT, EDL>(p, c, b, cval, eps_dinf);
         if (prim_ok && dual_ok) {
             st = approximate ? MPCQP_SOLVED_INACCURATE_ : MPCQP_SOLVED_;
             done = true;
@@ -1553,10 +1565,10 @@ __device__ __forceinline__ int check_termination_ph(const KParams* gp, long b, d
     __syncthreads();
     return done ? st : MPCQP_UNSOLVED_;
 }
-template <int TT>
+template <int TT, bool EDL = false>
 __device__ __noinline__ int check_termination_nl(const KParams* gp, long b, double cval, double cinv,
                                                  int approximate) {
-    return check_termination_ph<TT>(gp, b, cval, cinv, approximate);
+    return check_termination_ph<TT, EDL>(gp, b, cval, cinv, approximate);
 }
 
 // compute_obj_val (needs X)
@@ -1586,15 +1598,15 @@ __device__ __noinline__ void objective_nl(const KParams* gp, double cinv) {
 // no later call reads the workspace, so the warm-start iterates x, z, y and the infeasibility
 // certificates are not stored -- the outputs, the status / iteration count (the next dispatch
 // order) and the info are
-template <int TT, bool ONE = false>
+template <int TT, bool ONE = false, bool EDL = false>
 __device__ __forceinline__ void finalize_ph(const KParams* gp, long b, double* __restrict__ xo,
                                          double* __restrict__ yo, double cinv, double rho, int status,
                                          int info_iter, int rho_updates, int* ostat, int* oiter) {
     KPc& p = kconst(gp);
     SL2 c = carve(p);
     const int tid = threadIdx.x, n = p.n, m = p.m, npad = p.npad;
-    const double* Eg = p.E + b * m;
-    const double* Dg = p.D + b * npad;
+    const double* Eg = EDL ? edl_E(p, c) : p.E + b * m;
+    const double* Dg = EDL ? edl_D(p, c) : p.D + b * npad;
     Res R;
     R.restore(c.L.res);
     double rho_est;
@@ -1661,11 +1673,11 @@ __device__ __forceinline__ void finalize_ph(const KParams* gp, long b, double* _
         p.scal[b * 4 + 2] = rho;
     }
 }
-template <int TT, bool ONE = false>
+template <int TT, bool ONE = false, bool EDL = false>
 __device__ __noinline__ void finalize_nl(const KParams* gp, long b, double* __restrict__ xo,
                                          double* __restrict__ yo, double cinv, double rho, int status,
                                          int info_iter, int rho_updates, int* ostat, int* oiter) {
-    finalize_ph<TT, ONE>(gp, b, xo, yo, cinv, rho, status, info_iter, rho_updates, ostat, oiter);
+    finalize_ph<TT, ONE, EDL>(gp, b, xo, yo, cinv, rho, status, info_iter, rho_updates, ostat, oiter);
 }
 
 template <int TT>

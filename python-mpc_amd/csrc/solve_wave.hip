@@ -1174,8 +1174,9 @@ __device__ __forceinline__ void form_dense_rows(__attribute__((address_space(1))
 // problem in this carve (setup_r.h ONE) and finalize stores no warm-start state -- no workspace
 // round trip for data no later call reads; GL 1 (where the LDS budget of two workgroups per CU
 // allows it, one_shot_form 2): the G blocks go to an LDS region after the S_k^{-1} tiles instead
-// of the instance's H tiles, and a refactorisation keeps y there instead of in the workspace;
-// GL 2 (one_shot_form 3): the G blocks go straight into gl (factorize_w4_gl)
+// of the instance's H tiles, a refactorisation keeps y there instead of in the workspace, and
+// the setup leaves E and D in the carve (edl_E / edl_D); GL 2 (one_shot_form 3): the G blocks go
+// straight into gl (factorize_w4_gl)
 template <int K, int KPK, int QR, bool EL = false, int KC = K, bool DK = false, bool RU = false, bool ONE = false,
           int GL = 0>
 __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restrict__ xo, double* __restrict__ yo,
@@ -1700,8 +1701,14 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
                 pg.clear(lds_addr(L.Pv) + 8u * nnzP, Xbase);
             }
             const int oz = opaque_zero();
-            const double Dv = col >= 0 ? opaque_gptr(p.D + b * npad)[col] : 1.0;
-            const double Ev = ri < m ? opaque_gptr(p.E + b * m)[ri] : 1.0;
+            double Dv, Ev;
+            if constexpr (GL == 1) {  // (E and D on chip: the one-shot form 2, edl_E / edl_D)
+                Dv = col >= 0 ? edl_D(p, C)[col] : 1.0;
+                Ev = ri < m ? edl_E(p, C)[ri] : 1.0;
+            } else {
+                Dv = col >= 0 ? opaque_gptr(p.D + b * npad)[col] : 1.0;
+                Ev = ri < m ? opaque_gptr(p.E + b * m)[ri] : 1.0;
+            }
             // inline update_info + check_termination (as solve_w2_body's), one row per thread
             const bool unscale = p.scaling && !p.scaled_term;
             const unsigned ysbase = lds_addr(L.ys), dYbase = lds_addr(C.dY), dxbase = lds_addr(L.dx);
@@ -1870,19 +1877,19 @@ __device__ __forceinline__ void solve_w4_body(const KParams& p, double* __restri
     }
     const double cval = cscal(0), cinv = cscal(1);
     if (!can_check && status == MPCQP_UNSOLVED_) {
-        update_info_nl<T4>(p.self, b, cinv);
+        update_info_nl<T4, GL == 1>(p.self, b, cinv);
         info_iter = iter;
-        status = check_termination_nl<T4>(p.self, b, cval, cinv, 0);
+        status = check_termination_nl<T4, GL == 1>(p.self, b, cval, cinv, 0);
     }
     const bool has_sol = !(status == MPCQP_PRIMAL_INFEASIBLE_ || status == MPCQP_PRIMAL_INFEASIBLE_INACCURATE_ ||
                            status == MPCQP_DUAL_INFEASIBLE_ || status == MPCQP_DUAL_INFEASIBLE_INACCURATE_ ||
                            status == MPCQP_NON_CVX_);
     if (has_sol) objective_nl<T4>(p.self, cinv);
     if (status == MPCQP_UNSOLVED_) {
-        status = check_termination_nl<T4>(p.self, b, cval, cinv, 1);
+        status = check_termination_nl<T4, GL == 1>(p.self, b, cval, cinv, 1);
         if (status == MPCQP_UNSOLVED_) status = MPCQP_MAX_ITER_REACHED_;
     }
-    finalize_nl<T4, ONE>(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates, p.ostat, p.oiter);
+    finalize_nl<T4, ONE, GL == 1>(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates, p.ostat, p.oiter);
 #ifdef MPCQP_PHASE_PROF
     if (prof) {
         __syncthreads();
@@ -1923,7 +1930,7 @@ __global__ __launch_bounds__(T4, 2) void k_setup_solve_w4(KParams p, const doubl
                                                           const double* __restrict__ u_in, double* __restrict__ xo,
                                                           double* __restrict__ yo) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    setup_r_body<T4, SK, 4, 1, SAS, 1, false, ONE>(p, instance_of(p), Px_in, Ax_in, q_in, l_in, u_in, sm);
+    setup_r_body<T4, SK, 4, 1, SAS, 1, false, ONE, GL == 1>(p, instance_of(p), Px_in, Ax_in, q_in, l_in, u_in, sm);
     __syncthreads();
     solve_w4_body<K, KPK, QR, EL, KC, DK, false, ONE, GL>(p, xo, yo);
     order_epilogue<T4>(p, (int*)sm);
@@ -2475,8 +2482,11 @@ int one_shot_form(const KParams& p, size_t* lds) {
     const size_t g = sizeof(double) * ((size_t)(p.nb * (p.nb - 1) / 2) * p.amax * S + (size_t)p.m);
     // form 3 (GL 2): the G blocks straight into the solve's gl copy, with factorize_w4_gl's
     // scratch (the E tiles and wave buffers) in the carve's V span before gl
+    // form 2 also keeps E and D after gl (edl_E / edl_D: the V span's room past gl)
     const long vspan = 3L * solve_mpad(p.m) + 2L * p.npad;
-    const int form = base + g <= 80 * 1024 ? 2 : (p.amax <= 8 && 4L * p.amax * S + 8 * S + 8 <= vspan ? 3 : 1);
+    const long vfree = solve_vlen(p.m, p.npad, p.nb, p.amax, p.mode) - vspan - solve_glen(p.nb, p.amax, p.mode);
+    const bool edl = vfree >= ((p.m + 1) & ~1) + p.npad;
+    const int form = base + g <= 80 * 1024 && edl ? 2 : (p.amax <= 8 && 4L * p.amax * S + 8 * S + 8 <= vspan ? 3 : 1);
     if (lds) *lds = form == 2 ? base + g : base;
     return form;
 }
