@@ -336,7 +336,7 @@ size_t workspace_bytes(const Plan& pl, long B, bool with_io) {
     carve<double>(off, B * m); carve<double>(off, B * n);              // certificates
     for (int i = 0; i < 4; ++i) carve<double>(off, B);
     carve<signed char>(off, B * m);
-    for (int i = 0; i < 7; ++i) carve<int>(off, B);
+    for (int i = 0; i < 8; ++i) carve<int>(off, B);
     carve<int>(off, 1);  // done (fused order epilogue)
     carve<long long>(off, B * kProfSlots);
     carve<KParams>(off, 1);
@@ -407,6 +407,9 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io, bool sync = true) {
         int* ord = (int*)(base + carve<int>(off, B));
         HIPCHK(launch_iota(ord, B, s.stream));
         k.order = ord;
+        k.pred = (int*)(base + carve<int>(off, B));  // zero from the memset above
+        const char* od = getenv("MPCQP_ORDER_DECAY");
+        k.odecay = od ? std::max(0, std::min(8, atoi(od))) : 7;  // (tools/pred_sim.py, profiles/r6/dispatch.txt)
         strace().mark("order upload");
         if (const char* ev = getenv("MPCQP_DISPATCH"); ev && !strcmp(ev, "identity")) k.order = nullptr;  // A/B
     }

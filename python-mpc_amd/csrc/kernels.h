@@ -86,6 +86,12 @@ struct KParams {
     // k_solve_b's factorisation chain runs on LDS copies of its tiles (solve_big.hip::
     // factorize2s_lds_chain; MPCQP_LDS_CHAIN=0: the workspace form, A/B)
     int lchain;
+    // dispatch prediction with history (kernels.hip::k_order): key = max(iter, pred), then
+    // pred = key * odecay / 8 per instance -- an instance that was slow in a recent solve keeps
+    // an early slot for a few solves (MPCQP_ORDER_DECAY=0..8, default 7; 0: the previous count
+    // alone)
+    int* pred;
+    int odecay;
 };
 constexpr long kOrderFuseMax = 16384;  // larger batches sort in k_order (1024 threads)
 

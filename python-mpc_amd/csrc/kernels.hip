@@ -468,14 +468,16 @@ hipError_t launch_iota(int* order, long B, hipStream_t st) {
 // every instance's arithmetic, and so its result, is unchanged.
 // One workgroup: counting sort on iter >> shift (descending), 256 bins.
 constexpr int kOrderT = 1024, kOrderBins = 256;
+// pred / odecay (KParams::pred): the key is max(iter, pred), and pred becomes key * odecay / 8.
 __global__ __launch_bounds__(kOrderT) void k_order(const int* __restrict__ iter, int* __restrict__ order, long B,
-                                                  int shift) {
+                                                  int shift, int* __restrict__ pred, int odecay) {
     __shared__ int cnt[kOrderBins];
     const int t = threadIdx.x;
     if (t < kOrderBins) cnt[t] = 0;
     __syncthreads();
+    auto key = [&](long i) { return odecay ? max(iter[i], pred[i]) : iter[i]; };
     auto bin = [&](long i) {
-        const int k = iter[i] >> shift;
+        const int k = key(i) >> shift;
         return kOrderBins - 1 - (k < kOrderBins - 1 ? k : kOrderBins - 1);
     };
     for (long i = t; i < B; i += kOrderT) atomicAdd(&cnt[bin(i)], 1);
@@ -489,7 +491,10 @@ __global__ __launch_bounds__(kOrderT) void k_order(const int* __restrict__ iter,
         }
     }
     __syncthreads();
-    for (long i = t; i < B; i += kOrderT) order[atomicAdd(&cnt[bin(i)], 1)] = (int)i;
+    for (long i = t; i < B; i += kOrderT) {
+        order[atomicAdd(&cnt[bin(i)], 1)] = (int)i;
+        if (odecay) pred[i] = (int)(((long)key(i) * odecay) >> 3);  // (only thread t reads / writes pred[i])
+    }
 }
 
 hipError_t launch_order(const KParams& p, long B, hipStream_t st) {
@@ -500,7 +505,7 @@ hipError_t launch_order(const KParams& p, long B, hipStream_t st) {
     int shift = 0;
     while ((p.max_iter >> shift) >= kOrderBins) ++shift;
     hipLaunchKernelGGL(k_order, dim3(1), dim3(kOrderT), 0, st, (const int*)p.iter, const_cast<int*>(p.order), B,
-                       shift);
+                       shift, p.odecay && p.pred ? p.pred : nullptr, p.odecay && p.pred ? p.odecay : 0);
     return hipGetLastError();
 }
 // Streaming copy (mpcqp_debug_copy, bench.py's achievable-HBM reference): each lane moves G

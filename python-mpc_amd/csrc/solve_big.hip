@@ -1253,6 +1253,11 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
             for (int k = 8; k < 15; ++k) p.prof[b * kProfSlots + k] = L.pacc[k];
             p.prof[b * kProfSlots + 6] = clock64() - t0c;
             p.prof[b * kProfSlots + 7] = wall_clock64() - t0w;
+            p.prof[b * kProfSlots + 15] = t0w;  // (the start, for the dispatch timeline)
+            if constexpr (!IF) {  // the CU: HW_REG_HW_ID, HW_REG_XCC_ID (tools/dispatch_timeline.py)
+                p.prof[b * kProfSlots + 22] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
+                p.prof[b * kProfSlots + 23] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11));
+            }
             if constexpr (IF) {  // wave 0: its chain, T and X; wave 1 (below): its chain
                 p.prof[b * kProfSlots + 16] = pwr[0];
                 p.prof[b * kProfSlots + 18] = pwr[2];

@@ -1,0 +1,18 @@
+# Same-box A/B of the long-horizon kernel's persistent form: this build (persistent; and with
+# MPCQP_PERSIST=0) against ab/prev, with and without the history predictor (MPCQP_ORDER_DECAY).
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp; cd "$GRAFT_REPO_ROOT" || exit 1
+o=gpurun_out/$1; mkdir -p $o
+PREV=$GRAFT_REPO_ROOT/ab/prev/python-mpc_amd
+timeout -k 10 120 python3 tools/lchain_check.py $o/new.npz > $o/check.log 2>&1 || exit 1
+MPCQP_PKG=$PREV timeout -k 10 120 python3 tools/lchain_check.py $o/prev.npz >> $o/check.log 2>&1 || exit 1
+python3 tools/lchain_check.py --compare $o/new.npz $o/prev.npz >> $o/check.log 2>&1; rm -f $o/new.npz $o/prev.npz
+C="--config 5 --no-cpu --no-pcie --no-latency --no-dispatch-ab --steps 8 --warmup 3"
+for r in 1 2; do
+  timeout -k 10 200 python3 bench.py $C > $o/new.$r.json 2>>$o/err || exit 1
+  MPCQP_PERSIST=0 timeout -k 10 200 python3 bench.py $C > $o/nopersist.$r.json 2>>$o/err || exit 1
+  MPCQP_PKG=$PREV timeout -k 10 200 python3 bench.py $C > $o/prev.$r.json 2>>$o/err || exit 1
+  MPCQP_ORDER_DECAY=6 timeout -k 10 200 python3 bench.py $C > $o/new_d6.$r.json 2>>$o/err || exit 1
+done
+timeout -k 10 200 python3 tools/latency_ab.py 5 > $o/lat_new.json 2>>$o/err || exit 1
+echo ok > $o/ok
