@@ -1426,6 +1426,51 @@ def test_long_horizon_factor_reuse_is_exact(monkeypatch):
 
 
 @pytest.mark.gpu
+def test_dispatch_history_moves_no_result(monkeypatch):
+    """The dispatch order with history (kernels.hip::k_order, KParams::pred / odecay: the default
+    7/8 decay against MPCQP_ORDER_DECAY=0, the previous count alone) only moves instances
+    between workgroup slots: a cfg-5 batch larger than the resident slots, solved four times
+    with moving bounds (the order changes between solves), agrees bit for bit."""
+    import torch
+    from osqp_amd import DeviceBatch, _drop_common_zeros
+    B = 1024
+    b = mpc.make_batch(5, B=B, seed=29)
+    P, Px = _drop_common_zeros(b["P"], b["Px"])
+    A, Ax = _drop_common_zeros(b["A"], b["Ax"])
+    s = {k: v for k, v in b["settings"].items() if k != "verbose"}
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    dPx, dAx, dq = t(Px), t(Ax), t(b["q"])
+    rng = np.random.default_rng(3)
+    bounds = []
+    for k in range(4):
+        l, u = b["l"].copy(), b["u"].copy()
+        eq = np.isfinite(l) & np.isfinite(u) & (l == u)
+        sh = rng.normal(scale=0.01, size=l.shape) * eq
+        bounds.append((t(l + sh), t(u + sh)))
+    torch.cuda.synchronize()
+    hs = []
+    for dec in ("7", "0"):
+        monkeypatch.setenv("MPCQP_ORDER_DECAY", dec)
+        hs.append(DeviceBatch(P, A, B, device=0, **s))
+    monkeypatch.delenv("MPCQP_ORDER_DECAY")
+    for l, u in bounds:
+        outs = []
+        for h in hs:
+            o = (torch.empty((B, b["n"]), dtype=torch.float64, device=dev),
+                 torch.empty((B, b["m"]), dtype=torch.float64, device=dev),
+                 torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev))
+            h.setup(dPx, dAx, dq, l, u)
+            h.solve(*o)
+            h.synchronize()
+            outs.append([v.cpu().numpy() for v in o])
+        for a, c in zip(*outs):
+            assert np.array_equal(a.view(np.int64) if a.dtype == np.float64 else a,
+                                  c.view(np.int64) if c.dtype == np.float64 else c)
+        assert (outs[0][2] == 1).mean() > 0.99
+
+
+@pytest.mark.gpu
 def test_long_horizon_lds_chain_is_exact(monkeypatch):
     """The long-horizon factorisation's chain on LDS copies of its tiles (round 6,
     solve_big.hip::factorize2s_lds_chain) against the workspace form (MPCQP_LDS_CHAIN=0): the
