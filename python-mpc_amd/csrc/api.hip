@@ -338,6 +338,7 @@ size_t workspace_bytes(const Plan& pl, long B, bool with_io) {
     carve<signed char>(off, B * m);
     for (int i = 0; i < 8; ++i) carve<int>(off, B);
     carve<int>(off, 1);  // done (fused order epilogue)
+    carve<int>(off, 2);  // queue (k_solve_b's persistent form)
     carve<long long>(off, B * kProfSlots);
     carve<KParams>(off, 1);
     if (with_io) {
@@ -414,6 +415,10 @@ int alloc_shard(mpcqp_handle* h, Shard& s, bool with_io, bool sync = true) {
         if (const char* ev = getenv("MPCQP_DISPATCH"); ev && !strcmp(ev, "identity")) k.order = nullptr;  // A/B
     }
     int* const done = (int*)(base + carve<int>(off, 1));  // zero from the memset above
+    k.queue = (int*)(base + carve<int>(off, 2));          // zero from the memset above
+    k.qpersist = !(getenv("MPCQP_PERSIST") && getenv("MPCQP_PERSIST")[0] == '0');
+    k.persist = 0;
+    k.qn = 0;
     k.prof = nullptr;
     if (const char* ev = getenv("MPCQP_PHASE_PROF"); ev && ev[0] == '1')
         k.prof = (long long*)(base + carve<long long>(off, B * kProfSlots));

@@ -92,6 +92,12 @@ struct KParams {
     // alone)
     int* pred;
     int odecay;
+    // k_solve_b's persistent form (solve_big.hip; MPCQP_PERSIST=0: off): queue[0] the next index
+    // of the order, queue[1] the workgroups done (zero between launches); persist / qn per launch
+    int* queue;
+    int qpersist;
+    int persist;
+    long qn;
 };
 constexpr long kOrderFuseMax = 16384;  // larger batches sort in k_order (1024 threads)
 

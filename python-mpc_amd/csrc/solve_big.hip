@@ -973,305 +973,52 @@ __host__ __device__ inline int big_fg_len(const KP& p) {
 // TTK = 512: TwoSided / twisted_solve (nb up to 24); TTK = 128: TwoSidedW / wave_twisted_solve (nb <= 8).
 // NS: the most steps one chain takes, max(p, nb-1-p).
 template <int TTK, int NS, int K, int CS, int RS, bool IF = false>
+__device__ __forceinline__ void solve_b_body(const KParams& p, const long b, double* __restrict__ xo,
+                                             double* __restrict__ yo, int factor_only) {
+    const int tid = threadIdx.x;
+#include "solve_big_body.inc"
+}
+
+// The kernel: one workgroup per instance in the dispatch order, or -- PERSIST, for a batch
+// larger than the resident slots (go_b; MPCQP_PERSIST=0 turns it off) -- one workgroup per
+// resident slot taking the next instance of the order from a counter as soon as it finishes one.
+// The command processor issues a grid in order and holds it while the next workgroup's XCD has
+// no free CU (profiles/r6/dispatch.txt): the persistent form never waits on it.  Its body inlined
+// into the loop spills 29 VGPRs (4.6 % a solve, pinned in tests/test_isa_shape.py; the body text
+// in a lambda instead of solve_b_body: 40) and still wins (cfg 5 274.7 k -> 292 k); the
+// one-instance form includes the same body text straight into the kernel
+// (solve_big_body.inc), so its code is the stand-alone kernel's.  Each instance's arithmetic is
+// the same either way.
+template <int TTK, int NS, int K, int CS, int RS, bool IF = false, bool PERSIST = false>
 __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restrict__ xo, double* __restrict__ yo,
                                                    int factor_only) {
+    if constexpr (!PERSIST) {
+        const int tid = threadIdx.x;
+        const long b = instance_of(p);
+#include "solve_big_body.inc"
+    } else {
     const int tid = threadIdx.x;
-    const long b = instance_of(p);
-    const int n = p.n, m = p.m, npad = p.npad, nnzP = p.nnzP, nnzA = p.nnzA, nb = p.nb, amax = p.amax;
-    SL2 C = carve(p);
-    SLds& L = C.L;
-    double* X = C.X;
-    double* Z = C.Z;
-    double* dY = C.dY;
-    double* Fc = big_fc(L);
-    double* Gc = Fc + p.pmeet * amax * FGS;
-    int* toffL = (int*)(Fc + big_fg_len(p));  // the plan's toff[], after the F/G region
-    const double* Fg = p.F + b * (long)nb * SS;
-    const double* Hg = p.H + b * (long)nb * SS;
-    const double* Sg = p.Si + b * (long)nb * SS;
-
-    if (p.err[b]) {  // invalid data (flagged by setup/update): NaN outputs
-        for (int j = tid; j < n; j += TTK) if (xo) xo[b * n + j] = __builtin_nan("");
-        for (int i = tid; i < m; i += TTK) if (yo) yo[b * m + i] = __builtin_nan("");
-        if (tid == 0) fail_status(p, b);
-        return;
-    }
-
-#ifdef MPCQP_PHASE_PROF
-    long long tph = 0, t0c = 0, t0w = 0;
-    const bool prof = p.prof != nullptr;
-    if (prof) { t0w = wall_clock64(); t0c = tph = clock64(); if (tid < 16) L.pacc[tid] = 0; }
-#define PH(k) if (prof && tid == 0) { const long long t_ = clock64(); L.pacc[k] += t_ - tph; tph = t_; }
-#else
-#define PH(k)
-#endif
-
-    const double cval = p.scal[b * 4 + 0], cinv = p.scal[b * 4 + 1];
-    double rho = p.scal[b * 4 + 2];
-    const double sigma = p.sigma, alpha = p.alpha;
-    const bool warm = p.warm_start != 0;
-    for (int e = tid; e < nnzA; e += TTK) L.Acsc[e] = p.Ax[b * nnzA + e];
-    if (tid == 0) L.Acsc[nnzA] = 0.0;  // the gather lists' padding slot
-    for (int v = tid; v < nnzP; v += TTK) L.Pv[v] = p.Px[b * nnzP + v];
-    if (tid == 0) L.Pv[nnzP] = 0.0;
-    for (int i = tid; i < m; i += TTK) {
-        L.lo[i] = p.l[b * m + i];
-        L.up[i] = p.u[b * m + i];
-        L.ct[i] = p.ct[b * m + i];
-        Z[i] = warm ? p.z[b * m + i] : 0.0;
-        dY[i] = 0.0;
-    }
-    for (int pc = tid; pc < npad; pc += TTK) {
-        L.qv[pc] = p.q[b * npad + pc];
-        X[pc] = warm ? p.x[b * npad + pc] : 0.0;
-    }
-    if (tid < 16) L.res[tid] = 0.0;
-    if (tid < 4) L.flag[tid] = 0;
-    for (int k = tid; k < nb; k += TTK) toffL[k] = p.toff[k];
-    for (int e = tid; e < 2 * npad; e += TTK) L.cor[e] = 0.0;  // corT | corB of the sweep (cor, tv)
-
-    int status = MPCQP_UNSOLVED_, rho_updates = 0, iter = 0, info_iter = 0;
-#ifdef MPCQP_PHASE_PROF
-    long long pwr[6] = {0, 0, 0, 0, 0, 0};  // the interface form's per-wave sub-phase times (iface_solve)
-#endif
-    // the workspace factor is the current one (KParams::ffresh: this instance's convexity check
-    // at setup, or its previous solve, factored K at this rho and these row classes): start
-    // without refactoring -- the single-QP path's setup() + solve() factored twice before
-    const bool fresh = p.reuse && p.ffresh[b] == 1 && p.scal[b * 4 + 3] == rho;
-    if (fresh && factor_only) return;
-    bool can_check = false, need_factor = !fresh;
-    bool frows = true;  // the F / G rows must be (re)loaded into LDS at the next run start
-    // y in registers for the whole solve (ys is its LDS copy for the out-of-line phases)
-    double y[RS];
-#pragma unroll
-    for (int s = 0; s < RS; ++s) {
-        const int i = tid + s * TTK;
-        y[s] = (i < m && warm) ? p.y[b * m + i] : 0.0;
-    }
-    PH(5)
-    for (;;) {
+    int* const slot = carve(p).L.flag + 8;  // (a flag word the body does not use)
+    auto next = [&]() -> long {
+        if (tid == 0) *slot = atomicAdd(p.queue, 1);
         __syncthreads();
-        if (need_factor) {  // start, and after a rho change
-            need_factor = false;
-            const bool ok = factorize2_nl<TTK>(p.self, b, rho, Fc);  // scratch tiles in the F/G region
-            frows = true;
-            if (!ok) {
-                if (tid == 0) p.ffresh[b] = 0;
-                if (iter == 0) {
-                    for (int j = tid; j < n; j += TTK) if (xo) xo[b * n + j] = __builtin_nan("");
-                    for (int i = tid; i < m; i += TTK) if (yo) yo[b * m + i] = __builtin_nan("");
-                    if (tid == 0) fail_status(p, b);
-                    return;
-                }
-                status = MPCQP_NON_CVX_;
-                can_check = true;  // skip the final check_termination
-                break;
-            }
-            if (factor_only) {
-                if (tid == 0) p.ffresh[b] = 1;
-                return;
-            }
-            PH(0)
-        }
-        // ---- run state (re-derived at every run start; nothing but scalars lives across calls) ----
-        std::conditional_t<IF, TwoSidedQ<NS + 1>,
-                           std::conditional_t<TTK == 512, TwoSided<NS + 1>,
-                                              std::conditional_t<TTK == 256, TwoSided4<NS + 1>, TwoSidedW<NS>>>> RF;
-        int so[NS + 1], fo[NS + 1];  // (TTK == 512, NS < 10: twisted_solve's step offsets)
-        // the interface form: toff[lane] in one VGPR (iface_solve::toff_of)
-        int tvl = 0;
-        if constexpr (IF) {
-            tvl = (tid & 63) < nb ? toffL[tid & 63] : 0;
-            asm volatile("" : "+v"(tvl));
-        }
-        if constexpr (!IF && (TTK == 512 || TTK == 256) && NS < 10)
-            step_offsets<NS + 1, TTK>(p, toffL, L.rb, L.xt, L.tv, Fc, so, fo);
-        int cvar[CS];
-        // gather lists as LDS-base offsets (GatherR): A' w for the rhs, A x~ for the rows
-        extern __shared__ __attribute__((aligned(16))) double smb[];
-        const unsigned oA = (unsigned)(L.Acsc - smb), oW = (unsigned)(L.w - smb), oXt = (unsigned)(L.xt - smb);
-        // the list strides from the kernel arguments through an empty asm per run (not a load of
-        // p.self's copy in front of the list loads; not hoisted out of the run loop either)
-        int stc = npad, str = m;
-        asm volatile("" : "+s"(stc), "+s"(str));
-        GatherR<K> cg[CS];
-#pragma unroll
-        for (int s = 0; s < CS; ++s) {
-            const int pc = tid + s * TTK;
-            cvar[s] = pc < npad ? p.pad_var[pc] : -1;
-            if (pc < npad) cg[s].load(p.gcol + pc, stc, oA, oW);
-            else cg[s].clear(nnzA, oA, oW);
-        }
-        GatherR<K> rg[RS];
-#pragma unroll
-        for (int s = 0; s < RS; ++s) {
-            const int i = tid + s * TTK;
-            if (i < m) {
-                rg[s].load(p.grow + i, str, oA, oXt);
-                L.w[i] = rho_of(L.ct[i], rho) * Z[i] - y[s];  // w = rho z_prev - y (rho may be new)
-            } else {
-                rg[s].clear(nnzA, oA, oXt);
-            }
-        }
-        // the factor last: global loads return in order, so the rhs phase waits for the lists
-        // alone and the factor's loads stay in flight under it (the sweep is their first use)
-        if constexpr (IF || TTK == 512) {
-            RF.load(nb, p.pmeet, amax, p.bmax, Fg, Hg, Sg, Fc, Gc, frows);
-            frows = false;
-        } else {
-            RF.load(nb, p.pmeet, amax, p.bmax, Fg, Hg, Sg, Fc, Gc);
-        }
-        int stop_at = p.max_iter;
-        if (p.check_term) stop_at = min(stop_at, (iter / p.check_term + 1) * p.check_term);
-        if (p.adaptive_rho && p.rho_interval) stop_at = min(stop_at, (iter / p.rho_interval + 1) * p.rho_interval);
+        const long i = __builtin_amdgcn_readfirstlane(*slot);
         __syncthreads();
-        PH(5)
-        const double r_hi = RHO_EQ_OVER_RHO_INEQ * rho;
-        double ri_lo = 1.0 / RHO_MIN, ri_mid = 1.0 / rho, ri_hi = 1.0 / r_hi;
-        // (through an empty asm: seen as reciprocals, the row update's select among them was
-        // folded into one division of the selected rho -- a full f64 division per row per
-        // iteration inside the loop)
-        asm volatile("" : "+v"(ri_mid), "+v"(ri_hi));
-        while (iter < stop_at) {
-            ++iter;
-            int opq = 0;
-            asm volatile("" : "+s"(opq));
-            const int tido = tid + opq;
-            // rhs = sigma x_prev - q + A' (rho z_prev - y)
-#pragma unroll
-            for (int s = 0; s < CS; ++s) {
-                const int pc = tido + s * TTK;
-                if (pc < npad)
-                    L.rb[pc] = cvar[s] >= 0 ? (sigma * X[pc] - L.qv[pc]) + cg[s].dot() : 0.0;
-            }
-            __syncthreads();
-            PH(1)
-#ifdef MPCQP_PHASE_PROF
-            long long* pacc = prof ? L.pacc : nullptr;
-#else
-            long long* pacc = nullptr;
-#endif
-#ifdef MPCQP_PHASE_PROF
-            long long* pwp = prof ? pwr : nullptr;
-#else
-            long long* pwp = nullptr;
-#endif
-            if constexpr (IF) iface_solve<NS + 1>(RF, p, Fc, Gc, tvl, L.rb, L.xt, L.tv, L.cor, pacc, pwp);
-            else if constexpr (TTK == 512) twisted_solve<NS + 1>(RF, p, Fc, Gc, toffL, so, fo, L.rb, L.xt, L.tv, pacc);
-            else if constexpr (TTK == 256) twisted_solve4<NS + 1>(RF, p, Fc, Gc, toffL, so, fo, L.rb, L.xt, L.tv, pacc);
-            else wave_twisted_solve<NS>(RF, p, Fc, Gc, toffL, L.rb, L.xt, L.cor, pacc);
-            PH(2)
-            // z~ = A x~ ; relaxed + projected z ; y ; next w.   x update; deltas for the checks.
-#pragma unroll
-            for (int s = 0; s < RS; ++s) {
-                const int i = tido + s * TTK;
-                if (i < m) {
-                    const double zt = rg[s].dot();
-                    const signed char cl = L.ct[i];
-                    const double rv = cl < 0 ? RHO_MIN : (cl > 0 ? r_hi : rho);
-                    const double rvi = cl < 0 ? ri_lo : (cl > 0 ? ri_hi : ri_mid);
-                    const double zr = alpha * zt + (1.0 - alpha) * Z[i];
-                    const double zn = cmin(cmax(zr + rvi * y[s], L.lo[i]), L.up[i]);
-                    const double d = rv * (zr - zn);
-                    Z[i] = zn;
-                    dY[i] = d;
-                    y[s] += d;
-                    L.w[i] = rv * zn - y[s];
-                }
-            }
-#pragma unroll
-            for (int s = 0; s < CS; ++s) {
-                const int pc = tido + s * TTK;
-                if (pc < npad) {
-                    const double xold = X[pc];
-                    const double xn = alpha * L.xt[pc] + (1.0 - alpha) * xold;
-                    X[pc] = xn;
-                    L.rb[pc] = xn - xold;
-                }
-            }
-            __syncthreads();
-            PH(3)
-        }
-#pragma unroll
-        for (int s = 0; s < RS; ++s) { const int i = tid + s * TTK; if (i < m) L.ys[i] = y[s]; }
+        return i;
+    };
+    long idx = next();
+#pragma unroll 1
+    while (idx < p.qn) {
+        const long b = p.order ? (long)__builtin_amdgcn_readfirstlane(p.order[idx]) : idx;
+        solve_b_body<TTK, NS, K, CS, RS, IF>(p, b, xo, yo, factor_only);
         __syncthreads();
-        // ---- out-of-line phases ----
-        can_check = p.check_term && (iter % p.check_term == 0);
-        const bool do_rho = p.adaptive_rho && p.rho_interval && (iter % p.rho_interval == 0);
-        if (!can_check && !do_rho) break;  // max_iter reached
-        update_info_nl<TTK>(p.self, b, cinv);
-        info_iter = iter;
-        bool stop = false;
-        if (can_check) {
-            status = check_termination_nl<TTK>(p.self, b, cval, cinv, 0);
-            stop = status != MPCQP_UNSOLVED_;
-        }
-        if (!stop && do_rho) {
-            Res R;
-            R.restore(L.res);
-            const double pr = R.rpri / (cmax(R.rz, R.rax) + DIVISION_TOL);
-            const double du = R.rdua / (cmax(cmax(R.rq, R.raty), R.rpx) + DIVISION_TOL);
-            double rn = rho * sqrt(pr / (du + DIVISION_TOL));
-            rn = cmin(cmax(rn, RHO_MIN), RHO_MAX);
-            if (rn > rho * p.rho_tol || rn < rho / p.rho_tol) {
-                rho = cmin(cmax(rn, RHO_MIN), RHO_MAX);
-                rho_updates++;
-                need_factor = true;
-            }
-        }
-        __syncthreads();
-        PH(4)
-        if (stop || iter >= p.max_iter) break;
+        idx = next();
     }
-    if (!can_check && status == MPCQP_UNSOLVED_) {
-        update_info_nl<TTK>(p.self, b, cinv);
-        info_iter = iter;
-        status = check_termination_nl<TTK>(p.self, b, cval, cinv, 0);
+    if (tid == 0 && atomicAdd(p.queue + 1, 1) == (int)gridDim.x - 1) {
+        __hip_atomic_store(p.queue, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(p.queue + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    const bool has_sol = !(status == MPCQP_PRIMAL_INFEASIBLE_ || status == MPCQP_PRIMAL_INFEASIBLE_INACCURATE_ ||
-                           status == MPCQP_DUAL_INFEASIBLE_ || status == MPCQP_DUAL_INFEASIBLE_INACCURATE_ ||
-                           status == MPCQP_NON_CVX_);
-    if (has_sol) objective_nl<TTK>(p.self, cinv);
-    if (status == MPCQP_UNSOLVED_) {
-        status = check_termination_nl<TTK>(p.self, b, cval, cinv, 1);
-        if (status == MPCQP_UNSOLVED_) status = MPCQP_MAX_ITER_REACHED_;
     }
-    finalize_nl<TTK>(p.self, b, xo, yo, cinv, rho, status, info_iter, rho_updates, p.ostat, p.oiter);
-    // the workspace now holds the factor of the final rho (the next solve's): fresh unless the
-    // last factorisation failed, or a rho step at the last iteration (max_iter a multiple of the
-    // rho interval) left the refactorisation it asked for undone -- finalize_nl stores that new
-    // rho, while F / H / Si still hold the old one's factor (OSQP 0.6 refactors inside adapt_rho)
-    if (tid == 0) p.ffresh[b] = (status == MPCQP_NON_CVX_ || need_factor) ? 0 : 1;
-#ifdef MPCQP_PHASE_PROF
-    if (prof) {
-        __syncthreads();
-        PH(5)
-        if (tid == 0) {
-#pragma unroll
-            for (int k = 0; k < 6; ++k) p.prof[b * kProfSlots + k] = L.pacc[k];
-#pragma unroll
-            for (int k = 8; k < 15; ++k) p.prof[b * kProfSlots + k] = L.pacc[k];
-            p.prof[b * kProfSlots + 6] = clock64() - t0c;
-            p.prof[b * kProfSlots + 7] = wall_clock64() - t0w;
-            p.prof[b * kProfSlots + 15] = t0w;  // (the start, for the dispatch timeline)
-            if constexpr (!IF) {  // the CU: HW_REG_HW_ID, HW_REG_XCC_ID (tools/dispatch_timeline.py)
-                p.prof[b * kProfSlots + 22] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
-                p.prof[b * kProfSlots + 23] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11));
-            }
-            if constexpr (IF) {  // wave 0: its chain, T and X; wave 1 (below): its chain
-                p.prof[b * kProfSlots + 16] = pwr[0];
-                p.prof[b * kProfSlots + 18] = pwr[2];
-                p.prof[b * kProfSlots + 20] = pwr[4];
-                p.prof[b * kProfSlots + 21] = pwr[5];
-            }
-        }
-        if (IF && tid == 64) {
-            p.prof[b * kProfSlots + 17] = pwr[0];
-            p.prof[b * kProfSlots + 19] = pwr[2];
-        }
-    }
-#endif
-#undef PH
 }
 
 size_t lds_solve_bytes_big(const KParams& p) {
@@ -1300,9 +1047,19 @@ static hipError_t go_b(const KParams& p, long B, double* xo, double* yo, int fo,
         if (big_iface() && p.ifok) k = k_solve_b<TTK, NS, K, CS, RS, true>;
 #endif
     if (ref) { *ref = {(const void*)k, TTK, lds}; return hipSuccess; }
+    KParams q = p;
+    q.persist = !fo && p.queue && p.qpersist && p.slots > 0 && B > p.slots;
+    q.qn = B;
+    if (q.persist) {
+        k = k_solve_b<TTK, NS, K, CS, RS, false, true>;
+#ifdef MPCQP_EXPERIMENTAL
+        if constexpr (TTK == 512)
+            if (big_iface() && p.ifok) k = k_solve_b<TTK, NS, K, CS, RS, true, true>;
+#endif
+    }
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(TTK), lds, st, p, xo, yo, fo);
+    hipLaunchKernelGGL(k, dim3((unsigned)(q.persist ? p.slots : B)), dim3(TTK), lds, st, q, xo, yo, fo);
     return hipGetLastError();
 }
 

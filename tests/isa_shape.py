@@ -77,7 +77,9 @@ HOT = {
     # configs[2] / [3]: the slack layouts' eliminated-column instantiation
     "cfg3": ("_ZN5mpcqp16k_setup_solve_w4ILi6ELi4ELi8ELi8ELi3ELb1ELi8ELb0ELb0ELi0EE", "w4"),
     # configs[4]: the long-horizon two-sided kernel, variant 12
-    "cfg5": ("_ZN5mpcqp9k_solve_bILi512ELi9ELi8ELi2ELi2ELb0EE", "big"),
+    "cfg5": ("_ZN5mpcqp9k_solve_bILi512ELi9ELi8ELi2ELi2ELb0ELb0EE", "big"),
+    # ... and its persistent form (the batch path: the instance body inlined into the work loop)
+    "cfg5p": ("_ZN5mpcqp9k_solve_bILi512ELi9ELi8ELi2ELi2ELb0ELb1EE", "big"),
 }
 
 if __name__ == "__main__":

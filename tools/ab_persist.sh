@@ -12,7 +12,7 @@ for r in 1 2; do
   timeout -k 10 200 python3 bench.py $C > $o/new.$r.json 2>>$o/err || exit 1
   MPCQP_PERSIST=0 timeout -k 10 200 python3 bench.py $C > $o/nopersist.$r.json 2>>$o/err || exit 1
   MPCQP_PKG=$PREV timeout -k 10 200 python3 bench.py $C > $o/prev.$r.json 2>>$o/err || exit 1
-  MPCQP_ORDER_DECAY=6 timeout -k 10 200 python3 bench.py $C > $o/new_d6.$r.json 2>>$o/err || exit 1
+  MPCQP_ORDER_DECAY=0 timeout -k 10 200 python3 bench.py $C > $o/new_d0.$r.json 2>>$o/err || exit 1
 done
 timeout -k 10 200 python3 tools/latency_ab.py 5 > $o/lat_new.json 2>>$o/err || exit 1
 echo ok > $o/ok
