@@ -31,6 +31,7 @@
 #include <type_traits>
 
 #include "solve_phases.h"
+#include "wave_util.h"
 
 namespace mpcqp {
 
@@ -778,12 +779,13 @@ __device__ __forceinline__ double dot4c(const double (&a)[4], const double (&v)[
 // chain's rows [0, amax): when those are disjoint (toff_p >= amax: the middle block's first and
 // last BFS levels apart, every long-horizon workload here) the bottom chain updates rb in place
 // like every other step, and the middle step reads w_p alone (no corB reads or subtraction).
-__device__ __forceinline__ int middle_apart(const KParams& p, const int* toffL) {
+template <class KP>
+__device__ __forceinline__ int middle_apart(const KP& p, const int* toffL) {
     return p.apart && p.pmeet < p.nb - 1 && toffL[p.pmeet] >= p.amax;
 }
 
-template <int SL, int TT = 512>
-__device__ __forceinline__ void step_offsets(const KParams& p, const int* toffL, const double* rb, const double* xt,
+template <int SL, int TT = 512, class KP>
+__device__ __forceinline__ void step_offsets(const KP& p, const int* toffL, const double* rb, const double* xt,
                                              const double* corB, const double* Fc, int (&so)[SL], int (&fo)[SL]) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int half = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / (TT / 2)));
@@ -808,8 +810,8 @@ __device__ __forceinline__ void step_offsets(const KParams& p, const int* toffL,
     }
 }
 
-template <int SL>
-__device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KParams& p, const double* Fc,
+template <int SL, class KP>
+__device__ __forceinline__ void twisted_solve(const TwoSided<SL>& R, const KP& p, const double* Fc,
                                               const double* Gc, const int* toffL, const int (&so)[SL],
                                               const int (&fo)[SL], double* rb, double* xt, double* corB,
                                               long long* pacc) {
@@ -973,9 +975,15 @@ __host__ __device__ inline int big_fg_len(const KP& p) {
 // TTK = 512: TwoSided / twisted_solve (nb up to 24); TTK = 128: TwoSidedW / wave_twisted_solve (nb <= 8).
 // NS: the most steps one chain takes, max(p, nb-1-p).
 template <int TTK, int NS, int K, int CS, int RS, bool IF = false>
-__device__ __forceinline__ void solve_b_body(const KParams& p, const long b, double* __restrict__ xo,
-                                             double* __restrict__ yo, int factor_only) {
-    const int tid = threadIdx.x;
+__device__ __forceinline__ void solve_b_body(const long b, double* __restrict__ xo, double* __restrict__ yo,
+                                             int factor_only) {
+    // the lane id and the parameter block (the kernel's first argument, at the start of the
+    // kernarg segment) through empty asms per instance: what the body derives from them is
+    // formed in the body, not hoisted out of the work loop and held across every solve
+    const int tid = opaque_v((int)threadIdx.x);
+    KPc* pk = (KPc*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(pk));
+    KPc& p = *pk;
 #include "solve_big_body.inc"
 }
 
@@ -984,11 +992,11 @@ __device__ __forceinline__ void solve_b_body(const KParams& p, const long b, dou
 // resident slot taking the next instance of the order from a counter as soon as it finishes one.
 // The command processor issues a grid in order and holds it while the next workgroup's XCD has
 // no free CU (profiles/r6/dispatch.txt): the persistent form never waits on it.  Its body inlined
-// into the loop spills 29 VGPRs (4.6 % a solve, pinned in tests/test_isa_shape.py; the body text
-// in a lambda instead of solve_b_body: 40) and still wins (cfg 5 274.7 k -> 292 k); the
-// one-instance form includes the same body text straight into the kernel
-// (solve_big_body.inc), so its code is the stand-alone kernel's.  Each instance's arithmetic is
-// the same either way.
+// into the loop (solve_b_body, the lane id and the parameter block laundered per instance: 29
+// spilled VGPRs without, 40 with the body text in a lambda) keeps one spilled scalar in the
+// sweep steps (pinned in tests/test_isa_shape.py) and wins: cfg 5 274.3 k -> 294.2 k.  The
+// one-instance form includes the same body text straight into the kernel (solve_big_body.inc),
+// so its code is the stand-alone kernel's.  Each instance's arithmetic is the same either way.
 template <int TTK, int NS, int K, int CS, int RS, bool IF = false, bool PERSIST = false>
 __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restrict__ xo, double* __restrict__ yo,
                                                    int factor_only) {
@@ -1010,7 +1018,7 @@ __global__ __launch_bounds__(TTK, 1) void k_solve_b(KParams p, double* __restric
 #pragma unroll 1
     while (idx < p.qn) {
         const long b = p.order ? (long)__builtin_amdgcn_readfirstlane(p.order[idx]) : idx;
-        solve_b_body<TTK, NS, K, CS, RS, IF>(p, b, xo, yo, factor_only);
+        solve_b_body<TTK, NS, K, CS, RS, IF>(b, xo, yo, factor_only);
         __syncthreads();
         idx = next();
     }

@@ -38,13 +38,13 @@ PINNED = {
     "cfg5": dict(vgpr_count=254, agpr_count=0, vgpr_spill_count=0, private_segment_fixed_size=20, sgpr_spill_max=238,
                  loop=dict(instructions=1606, barriers=21, readlane=39, scratch=0),
                  step_readlane=0, step_scratch=0),
-    # cfg 5's persistent form (round 6, the batch path: the instance body inlined into the work
-    # loop): 29 spilled VGPRs and v_readlane reloads in the sweep steps, none of them in a step's
-    # scratch; measured 4.6 % slower a solve than the plain kernel and 6.4 % faster a launch
-    # (no dispatcher wait: 274.2 k -> 291.7 k, profiles/r6/dispatch.txt).  Pinned so that a
-    # change that makes it worse shows
-    "cfg5p": dict(vgpr_count=256, agpr_count=0, vgpr_spill_count=29, private_segment_fixed_size=148,
-                  sgpr_spill_max=331, loop=dict(instructions=1661, barriers=21, readlane=94, scratch=0),
+    # cfg 5's persistent form (round 6, the batch path: the instance body inside the work loop,
+    # the lane id and the parameter block laundered per instance -- 29 spilled VGPRs without):
+    # v_readlane reloads of one spilled 64-bit scalar in the sweep steps, no scratch access in
+    # them; 294.2 k against the plain kernel's 275 k a launch (no dispatcher wait,
+    # profiles/r6/dispatch.txt).  Pinned so that a change that makes it worse shows
+    "cfg5p": dict(vgpr_count=256, agpr_count=0, vgpr_spill_count=0, private_segment_fixed_size=20,
+                  sgpr_spill_max=232, loop=dict(instructions=1659, barriers=21, readlane=90, scratch=0),
                   step_readlane=50, step_scratch=0),
 }
 
