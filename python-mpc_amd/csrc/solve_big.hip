@@ -348,7 +348,7 @@ __device__ __forceinline__ bool factorize2s_lds_chain(const KP& p, SLds& L, doub
                                                       double* __restrict__ Xl, const int ntop, const int nbot,
                                                       const int nst, bool okw) {
     constexpr int NW = TT / 64, HT = TT / 2;
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, half = tid / HT, u = tid % HT;
+    const int tid = threadIdx.x, w = tid >> 6, half = tid / HT, u = tid % HT;
     const int nb = p.nb, amax = p.amax, bmax = p.bmax, pm = p.pmeet;
 #if defined(MPCQP_PHASE_PROF) && defined(MPCQP_CHAIN_STAMPS)
     long long tc = clock64();  // (diagnostic: wave 0's products / corners / pivots, slots 8 / 10 / 11)
