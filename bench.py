@@ -85,6 +85,9 @@ def parse(argv=None):
                     help="mpcqp_set_one_shot (default on): the fused kernel keeps no workspace state for later "
                          "calls -- the reference's fresh OSQP() + setup() + solve() per call "
                          "(mpc_kinematics.py:194-198); outputs bit-identical to --no-one-shot's persisting kernel")
+    ap.add_argument("--fuse-warm", action=argparse.BooleanOptionalAction, default=True,
+                    help="cfg 5: setup() + warm_start() as one call (mpcqp_setup_warm_device, default on; one "
+                         "kernel where the wide batch setup applies), identical results to the two calls")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no HIP events in the timed region (roofline kernel_ms from the untimed pass)")
     ap.add_argument("--no-dispatch-ab", action="store_true",
@@ -564,6 +567,7 @@ def main(argv=None, solver_cls=None, device=None):
     one_shot = bool(args.one_shot and not warm and not args.separate_setup and hasattr(solver, "one_shot")
                     and solver.one_shot(True))
     xs = ys = None
+    fuse_warm = bool(warm and args.fuse_warm and hasattr(solver, "setup_warm"))
     if warm:
         # SURVEY.md §8d D2, cfg 5 ("warm-started ADMM"): solve once cold, shift the solution
         # one stage as the reference shifts its horizon (mpc_dynamics.py:589-610), and time
@@ -579,7 +583,10 @@ def main(argv=None, solver_cls=None, device=None):
         sl, su = seq[t]
         if args.assemble:  # F1: q, l, u from theta on the device, on the solver's stream order
             asm.assemble(ths[t], dreg, out=(dq, sl, su), stream=sv.stream_handle())
-        if warm:  # setup, then the warm start, then the solve
+        if warm and fuse_warm:  # setup + warm start in one call (mpcqp_setup_warm_device), then the solve
+            sv.setup_warm(dPx, dAx, dq, sl, su, xs, ys)
+            sv.solve(dx, dy, dst, dit)
+        elif warm:  # setup, then the warm start, then the solve
             sv.setup(dPx, dAx, dq, sl, su)
             sv.warm_start(xs, ys)
             sv.solve(dx, dy, dst, dit)
@@ -801,7 +808,10 @@ def main(argv=None, solver_cls=None, device=None):
                        "global_batch": B_global, "horizon_N": b["N"], "n": n, "m": m,
                        "nnz_triuP": nnzP, "nnz_A": nnzA, "nnz_A_per_instance": nnzA_alg,
                        "eps_abs": 1e-3, "eps_rel": 1e-3,
-                       "step": ("setup()+warm_start(base solution shifted one stage)+solve()" if warm else
+                       "step": ("setup()+warm_start(base solution shifted one stage)+solve()" +
+                                (" (mpcqp_setup_warm_device: setup + warm start one call"
+                                 + (", one kernel)" if solver.setup_warm_fused() else ")") if fuse_warm else "")
+                                if warm else
                                 "setup()+solve()" + ("" if args.separate_setup else
                                                      f" (mpcqp_setup_solve_device: one call; kernel {kname}"
                                                      + (", one-shot: no workspace state kept)" if one_shot else ")")))
@@ -809,6 +819,7 @@ def main(argv=None, solver_cls=None, device=None):
                                ("initial states drawn afresh)" if args.independent else
                                 f"initial states jittered +-{args.jitter:.0%} of the D2 ranges)"),
                        "one_shot": one_shot,
+                       "fuse_warm": fuse_warm,
                        "parallelism": f"batch-shard x{world}",
                        "dispatch": "longest previous solve first (kernels.hip::k_order), predicted from the "
                                    "previous step's different batch",

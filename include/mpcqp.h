@@ -184,6 +184,19 @@ int mpcqp_update_device(mpcqp_handle *h, const double *dq, const double *dl, con
 int mpcqp_warm_start_device(mpcqp_handle *h, const double *dx, const double *dy, void *stream);
 int mpcqp_solve_device(mpcqp_handle *h, double *dx, double *dy, int32_t *dstatus, int32_t *diters,
                        void *stream);
+/* setup + warm start of the same call: mpcqp_setup_device(dPx..du) followed by
+ * mpcqp_warm_start_device(dx0, dy0), with identical results (either may be null, as there).
+ * Where the wide batch setup applies (the long-horizon plans: setup_wide.h) both run as ONE
+ * kernel -- each workgroup scales its instance and forms x = D^-1 x0, y = E^-1 y0 c, z = A x
+ * from the values still on chip -- so the warm-start kernel's pass over the workspace goes.
+ * The reference's warm-started step prob.setup(...); prob.warm_start(x=, y=); prob.solve()
+ * (mpc_dynamics.py:589-610 shifting the previous solution) maps onto it
+ * followed by mpcqp_solve_device.  mpcqp_setup_warm_fused: 1 when the handle's plan takes the
+ * one-kernel form, 0 when the call runs as the two launches. */
+int mpcqp_setup_warm_device(mpcqp_handle *h, const double *dPx, const double *dAx, const double *dq,
+                            const double *dl, const double *du, const double *dx0, const double *dy0,
+                            void *stream);
+int mpcqp_setup_warm_fused(const mpcqp_handle *h);
 /* setup + solve of the same inputs in one call: mpcqp_setup_device(dPx..du) followed by
  * mpcqp_solve_device(dx, dy, dstatus, diters), with identical results.  Where the
  * solve kernel allows it -- the four-wave kernel k_setup_solve_w4 (the N=20 lateral

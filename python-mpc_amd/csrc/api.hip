@@ -1454,6 +1454,30 @@ int mpcqp_warm_start_device(mpcqp_handle* h, const double* dx, const double* dy,
     return stream_leave(s, st);
 }
 
+int mpcqp_setup_warm_device(mpcqp_handle* h, const double* dPx, const double* dAx, const double* dq,
+                            const double* dl, const double* du, const double* dx0, const double* dy0, void* stream) {
+    if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "device entry points need a single-device handle");
+    h->staged = false;  // (device work: the staged results of the last solve are stale)
+    Shard& s = h->shards[0];
+    hipStream_t st = pick(s, stream);
+    HIPCHK(hipSetDevice(s.dev));
+    if (int e = stream_enter(s, st)) return e;
+    if (h->collect_setup)
+        if (int e = ev_begin(h->collect_setup, h->ev_setup, st)) return e;
+    HIPCHK(launch_setup_warm(s.kp, s.B, dPx, dAx, dq, dl, du, dx0, dy0, st));
+    if (h->collect_setup)
+        if (int e = ev_end(h->collect_setup, h->ev_setup, st)) return e;
+    h->state_gone = false;
+    s.kp.warm_start = 1;
+    h->set.warm_start = 1;
+    return stream_leave(s, st);
+}
+
+int mpcqp_setup_warm_fused(const mpcqp_handle* h) {
+    if (!h || h->shards.empty()) return fail(MPCQP_EINVAL, "mpcqp_setup_warm_fused: null handle");
+    return setup_warm_fused(h->shards[0].kp) ? 1 : 0;
+}
+
 int mpcqp_solve_device(mpcqp_handle* h, double* dx, double* dy, int32_t* dstatus, int32_t* diters, void* stream) {
     if (int e = need_state(h, "mpcqp_solve_device")) return e;
     if (!h || h->shards.size() != 1) return fail(MPCQP_EINVAL, "device entry points need a single-device handle");

@@ -120,6 +120,11 @@ hipError_t launch_update_mat(const KParams& p, long B, double* Px_io, double* Ax
 hipError_t launch_update(const KParams& p, long B, const double* q, const double* l, const double* u,
                          hipStream_t st);
 hipError_t launch_warm(const KParams& p, long B, const double* x, const double* y, hipStream_t st);
+// launch_setup then launch_warm(x0, y0), identical results; one kernel where the wide batch
+// setup applies (setup_warm_fused: the long-horizon plans, setup_wide.h WARM)
+bool setup_warm_fused(const KParams& p);
+hipError_t launch_setup_warm(const KParams& p, long B, const double* Px, const double* Ax, const double* q,
+                             const double* l, const double* u, const double* x0, const double* y0, hipStream_t st);
 // longest-processing-time dispatch: sort the instances by the iteration count of the
 // solve just run (descending) into p.order, for the next solve on this workspace
 hipError_t launch_order(const KParams& p, long B, hipStream_t st);

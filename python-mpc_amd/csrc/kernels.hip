@@ -24,6 +24,7 @@
 
 #include "device_common.h"
 #include "setup_r.h"
+#include "setup_wide.h"
 #include "wave_util.h"
 
 namespace mpcqp {
@@ -187,18 +188,23 @@ __global__ __launch_bounds__(T) void k_setup_r(KParams p, const double* __restri
     setup_r_body<T, K, KP, 1, AS, PS, KEEP>(p, (long)blockIdx.x, Px_in, Ax_in, q_in, l_in, u_in, sm);
 }
 
-// the same for the long-horizon plans (cfg 5: npad 544, m 916, nnz(A) 2666): 1024 threads, one
-// padded column and one row per thread, three A values -- the register-list setup instead of
+// the same for the long-horizon plans (cfg 5: npad 544, m 916, nnz(A) 2666), setup_wide.h:
+// 1024 threads with one padded column, one row and three A values each for a few instances
+// (one instance per CU), 512 threads with two of each and six A values for batches (two
+// instances per CU: the setup is latency-bound) -- the register-list setup instead of
 // k_setup's index chains (one cfg-5 instance: ten Ruiz passes ~165 us there)
 constexpr int TWIDE = 1024;
-template <int K, int KP, int AS, int PS, bool KEEP>
-__global__ __launch_bounds__(TWIDE) void k_setup_rw(KParams p, const double* __restrict__ Px_in,
-                                                    const double* __restrict__ Ax_in,
-                                                    const double* __restrict__ q_in,
-                                                    const double* __restrict__ l_in,
-                                                    const double* __restrict__ u_in) {
+template <int TT, int CS, int AS, bool KEEP, bool WARM = false>
+__global__ __launch_bounds__(TT, TT == 512 ? 4 : 1) void k_setup_wide(KParams p, const double* __restrict__ Px_in,
+                                                                      const double* __restrict__ Ax_in,
+                                                                      const double* __restrict__ q_in,
+                                                                      const double* __restrict__ l_in,
+                                                                      const double* __restrict__ u_in,
+                                                                      const double* __restrict__ x0,
+                                                                      const double* __restrict__ y0) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    setup_r_body<TWIDE, K, KP, 1, AS, PS, KEEP>(p, (long)blockIdx.x, Px_in, Ax_in, q_in, l_in, u_in, sm);
+    setup_wide_body<TT, CS, CS, 8, 4, AS, CS, KEEP, WARM>(p, (long)blockIdx.x, Px_in, Ax_in, q_in, l_in, u_in, sm,
+                                                          x0, y0);
 }
 
 // ------------------------------------------------------- matrix update --
@@ -375,7 +381,9 @@ static int setup_r_variant(const KParams& p) {
     if (p.gk <= 8 && p.nnzA <= 3 * T && p.nnzP <= T) return 2;
     return 0;
 }
-// the 1024-thread one (k_setup_rw): 1 when it fits
+// the wide one (k_setup_wide): 1 when it fits; the 512-thread form from kSetupHalfB instances
+// (two per CU) -- fewer leave CUs idle, where the 1024-thread form's shorter latency wins
+constexpr long kSetupHalfB = 512;
 static int setup_rw_fits(const KParams& p) {
     return p.npad <= TWIDE && p.m <= TWIDE && p.pk <= 4 && p.gk <= 8 && p.nnzA <= 3 * TWIDE && p.nnzP <= TWIDE;
 }
@@ -392,11 +400,15 @@ hipError_t launch_setup(const KParams& p, long B, const double* Px, const double
         return hipGetLastError();
     }
     if (setup_rw_fits(p) && !getenv_flag("MPCQP_SETUP_STAGED")) {
-        const size_t lds = lds_setup_r_bytes(p.nnzP, p.nnzA, p.npad, p.m, TWIDE);
-        auto k = keep ? k_setup_rw<8, 4, 3, 1, true> : k_setup_rw<8, 4, 3, 1, false>;
+        // (the same columns / rows / values per workgroup either way: the fit is the same)
+        const size_t lds = lds_setup_wide_bytes(p.nnzP, p.nnzA, p.npad, p.m, TWIDE);
+        const bool half = B >= kSetupHalfB && !getenv_flag("MPCQP_SETUP_FULL");
+        auto k = half ? (keep ? k_setup_wide<512, 2, 6, true> : k_setup_wide<512, 2, 6, false>)
+                      : (keep ? k_setup_wide<TWIDE, 1, 3, true> : k_setup_wide<TWIDE, 1, 3, false>);
         hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(TWIDE), lds, st, p, Px, Ax, q, l, u);
+        hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(half ? 512 : TWIDE), lds, st, p, Px, Ax, q, l, u,
+                           (const double*)nullptr, (const double*)nullptr);
         return hipGetLastError();
     }
     size_t lds = lds_setup_bytes(p);
@@ -422,6 +434,21 @@ hipError_t launch_update(const KParams& p, long B, const double* q, const double
 }
 hipError_t launch_warm(const KParams& p, long B, const double* x, const double* y, hipStream_t st) {
     hipLaunchKernelGGL(k_warm, dim3((unsigned)B), dim3(T), 0, st, p, x, y);
+    return hipGetLastError();
+}
+bool setup_warm_fused(const KParams& p) { return setup_rw_fits(p) && !getenv_flag("MPCQP_SETUP_STAGED"); }
+hipError_t launch_setup_warm(const KParams& p, long B, const double* Px, const double* Ax, const double* q,
+                             const double* l, const double* u, const double* x0, const double* y0, hipStream_t st) {
+    if (!setup_warm_fused(p)) {
+        if (hipError_t e = launch_setup(p, B, Px, Ax, q, l, u, st, false); e != hipSuccess) return e;
+        return launch_warm(p, B, x0, y0, st);
+    }
+    const size_t lds = lds_setup_wide_bytes(p.nnzP, p.nnzA, p.npad, p.m, TWIDE);
+    const bool half = B >= kSetupHalfB && !getenv_flag("MPCQP_SETUP_FULL");
+    auto k = half ? k_setup_wide<512, 2, 6, false, true> : k_setup_wide<TWIDE, 1, 3, false, true>;
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(half ? 512 : TWIDE), lds, st, p, Px, Ax, q, l, u, x0, y0);
     return hipGetLastError();
 }
 

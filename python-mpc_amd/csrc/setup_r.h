@@ -28,7 +28,7 @@
 namespace mpcqp {
 
 __host__ __device__ inline size_t lds_setup_r_bytes(int nnzP, int nnzA, int npad, int m, int tt = 256) {
-    return sizeof(double) * ((size_t)nnzP + 1 + nnzA + 1 + npad + m + (tt > 512 ? tt / 32 : 8)) + 16;
+    return sizeof(double) * ((size_t)nnzP + 1 + nnzA + 1 + npad + m + (tt > 512 ? tt / 64 : 8)) + 16;
 }
 
 // ONE (the one-shot fused setup + solve, mpcqp_set_one_shot): the scaled problem is left in LDS
@@ -36,35 +36,6 @@ __host__ __device__ inline size_t lds_setup_r_bytes(int nnzP, int nnzA, int npad
 // q, x = z = 0) instead of in the workspace -- no later call reads it there; D, E, c and the
 // status slots are written as always
 // EDL (with ONE; one_shot_form 2): E and D too go to the carve (solve_phases.h::edl_E / edl_D)
-// WIDE gathers: the lists are padded at their ends with the zero slot, and the longest list
-// of a wave bounds what it reads -- span 0: one slot, 1: the first K/2, 2: all K (a wave's
-// span from a ballot in the prologue: uniform, so the branches are scalar).  The pads
-// leave the maximum as it is (vmax(|0|, d) = d for the d >= 0 the chain carries), so the
-// shorter chains give the same value.
-template <int K>
-__device__ __forceinline__ int wave_span(const unsigned (&g)[K], unsigned pad) {
-    int len = 0;
-#pragma unroll
-    for (int k = 0; k < K; ++k) len += g[k] != pad;
-    const bool gt1 = __builtin_amdgcn_ballot_w64(len > 1) != 0;
-    const bool gth = __builtin_amdgcn_ballot_w64(len > K / 2) != 0;
-    return gth ? 2 : gt1 ? 1 : 0;
-}
-template <int K>
-__device__ __forceinline__ double gather_max(const unsigned (&g)[K], int span) {
-    double d = 0.0;
-    if (span == 0) {
-        d = vmax(fabs(lds_at(g[0])), d);
-    } else if (span == 1) {
-#pragma unroll
-        for (int k = 0; k < (K + 1) / 2; ++k) d = vmax(fabs(lds_at(g[k])), d);
-    } else {
-#pragma unroll
-        for (int k = 0; k < K; ++k) d = vmax(fabs(lds_at(g[k])), d);
-    }
-    return d;
-}
-
 template <int TT, int K, int KP, int RS, int AS, int PS, bool KEEP = false, bool ONE = false, bool EDL = false>
 __device__ __forceinline__ void setup_r_body(const KParams& p, const long b, const double* __restrict__ Px_in,
                                              const double* __restrict__ Ax_in, const double* __restrict__ q_in,
@@ -76,12 +47,7 @@ __device__ __forceinline__ void setup_r_body(const KParams& p, const long b, con
     double* Ac = Pv + nnzP + 1;    // [nnzA + 1]  padded-CSC order, Ac[nnzA] = 0
     double* Dt = Ac + nnzA + 1;    // [npad]
     double* Et = Dt + npad;        // [m]
-    // WIDE (the 1024-thread batch setup, kernels.hip::k_setup_rw): the thread's own A and P
-    // values, column and row scalings stay in registers too (LDS keeps the copy the gathers
-    // read), and the cost scaling's sum and maximum share one LDS round among the waves that
-    // hold columns -- the others only add zeros there (see the pass below)
-    constexpr bool WIDE = TT > 512;
-    constexpr int NRED = WIDE ? TT / 32 : 8;  // block_sum / block_max: one slot per wave (WIDE: two)
+    constexpr int NRED = TT > 512 ? TT / 64 : 8;  // block_sum / block_max: one slot per wave
     double* red = Et + m;          // [NRED]
     int* flag = (int*)(red + NRED);
     const unsigned pbase = lds_addr(Pv), abase = lds_addr(Ac);
@@ -102,18 +68,8 @@ __device__ __forceinline__ void setup_r_body(const KParams& p, const long b, con
 #pragma unroll
     for (int k = 0; k < KP; ++k)
         pg[k] = pbase + 8u * (colv ? ((unsigned)p.gpsym[(long)k * npad + pc] & 0xFFFFu) : (unsigned)nnzP);
-    int spc = 2, spp = 2, spr[RS];  // (WIDE: the wave's gather spans)
-#pragma unroll
-    for (int s = 0; s < RS; ++s) spr[s] = 2;
-    if constexpr (WIDE) {
-        spc = wave_span<K>(cg, abase + 8u * (unsigned)nnzA);
-        spp = wave_span<KP>(pg, pbase + 8u * (unsigned)nnzP);
-#pragma unroll
-        for (int s = 0; s < RS; ++s) spr[s] = wave_span<K>(rg[s], abase + 8u * (unsigned)nnzA);
-    }
     const long bm = p.mat_shared ? 0 : b;  // LTI batches: one P, A for every instance
     int ar[AS], ac[AS], pr[PS], pcol[PS];
-    double av[WIDE ? AS : 1], pv[WIDE ? PS : 1];  // (WIDE: the thread's values)
 #pragma unroll
     for (int s = 0; s < AS; ++s) {
         const int e = tid + s * TT;
@@ -121,9 +77,7 @@ __device__ __forceinline__ void setup_r_body(const KParams& p, const long b, con
         const int v = in ? p.acsc_v[e] : 0;
         ar[s] = in ? p.acsc_row[e] : 0;
         ac[s] = in ? p.a_c[v] : 0;
-        const double x = in ? Ax_in[bm * nnzA + v] : 0.0;
-        if (in) Ac[e] = x;
-        if constexpr (WIDE) av[s] = x;
+        if (in) Ac[e] = Ax_in[bm * nnzA + v];
     }
 #pragma unroll
     for (int s = 0; s < PS; ++s) {
@@ -131,9 +85,7 @@ __device__ __forceinline__ void setup_r_body(const KParams& p, const long b, con
         const bool in = v < nnzP;
         pr[s] = in ? p.p_r[v] : 0;
         pcol[s] = in ? p.p_c[v] : 0;
-        const double x = in ? Px_in[bm * nnzP + v] : 0.0;
-        if (in) Pv[v] = x;
-        if constexpr (WIDE) pv[s] = x;
+        if (in) Pv[v] = Px_in[bm * nnzP + v];
     }
     if (tid == 0) { Pv[nnzP] = 0.0; Ac[nnzA] = 0.0; }
     double qv = colv ? q_in[b * n + p.pad_var[pc]] : 0.0, Dv = 1.0, Ev[RS];
@@ -142,40 +94,28 @@ __device__ __forceinline__ void setup_r_body(const KParams& p, const long b, con
     double c = 1.0;
     __syncthreads();
 
-    double dr = 1.0, er[RS];  // (WIDE: this pass's Dt[pc], Et[rows] in registers)
     for (int it = 0; it < p.scaling; ++it) {
         // compute_inf_norm_cols_KKT / rows + limit_scaling + sqrt + reciprocal
         if (pc < npad) {
             double d = 1.0;
             if (colv) {
                 double d1 = 0.0, d2 = 0.0;
-                if constexpr (WIDE) {
-                    d1 = gather_max<KP>(pg, spp);
-                    d2 = gather_max<K>(cg, spc);
-                } else {
 #pragma unroll
-                    for (int k = 0; k < KP; ++k) d1 = vmax(fabs(lds_at(pg[k])), d1);
+                for (int k = 0; k < KP; ++k) d1 = vmax(fabs(lds_at(pg[k])), d1);
 #pragma unroll
-                    for (int k = 0; k < K; ++k) d2 = vmax(fabs(lds_at(cg[k])), d2);
-                }
+                for (int k = 0; k < K; ++k) d2 = vmax(fabs(lds_at(cg[k])), d2);
                 d = 1.0 / sqrt(limit_scaling(vmax(d1, d2)));
             }
             Dt[pc] = d;
-            dr = d;
         }
 #pragma unroll
         for (int s = 0; s < RS; ++s) {
             const int i = tid + s * TT;
             if (i < m) {
                 double e = 0.0;
-                if constexpr (WIDE) {
-                    e = gather_max<K>(rg[s], spr[s]);
-                } else {
 #pragma unroll
-                    for (int k = 0; k < K; ++k) e = vmax(fabs(lds_at(rg[s][k])), e);
-                }
+                for (int k = 0; k < K; ++k) e = vmax(fabs(lds_at(rg[s][k])), e);
                 Et[i] = 1.0 / sqrt(limit_scaling(e));
-                er[s] = Et[i];
             }
         }
         __syncthreads();
@@ -184,77 +124,27 @@ __device__ __forceinline__ void setup_r_body(const KParams& p, const long b, con
         for (int s = 0; s < PS; ++s) {
             const int v = tid + s * TT;
             if (v < nnzP) {
-                const double x = (WIDE ? pv[s] : Pv[v]) * Dt[pr[s]];
+                const double x = Pv[v] * Dt[pr[s]];
                 Pv[v] = x * Dt[pcol[s]];
-                if constexpr (WIDE) pv[s] = x * Dt[pcol[s]];
             }
         }
 #pragma unroll
         for (int s = 0; s < AS; ++s) {
             const int e = tid + s * TT;
             if (e < nnzA) {
-                const double x = (WIDE ? av[s] : Ac[e]) * Et[ar[s]];
+                const double x = Ac[e] * Et[ar[s]];
                 Ac[e] = x * Dt[ac[s]];
-                if constexpr (WIDE) av[s] = x * Dt[ac[s]];
             }
         }
         if (pc < npad) {
-            const double dt = WIDE ? dr : Dt[pc];
+            const double dt = Dt[pc];
             qv *= dt;
             Dv *= dt;
         }
 #pragma unroll
         for (int s = 0; s < RS; ++s)
-            if (tid + s * TT < m) Ev[s] *= WIDE ? er[s] : Et[tid + s * TT];
+            if (tid + s * TT < m) Ev[s] *= Et[tid + s * TT];
         __syncthreads();
-        if constexpr (WIDE) {
-            // the cost scaling with one LDS round: only the waves holding columns reduce (the
-            // others' terms are zeros: +0 leaves the sum as it is, and the maximum takes
-            // cmax(., 0) per such wave as block_max's chain does), and only the waves that
-            // use c_t (columns, P values) read the result -- block_sum / block_max's values
-            // and order exactly
-            constexpr int NW = TT / 64;
-            const int wid = tid >> 6, lane = tid & 63;
-            const int nwc = (npad + 63) >> 6, nwr = max(nwc, (nnzP + 63) >> 6);
-            if (wid < nwc) {
-                double d1 = 0.0, mq = 0.0;
-                if (colv) {
-                    d1 = gather_max<KP>(pg, spp);
-                    mq = fabs(qv);
-                }
-                const double su = wave_sum(d1), mx = wave_max(mq);
-                if (lane == 0) {
-                    red[wid] = su;
-                    red[NW + wid] = mx;
-                }
-            }
-            __syncthreads();
-            if (wid < nwr) {
-                double su = red[0], mx = red[NW];
-#pragma unroll
-                for (int w = 1; w < NW; ++w) {
-                    if (w < nwc) {
-                        su += red[w];
-                        mx = cmax(mx, red[NW + w]);
-                    } else {
-                        mx = cmax(mx, 0.0);
-                    }
-                }
-                double ct = su / (double)n;
-                ct = limit_scaling(cmax(ct, limit_scaling(mx)));
-                ct = 1.0 / ct;
-#pragma unroll
-                for (int s = 0; s < PS; ++s)
-                    if (tid + s * TT < nnzP) {
-                        pv[s] *= ct;
-                        Pv[tid + s * TT] = pv[s];
-                    }
-                qv *= ct;
-                c *= ct;
-            }
-            __syncthreads();
-            continue;
-        }
         // cost normalisation: mean column inf-norm of P vs ||q||_inf
         double acc[1] = {0.0}, mq[1] = {0.0};
         if (colv) {

@@ -134,6 +134,8 @@ def lib():
     L.mpcqp_update_device.argtypes = [vp, vp, vp, vp, vp]
     L.mpcqp_setup_solve_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.mpcqp_warm_start_device.argtypes = [vp, vp, vp, vp]
+    L.mpcqp_setup_warm_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.mpcqp_setup_warm_fused.argtypes = [vp]
     L.mpcqp_solve_device.argtypes = [vp, vp, vp, vp, vp, vp]
     L.mpcqp_synchronize.argtypes = [vp]
     L.mpcqp_set_shared_matrices.argtypes = [vp, C.c_int32]
@@ -609,6 +611,17 @@ class DeviceBatch:
 
     def warm_start(self, x=None, y=None, stream=None):
         _check(lib().mpcqp_warm_start_device(self._h.ptr, self._ptr(x), self._ptr(y), stream), "warm_start_device")
+
+    def setup_warm(self, Px, Ax, q, l, u, x=None, y=None, stream=None):
+        """setup(Px, Ax, q, l, u) then warm_start(x, y) -- one fused kernel where the wide batch
+        setup applies (mpcqp_setup_warm_device; setup_warm_fused()), identical results."""
+        self._shared(Px, Ax)
+        _check(lib().mpcqp_setup_warm_device(self._h.ptr, self._ptr(Px), self._ptr(Ax), self._ptr(q), self._ptr(l),
+                                             self._ptr(u), self._ptr(x), self._ptr(y), stream), "setup_warm_device")
+
+    def setup_warm_fused(self):
+        """1 when setup_warm runs as one kernel for this handle's plan (mpcqp_setup_warm_fused)."""
+        return int(lib().mpcqp_setup_warm_fused(self._h.ptr))
 
     def solve(self, x=None, y=None, status=None, iters=None, stream=None):
         _check(lib().mpcqp_solve_device(self._h.ptr, self._ptr(x), self._ptr(y), self._ptr(status),

@@ -1578,3 +1578,57 @@ def test_long_horizon_middle_block_in_place(monkeypatch):
             same = r.iter == it
             du = np.array([np.abs(r.x[k, b["u_block"]] - ro[k].x[b["u_block"]]).max() for k in range(len(ro))])
             assert np.all(du[same] < U_TOL), (step, du[same].max())
+
+
+@pytest.mark.gpu
+def test_wide_setup_forms_and_fused_warm_start_agree(monkeypatch):
+    """The wide batch setup (setup_wide.h): its 512-thread form (two instances per CU, batches of
+    512 or more) and its 1024-thread form (MPCQP_SETUP_FULL=1), each as setup() + warm_start()
+    and fused as setup_warm() (mpcqp_setup_warm_device: one kernel), give the same cfg-5 solve
+    bit for bit -- with x0 and y0, and with x0 alone (y stays zero as warm_start leaves it)."""
+    import torch
+    from osqp_amd import DeviceBatch, _drop_common_zeros
+    from osqp_amd.mpc_device import warm_shift
+    B = 640
+    b = mpc.make_batch(5, B=B, seed=41)
+    P, Px = _drop_common_zeros(b["P"], b["Px"])
+    A, Ax = _drop_common_zeros(b["A"], b["Ax"])
+    s = {k: v for k, v in b["settings"].items() if k != "verbose"}
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    dPx, dAx, dq, dl, du = (t(a) for a in (Px, Ax, b["q"], b["l"], b["u"]))
+
+    def outs():
+        return (torch.empty((B, b["n"]), dtype=torch.float64, device=dev),
+                torch.empty((B, b["m"]), dtype=torch.float64, device=dev),
+                torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev))
+
+    h0 = DeviceBatch(P, A, B, device=0, **s)
+    o = outs()
+    h0.setup(dPx, dAx, dq, dl, du)
+    h0.solve(*o)
+    h0.synchronize()
+    xs, ys = warm_shift(b["N"], 8, 2, o[0], o[1])
+    torch.cuda.synchronize()
+    for y0 in (ys, None):
+        runs = []
+        for full in ("0", "1"):
+            monkeypatch.setenv("MPCQP_SETUP_FULL", full)
+            for fused in (False, True):
+                h = DeviceBatch(P, A, B, device=0, **s)
+                assert h.setup_warm_fused() == 1
+                o = outs()
+                if fused:
+                    h.setup_warm(dPx, dAx, dq, dl, du, xs, y0)
+                else:
+                    h.setup(dPx, dAx, dq, dl, du)
+                    h.warm_start(xs, y0)
+                h.solve(*o)
+                h.synchronize()
+                runs.append([v.cpu().numpy() for v in o])
+        monkeypatch.delenv("MPCQP_SETUP_FULL")
+        for r in runs[1:]:
+            for a, c in zip(runs[0], r):
+                assert np.array_equal(a.view(np.int64) if a.dtype == np.float64 else a,
+                                      c.view(np.int64) if c.dtype == np.float64 else c)
+        assert (runs[0][2] == 1).mean() > 0.99

@@ -52,5 +52,18 @@ for tag in ("cold", "warm"):
     h.synchronize()
     out.update({f"{tag}_x": x.cpu().numpy(), f"{tag}_y": y.cpu().numpy(), f"{tag}_st": st.cpu().numpy(),
                 f"{tag}_it": it.cpu().numpy()})
+if cfg == 5:  # setup + warm start from the cold solution (fused where the build has it)
+    h2 = DeviceBatch(P, A, B, device=0, **s)
+    o = [torch.empty((B, b["n"]), dtype=torch.float64, device=dev), torch.empty((B, b["m"]), dtype=torch.float64, device=dev),
+         torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev)]
+    x0, y0 = (torch.from_numpy(out[k]).to(dev) for k in ("cold_x", "cold_y"))
+    if hasattr(h2, "setup_warm") and os.environ.get("LCHAIN_FUSED_WARM", "1") == "1":
+        h2.setup_warm(dPx, dAx, dq * 1.01, dl, du, x0, y0)
+    else:
+        h2.setup(dPx, dAx, dq * 1.01, dl, du)
+        h2.warm_start(x0, y0)
+    h2.solve(*o)
+    h2.synchronize()
+    out.update({f"sw_{k}": v.cpu().numpy() for k, v in zip(("x", "y", "st", "it"), o)})
 np.savez(sys.argv[1], **out)
 print("saved", sys.argv[1], "solved", float((out["cold_st"] == 1).mean()), "iters", out["cold_it"].mean())
