@@ -292,7 +292,7 @@ int upload_plan(const Plan& pl, Shard& s) {
         &pl.pad_var, &pl.acsc_ptr, &pl.acsc_row, &pl.acsc_v, &pl.acsr_ptr, &pl.acsr_col, &pl.acsr_v,
         &pl.psym_ptr, &pl.psym_col, &pl.psym_v, &pl.p_r, &pl.p_c, &pl.a_r, &pl.a_c,
         &pl.asm_blk_ptr, &pl.asm_tgt, &pl.tterm, &pl.acsr_pos, &pl.gcol, &pl.grow, &pl.gpsym, &pl.toff, &pl.bsize, &pl.tcnt,
-        &pl.eown, &pl.etterm};
+        &pl.eown, &pl.etterm, &pl.wide_cg, &pl.wide_pg, &pl.wide_rg, &pl.wide_as, &pl.wide_ps, &pl.csc_pos};
     std::vector<size_t> offs;
     size_t total = 0;
     for (auto* v : parts) {
@@ -317,7 +317,8 @@ int upload_plan(const Plan& pl, Shard& s) {
                          &s.kp.p_r, &s.kp.p_c, &s.kp.a_r, &s.kp.a_c, &s.kp.asm_blk_ptr, &s.kp.asm_tgt,
                          &s.kp.tterm, &s.kp.acsr_pos,
                          &s.kp.gcol, &s.kp.grow, &s.kp.gpsym, &s.kp.toff, &s.kp.bsize, &s.kp.tcnt,
-                         &s.kp.eown, &s.kp.etterm};
+                         &s.kp.eown, &s.kp.etterm, &s.kp.wcg, &s.kp.wpg, &s.kp.wrg, &s.kp.was, &s.kp.wps,
+                         &s.kp.csc_pos};
     for (size_t i = 0; i < parts.size(); ++i) *dst[i] = s.dplan + offs[i];
     return 0;
 }

@@ -98,6 +98,8 @@ struct KParams {
     int qpersist;
     int persist;
     long qn;
+    // the wide batch setup's plan lists (plan.h wide_*, csc_pos)
+    const int *wcg, *wpg, *wrg, *was, *wps, *csc_pos;
 };
 constexpr long kOrderFuseMax = 16384;  // larger batches sort in k_order (1024 threads)
 

@@ -8,6 +8,41 @@
 
 namespace mpcqp {
 
+// The wide batch setup's register lists (setup_wide.h), built here once per plan: its LDS
+// byte addresses (Pv at 0, Ac, Dt, Et after it, lds_setup_wide_bytes's layout), 16 bits each,
+// two to a word, so the kernel's prologue loads each word coalesced instead of chasing
+// gcol / grow / gpsym / acsc_v / a_c per instance (with csc_pos, the A values load in the
+// user's order, coalesced, and land at their padded-CSC places in LDS).  Built where that kernel applies
+// (kernels.hip::setup_rw_fits: its LDS stays below 64 KiB), empty elsewhere.
+static void build_wide_lists(Plan& pl) {
+    pl.wide_cg.clear(); pl.wide_pg.clear(); pl.wide_rg.clear(); pl.wide_as.clear(); pl.wide_ps.clear();
+    const int m = pl.m, npad = pl.npad, nnzA = pl.nnzA, nnzP = pl.nnzP;
+    if (npad > 1024 || m > 1024 || pl.p_k > 4 || pl.gather_k > 8 || nnzA > 3 * 1024 || nnzP > 1024) return;
+    const unsigned abase = 8u * (unsigned)(nnzP + 1), dbase = abase + 8u * (unsigned)(nnzA + 1),
+                   ebase = dbase + 8u * (unsigned)npad;
+    auto pk = [](unsigned lo, unsigned hi) { return (int)(lo | hi << 16); };
+    auto aad = [&](int g) { return abase + 8u * ((unsigned)g & 0xFFFFu); };
+    pl.wide_cg.resize((size_t)4 * npad);
+    pl.wide_pg.resize((size_t)2 * npad);
+    for (int pc = 0; pc < npad; ++pc) {
+        for (int k = 0; k < 4; ++k)
+            pl.wide_cg[(size_t)k * npad + pc] = pk(aad(pl.gcol[(size_t)(2 * k) * npad + pc]),
+                                                   aad(pl.gcol[(size_t)(2 * k + 1) * npad + pc]));
+        for (int k = 0; k < 2; ++k)
+            pl.wide_pg[(size_t)k * npad + pc] = pk(8u * ((unsigned)pl.gpsym[(size_t)(2 * k) * npad + pc] & 0xFFFFu),
+                                                   8u * ((unsigned)pl.gpsym[(size_t)(2 * k + 1) * npad + pc] & 0xFFFFu));
+    }
+    pl.wide_rg.resize((size_t)4 * m);
+    for (int r = 0; r < m; ++r)
+        for (int k = 0; k < 4; ++k)
+            pl.wide_rg[(size_t)k * m + r] = pk(aad(pl.grow[(size_t)(2 * k) * m + r]), aad(pl.grow[(size_t)(2 * k + 1) * m + r]));
+    pl.wide_as.resize(nnzA);
+    for (int e = 0; e < nnzA; ++e)
+        pl.wide_as[e] = pk(ebase + 8u * (unsigned)pl.acsc_row[e], dbase + 8u * (unsigned)pl.a_c[pl.acsc_v[e]]);
+    pl.wide_ps.resize(nnzP);
+    for (int v = 0; v < nnzP; ++v) pl.wide_ps[v] = pk(dbase + 8u * (unsigned)pl.p_r[v], dbase + 8u * (unsigned)pl.p_c[v]);
+}
+
 namespace {
 
 struct Graph {
@@ -447,6 +482,7 @@ std::string build_plan(int n, int m, const int32_t* Pp, const int32_t* Pi, const
     for (int r = 0; r < m; ++r)
         for (int e = pl.acsr_ptr[r], k = 0; e < pl.acsr_ptr[r + 1]; ++e, ++k)
             pl.grow[(size_t)k * m + r] = pl.acsr_pos[e] | (pl.acsr_col[e] << 16);
+    build_wide_lists(pl);
     return "";
 }
 

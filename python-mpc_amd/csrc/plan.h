@@ -59,6 +59,11 @@ struct Plan {
     std::vector<int> gcol, grow;
     int p_k = 0;                  // max nonzeros per column of the symmetric P
     std::vector<int> gpsym;       // [kGS][npad] P by padded column: (Pv index) | (padded column << 16)
+    // the wide batch setup's lists (plan.cpp::build_wide_lists; empty where it does not apply):
+    // LDS byte addresses two to a word -- [4][npad] A and [2][npad] P by column, [4][m] A by
+    // row, [nnzA] (Et row | Dt column) per padded-CSC value, [nnzP] (Dt row | Dt column) per P
+    // value -- and csc_pos, user A value index -> padded-CSC position
+    std::vector<int> wide_cg, wide_pg, wide_rg, wide_as, wide_ps;
     int amax = 0;                 // max over k of (last nonzero local row of E_k) + 1: F_k rows / H_{k-1} cols
     // the other side of the coupling: the columns of E_{k+1} (variables of block k that
     // couple to block k+1, its last BFS level) lie in [toff[k], toff[k] + bmax)

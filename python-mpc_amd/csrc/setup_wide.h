@@ -7,7 +7,8 @@
 // A thread holds CS padded columns (pc = tid + c * TT), RS rows (tid + s * TT), AS values of A
 // (padded-CSC order, e = tid + s * TT) and PS values of P, with every address the ten passes
 // chase in registers (setup_r.h's register lists, here as 16-bit LDS addresses two to a
-// register: the workgroup's LDS stays below 64 KiB) and, unlike setup_r_body, its own values
+// register, built once per plan: plan.cpp::build_wide_lists; the workgroup's LDS stays below
+// 64 KiB) and, unlike setup_r_body, its own values
 // too: LDS keeps only the copies the gathers read.  The gathers read no further
 // than the longest list of the wave (a ballot in the prologue), and the cost scaling's sum and
 // maximum take one LDS round among the waves that hold columns.
@@ -38,7 +39,6 @@ __host__ __device__ inline size_t lds_setup_wide_bytes(int nnzP, int nnzA, int n
 
 // slot k of a packed list: 16-bit LDS byte addresses, two to a register
 __device__ __forceinline__ unsigned slot(const unsigned* g, int k) { return k & 1 ? g[k >> 1] >> 16 : g[k >> 1] & 0xFFFFu; }
-__device__ __forceinline__ unsigned pack2(unsigned lo, unsigned hi) { return lo | hi << 16; }
 
 // The wave's span of a gather list of K slots, padded at its end with `pad` (the zero slot):
 // 0 = at most one entry in every lane, 1 = at most (K + 1) / 2, 2 = K.  Uniform (a ballot),
@@ -87,7 +87,11 @@ __device__ __forceinline__ void setup_wide_body(const KParams& p, const long b, 
     const unsigned pbase = lds_addr(Pv), abase = lds_addr(Ac);
     const unsigned apad = abase + 8u * (unsigned)nnzA, ppad = pbase + 8u * (unsigned)nnzP;
 
+    static_assert(K == 8 && KP == 4, "the plan's wide lists (plan.cpp::build_wide_lists) hold 8 + 4 slots");
     constexpr int K2 = (K + 1) / 2, KP2 = (KP + 1) / 2;
+    // the plan's packed lists are LDS offsets from the dynamic LDS's start: add its address to
+    // both halves (no carry: the setup's LDS stays below 64 KiB)
+    const unsigned sb = lds_addr(sm) * 0x10001u, apad2 = apad * 0x10001u, ppad2 = ppad * 0x10001u;
     bool colv[CS];
     unsigned cg[CS][K2], pg[CS][KP2], rg[RS][K2];
     int spc[CS], spp[CS], spr[RS];
@@ -96,26 +100,11 @@ __device__ __forceinline__ void setup_wide_body(const KParams& p, const long b, 
     for (int c = 0; c < CS; ++c) {
         const int pc = tid + c * TT;
         const int j = pc < npad ? p.pad_var[pc] : -1;
-        colv[c] = j >= 0;
+        colv[c] = j >= 0;  // (the padding columns' lists are all pads)
 #pragma unroll
-        for (int k = 0; k < K2; ++k) {
-            unsigned a[2];
+        for (int k = 0; k < K2; ++k) cg[c][k] = pc < npad ? (unsigned)p.wcg[(long)k * npad + pc] + sb : apad2;
 #pragma unroll
-            for (int h = 0; h < 2; ++h)
-                a[h] = colv[c] && 2 * k + h < K ? abase + 8u * ((unsigned)p.gcol[(long)(2 * k + h) * npad + pc] & 0xFFFFu)
-                                                : apad;
-            cg[c][k] = pack2(a[0], a[1]);
-        }
-#pragma unroll
-        for (int k = 0; k < KP2; ++k) {
-            unsigned a[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-                a[h] = colv[c] && 2 * k + h < KP
-                           ? pbase + 8u * ((unsigned)p.gpsym[(long)(2 * k + h) * npad + pc] & 0xFFFFu)
-                           : ppad;
-            pg[c][k] = pack2(a[0], a[1]);
-        }
+        for (int k = 0; k < KP2; ++k) pg[c][k] = pc < npad ? (unsigned)p.wpg[(long)k * npad + pc] + sb : ppad2;
         spc[c] = wave_span<K>(cg[c], apad);
         spp[c] = wave_span<KP>(pg[c], ppad);
         qv[c] = colv[c] ? q_in[b * n + j] : 0.0;
@@ -125,35 +114,26 @@ __device__ __forceinline__ void setup_wide_body(const KParams& p, const long b, 
     for (int s = 0; s < RS; ++s) {
         const int i = tid + s * TT;
 #pragma unroll
-        for (int k = 0; k < K2; ++k) {
-            unsigned a[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-                a[h] = i < m && 2 * k + h < K ? abase + 8u * ((unsigned)p.grow[(long)(2 * k + h) * m + i] & 0xFFFFu)
-                                              : apad;
-            rg[s][k] = pack2(a[0], a[1]);
-        }
+        for (int k = 0; k < K2; ++k) rg[s][k] = i < m ? (unsigned)p.wrg[(long)k * m + i] + sb : apad2;
         spr[s] = wave_span<K>(rg[s], apad);
     }
     const long bm = p.mat_shared ? 0 : b;  // LTI batches: one P, A for every instance
-    // a value's two scalings: (Et[row] | Dt[col] << 16) for A, (Dt[row] | Dt[col] << 16) for P
-    const unsigned dbase = lds_addr(Dt), ebase = lds_addr(Et);
+    // a value's two scalings: (Et[row] | Dt[col] << 16) for A, (Dt[row] | Dt[col] << 16) for P;
+    // A loads in the user's order (coalesced) into its padded-CSC place (csc_pos), and the
+    // thread's own values come back from LDS after the barrier below
     unsigned as2[AS], ps2[PS];
     double av[AS], pv[PS];
 #pragma unroll
     for (int s = 0; s < AS; ++s) {
         const int e = tid + s * TT;
-        const bool in = e < nnzA;
-        const int v = in ? p.acsc_v[e] : 0;
-        as2[s] = in ? pack2(ebase + 8u * (unsigned)p.acsc_row[e], dbase + 8u * (unsigned)p.a_c[v]) : 0u;
-        av[s] = in ? Ax_in[bm * nnzA + v] : 0.0;
-        if (in) Ac[e] = av[s];
+        as2[s] = e < nnzA ? (unsigned)p.was[e] + sb : 0u;
+        if (e < nnzA) Ac[p.csc_pos[e]] = Ax_in[bm * nnzA + e];
     }
 #pragma unroll
     for (int s = 0; s < PS; ++s) {
         const int v = tid + s * TT;
         const bool in = v < nnzP;
-        ps2[s] = in ? pack2(dbase + 8u * (unsigned)p.p_r[v], dbase + 8u * (unsigned)p.p_c[v]) : 0u;
+        ps2[s] = in ? (unsigned)p.wps[v] + sb : 0u;
         pv[s] = in ? Px_in[bm * nnzP + v] : 0.0;
         if (in) Pv[v] = pv[s];
     }
@@ -166,6 +146,8 @@ __device__ __forceinline__ void setup_wide_body(const KParams& p, const long b, 
     const int nwc = (npad + 63) >> 6;
     const bool use_ct = wid * 64 < max(npad, nnzP);
     __syncthreads();
+#pragma unroll
+    for (int s = 0; s < AS; ++s) av[s] = tid + s * TT < nnzA ? Ac[tid + s * TT] : 0.0;
 
     for (int it = 0; it < p.scaling; ++it) {
         // (the packed lists opaque per pass: unpacked out of the loop they would take a
