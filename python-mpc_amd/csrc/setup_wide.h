@@ -38,7 +38,12 @@ __host__ __device__ inline size_t lds_setup_wide_bytes(int nnzP, int nnzA, int n
 }
 
 // slot k of a packed list: 16-bit LDS byte addresses, two to a register
-__device__ __forceinline__ unsigned slot(const unsigned* g, int k) { return k & 1 ? g[k >> 1] >> 16 : g[k >> 1] & 0xFFFFu; }
+// (sh = 16 and mk = 0xFFFF come through an empty asm once per pass in the loop: the unpacking
+// then cannot move out of the loop -- hoisted, it would take a register per address again --
+// while the packed words themselves stay untouched, so no spilled copy is rewritten per pass)
+__device__ __forceinline__ unsigned slot(const unsigned* g, int k, unsigned sh = 16, unsigned mk = 0xFFFFu) {
+    return k & 1 ? g[k >> 1] >> sh : g[k >> 1] & mk;
+}
 
 // The wave's span of a gather list of K slots, padded at its end with `pad` (the zero slot):
 // 0 = at most one entry in every lane, 1 = at most (K + 1) / 2, 2 = K.  Uniform (a ballot),
@@ -54,16 +59,16 @@ __device__ __forceinline__ int wave_span(const unsigned* g, unsigned pad) {
     return gth ? 2 : gt1 ? 1 : 0;
 }
 template <int K>
-__device__ __forceinline__ double gather_max(const unsigned* g, int span) {
+__device__ __forceinline__ double gather_max(const unsigned* g, int span, unsigned sh, unsigned mk) {
     double d = 0.0;
     if (span == 0) {
-        d = vmax(fabs(lds_at(slot(g, 0))), d);
+        d = vmax(fabs(lds_at(slot(g, 0, sh, mk))), d);
     } else if (span == 1) {
 #pragma unroll
-        for (int k = 0; k < (K + 1) / 2; ++k) d = vmax(fabs(lds_at(slot(g, k))), d);
+        for (int k = 0; k < (K + 1) / 2; ++k) d = vmax(fabs(lds_at(slot(g, k, sh, mk))), d);
     } else {
 #pragma unroll
-        for (int k = 0; k < K; ++k) d = vmax(fabs(lds_at(slot(g, k))), d);
+        for (int k = 0; k < K; ++k) d = vmax(fabs(lds_at(slot(g, k, sh, mk))), d);
     }
     return d;
 }
@@ -76,6 +81,7 @@ __device__ __forceinline__ void setup_wide_body(const KParams& p, const long b, 
                                                 const double* __restrict__ y0 = nullptr) {
     static_assert(!(WARM && KEEP), "a matrix update keeps its iterates");
     constexpr int NW = TT / 64, NV = CS * NW;  // waves; 64-column groups ("virtual waves")
+    constexpr bool AVR = TT > 512;  // the thread's A values in registers (the 512-thread form: LDS)
     const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
     const int n = p.n, m = p.m, npad = p.npad, nnzP = p.nnzP, nnzA = p.nnzA;
     double* Pv = sm;             // [nnzP + 1]  user order, Pv[nnzP] = 0
@@ -147,26 +153,11 @@ __device__ __forceinline__ void setup_wide_body(const KParams& p, const long b, 
     const bool use_ct = wid * 64 < max(npad, nnzP);
     __syncthreads();
 #pragma unroll
-    for (int s = 0; s < AS; ++s) av[s] = tid + s * TT < nnzA ? Ac[tid + s * TT] : 0.0;
+    for (int s = 0; s < AS; ++s) av[s] = AVR && tid + s * TT < nnzA ? Ac[tid + s * TT] : 0.0;
 
     for (int it = 0; it < p.scaling; ++it) {
-        // (the packed lists opaque per pass: unpacked out of the loop they would take a
-        // register per address again)
-#pragma unroll
-        for (int c = 0; c < CS; ++c) {
-#pragma unroll
-            for (int k = 0; k < K2; ++k) asm volatile("" : "+v"(cg[c][k]));
-#pragma unroll
-            for (int k = 0; k < KP2; ++k) asm volatile("" : "+v"(pg[c][k]));
-        }
-#pragma unroll
-        for (int s = 0; s < RS; ++s)
-#pragma unroll
-            for (int k = 0; k < K2; ++k) asm volatile("" : "+v"(rg[s][k]));
-#pragma unroll
-        for (int s = 0; s < AS; ++s) asm volatile("" : "+v"(as2[s]));
-#pragma unroll
-        for (int s = 0; s < PS; ++s) asm volatile("" : "+v"(ps2[s]));
+        unsigned sh = 16, mk = 0xFFFFu;  // (opaque per pass: see slot)
+        asm volatile("" : "+s"(sh), "+s"(mk));
         // compute_inf_norm_cols_KKT / rows + limit_scaling + sqrt + reciprocal
 #pragma unroll
         for (int c = 0; c < CS; ++c) {
@@ -174,8 +165,8 @@ __device__ __forceinline__ void setup_wide_body(const KParams& p, const long b, 
             if (pc < npad) {
                 double d = 1.0;
                 if (colv[c]) {
-                    const double d1 = gather_max<KP>(pg[c], spp[c]);
-                    const double d2 = gather_max<K>(cg[c], spc[c]);
+                    const double d1 = gather_max<KP>(pg[c], spp[c], sh, mk);
+                    const double d2 = gather_max<K>(cg[c], spc[c], sh, mk);
                     d = 1.0 / sqrt(limit_scaling(vmax(d1, d2)));
                 }
                 Dt[pc] = d;
@@ -185,7 +176,7 @@ __device__ __forceinline__ void setup_wide_body(const KParams& p, const long b, 
         for (int s = 0; s < RS; ++s) {
             const int i = tid + s * TT;
             if (i < m) {
-                Et[i] = 1.0 / sqrt(limit_scaling(gather_max<K>(rg[s], spr[s])));
+                Et[i] = 1.0 / sqrt(limit_scaling(gather_max<K>(rg[s], spr[s], sh, mk)));
             }
         }
         __syncthreads();
@@ -194,8 +185,8 @@ __device__ __forceinline__ void setup_wide_body(const KParams& p, const long b, 
         for (int s = 0; s < PS; ++s) {
             const int v = tid + s * TT;
             if (v < nnzP) {
-                const double x = pv[s] * lds_at(ps2[s] & 0xFFFFu);
-                pv[s] = x * lds_at(ps2[s] >> 16);
+                const double x = pv[s] * lds_at(ps2[s] & mk);
+                pv[s] = x * lds_at(ps2[s] >> sh);
                 Pv[v] = pv[s];
             }
         }
@@ -203,9 +194,10 @@ __device__ __forceinline__ void setup_wide_body(const KParams& p, const long b, 
         for (int s = 0; s < AS; ++s) {
             const int e = tid + s * TT;
             if (e < nnzA) {
-                const double x = av[s] * lds_at(as2[s] & 0xFFFFu);
-                av[s] = x * lds_at(as2[s] >> 16);
-                Ac[e] = av[s];
+                const double x = (AVR ? av[s] : Ac[e]) * lds_at(as2[s] & mk);
+                const double y = x * lds_at(as2[s] >> sh);
+                Ac[e] = y;
+                if (AVR) av[s] = y;
             }
         }
 #pragma unroll
@@ -226,7 +218,7 @@ __device__ __forceinline__ void setup_wide_body(const KParams& p, const long b, 
         for (int c = 0; c < CS; ++c) {
             const int vw = c * NW + wid;
             if (vw < nwc) {  // (uniform: full-wave DPP)
-                const double d1 = colv[c] ? gather_max<KP>(pg[c], spp[c]) : 0.0;
+                const double d1 = colv[c] ? gather_max<KP>(pg[c], spp[c], sh, mk) : 0.0;
                 const double su = wave_sum(d1), mx = wave_max(colv[c] ? fabs(qv[c]) : 0.0);
                 if (lane == 0) {
                     red[vw] = su;
@@ -297,7 +289,7 @@ __device__ __forceinline__ void setup_wide_body(const KParams& p, const long b, 
         if (tid + s * TT < nnzP) p.Px[b * nnzP + tid + s * TT] = pv[s];
 #pragma unroll
     for (int s = 0; s < AS; ++s)
-        if (tid + s * TT < nnzA) p.Ax[b * nnzA + tid + s * TT] = av[s];
+        if (tid + s * TT < nnzA) p.Ax[b * nnzA + tid + s * TT] = AVR ? av[s] : Ac[tid + s * TT];
 #pragma unroll
     for (int c = 0; c < CS; ++c) {
         const int pc = tid + c * TT;
