@@ -68,3 +68,21 @@ def test_hot_kernel_shape_is_pinned(shapes, key):
     if "step_readlane" in want:
         assert got["step_loops"] >= 8, got  # the forward / backward step runs of the sweep were found
         assert got["step_readlane"] == want["step_readlane"] and got["step_scratch"] == want["step_scratch"], got
+
+
+@pytest.mark.skipif(not isa_shape.tools_present() or not os.path.exists(LIB), reason="no llvm tools or library")
+def test_wide_setup_has_no_spills():
+    """The wide batch setup (setup_wide.h, round 6): every instantiation of k_setup_wide keeps its
+    registers -- the 512-thread form at most 128 VGPRs (two instances per CU) with no spilled
+    VGPR (8 spilled VGPRs cost 4.5 % of its time: profiles/r6/setup_ab.txt item 8), the 1024-thread
+    form at most 128 (one workgroup of 16 waves per CU)."""
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        md = {}
+        for co in isa_shape.code_objects(LIB, d):
+            md.update({k: v for k, v in isa_shape.metadata(co).items() if "k_setup_wide" in k})
+    assert len(md) == 6, sorted(md)
+    for name, v in md.items():
+        assert v["vgpr_spill_count"] == 0, (name, v)
+        assert v["sgpr_spill_count"] <= 32, (name, v)  # (SGPR spills go to VGPR lanes: 26 in the 512 form)
+        assert v["vgpr_count"] + v["agpr_count"] <= 128, (name, v)
