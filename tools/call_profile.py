@@ -37,7 +37,8 @@ def call():
 for _ in range(5):
     call()
 ts = np.array([call()[:3] for _ in range(reps)])
-print("median ms: OSQP() %.3f setup %.3f solve %.3f total %.3f" % tuple(np.median(ts, 0).tolist() + [np.median(ts.sum(1))]))
+print("median ms: OSQP() %.3f setup %.3f solve %.3f total %.3f"
+      % tuple(1e3 * np.array(np.median(ts, 0).tolist() + [np.median(ts.sum(1))])))
 pr = cProfile.Profile()
 pr.enable()
 for _ in range(reps):
