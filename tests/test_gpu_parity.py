@@ -1632,3 +1632,36 @@ def test_wide_setup_forms_and_fused_warm_start_agree(monkeypatch):
                 assert np.array_equal(a.view(np.int64) if a.dtype == np.float64 else a,
                                       c.view(np.int64) if c.dtype == np.float64 else c)
         assert (runs[0][2] == 1).mean() > 0.99
+
+
+@pytest.mark.gpu
+def test_wide_setup_forms_agree_through_matrix_updates(monkeypatch):
+    """A matrix update rescales through the wide setup's KEEP form (launch_update_mat): on a
+    cfg-5 batch of 512 or more (its 512-thread form) and with MPCQP_SETUP_FULL=1 (the
+    1024-thread form) the setup, a P update and an A update by index each solve to the same
+    result bit for bit (test_matrix_updates_match_oracle holds the 1024-thread form to the
+    oracle at B = 12)."""
+    B = 520
+    b = mpc.make_batch(5, B=B, seed=9)
+    idx = np.concatenate([np.arange(0, b["A"].nnz, 3), [0]])
+    An = b["Ax"][:, idx] * np.random.default_rng(3).uniform(0.99, 1.01, (B, idx.size))
+    runs = []
+    for full in ("0", "1"):
+        monkeypatch.setenv("MPCQP_SETUP_FULL", full)
+        dev = OSQPBatch()
+        dev.setup(b["P"], b["q"], b["A"], b["l"], b["u"], Px=b["Px"], Ax=b["Ax"], warm_start=False)
+        out = []
+        for step in range(3):
+            if step == 1:
+                dev.update(Px=b["Px"] * 1.5)
+            elif step == 2:
+                dev.update(Ax=An, Ax_idx=idx)
+            r = dev.solve()
+            out.append((r.x.copy(), r.y.copy(), np.asarray(r.status_val).copy(), np.asarray(r.iter).copy()))
+        runs.append(out)
+    monkeypatch.delenv("MPCQP_SETUP_FULL")
+    for a, c in zip(*runs):
+        for u, v in zip(a, c):
+            assert np.array_equal(u.view(np.int64) if u.dtype == np.float64 else u,
+                                  v.view(np.int64) if v.dtype == np.float64 else v)
+    assert (runs[0][0][2] == 1).mean() > 0.99
